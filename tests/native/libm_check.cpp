@@ -1,0 +1,88 @@
+// Exhaustive host check: rt_libm.h restatements vs this machine's glibc.
+//   libm_check sincos            all float a in [0, 2*pi)   (AO angle domain, Raytracer.cpp:270-278)
+//   libm_check powf  y1 y2 ...   all float x in [0, 1.0001] for each exponent y (Raytracer.cpp:253)
+//   libm_check powf_random N     N random (x, y) pairs over the whole float range
+// Prints "mismatches=<n> checked=<m>" and the first few mismatches; exit 1 if any.
+#include "../../580-raytracer_amd/csrc/rt_libm.h"
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <atomic>
+#include <thread>
+#include <vector>
+#include <random>
+
+static std::atomic<long> g_bad{0}, g_checked{0};
+static std::atomic<int> g_printed{0};
+
+static void report(const char* what, double in1, double in2, double got, double want) {
+    if (g_printed.fetch_add(1) < 10)
+        std::printf("MISMATCH %s in=(%a, %a) port=%a glibc=%a\n", what, in1, in2, got, want);
+}
+
+template <class F>
+static void parallel(uint64_t n, F f) {
+    unsigned nt = std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("RT_THREADS")) nt = (unsigned)std::atoi(e);
+    if (nt < 1) nt = 1;
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++)
+        th.emplace_back([=] {
+            uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+            f(lo, hi);
+        });
+    for (auto& x : th) x.join();
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) return 2;
+    if (!std::strcmp(argv[1], "sincos")) {
+        uint32_t hi = rt_f2u(6.2831855f);   // first float >= 2*pi (float)
+        parallel(hi, [](uint64_t lo, uint64_t hi) {
+            long bad = 0;
+            for (uint64_t u = lo; u < hi; u++) {
+                double a = (double)rt_u2f((uint32_t)u);
+                double s0, c0, s1, c1;
+                sincos(a, &s0, &c0);
+                rt_glibc_sincos(a, &s1, &c1);
+                if (rt_d2u(s0) != rt_d2u(s1)) { bad++; report("sin", a, 0, s1, s0); }
+                if (rt_d2u(c0) != rt_d2u(c1)) { bad++; report("cos", a, 0, c1, c0); }
+            }
+            g_bad += bad; g_checked += (long)(hi - lo);
+        });
+    } else if (!std::strcmp(argv[1], "powf")) {
+        for (int i = 2; i < argc; i++) {
+            float y = std::strtof(argv[i], nullptr);
+            uint32_t hi = rt_f2u(1.0001f) + 1;
+            parallel(hi, [y](uint64_t lo, uint64_t hi) {
+                long bad = 0;
+                for (uint64_t u = lo; u < hi; u++) {
+                    float x = rt_u2f((uint32_t)u);
+                    float r0 = powf(x, y), r1 = rt_glibc_powf(x, y);
+                    if (rt_f2u(r0) != rt_f2u(r1)) { bad++; report("powf", x, y, r1, r0); }
+                }
+                g_bad += bad; g_checked += (long)(hi - lo);
+            });
+        }
+    } else if (!std::strcmp(argv[1], "powf_random")) {
+        uint64_t n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 100000000ull;
+        parallel(n, [](uint64_t lo, uint64_t hi) {
+            std::mt19937_64 g(lo * 2654435761ull + 580);
+            long bad = 0;
+            for (uint64_t i = lo; i < hi; i++) {
+                uint64_t r = g();
+                float x = rt_u2f((uint32_t)r), y = rt_u2f((uint32_t)(r >> 32));
+                if (i & 1) y = (float)((int)(r >> 40) % 2000) * 0.5f;   // integer-ish exponents
+                if (i & 2) x = rt_u2f((uint32_t)r & 0x3fffffffu);        // x in [0, 2)
+                float r0 = powf(x, y), r1 = rt_glibc_powf(x, y);
+                bool same = rt_f2u(r0) == rt_f2u(r1) || (r0 != r0 && r1 != r1);
+                if (!same) { bad++; report("powf_random", x, y, r1, r0); }
+            }
+            g_bad += bad; g_checked += (long)(hi - lo);
+        });
+    } else {
+        return 2;
+    }
+    std::printf("mismatches=%ld checked=%ld\n", g_bad.load(), g_checked.load());
+    return g_bad.load() ? 1 : 0;
+}
