@@ -1,0 +1,54 @@
+// raytracer.h — the reference's class surface (Raytracer.h:17-609) for the HIP
+// path: same constructor, LoadSceneJSON / InitializeRenderer / Render /
+// FlushFrameBufferToPPM, same int status codes (Raytracer.h:8-10), same JSON
+// scene format and "Assets/" relative paths (Raytracer.h:15). Render() runs the
+// per-pixel path on the GPU through the rt_gpu_* C ABI (include/rt580.h).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/rt580.h"
+#include "rt_scene.h"
+
+class Raytracer {
+  public:
+    struct Pixel {  // Raytracer.h:373-418 storage layout (int16 r, g, b)
+        short r, g, b;
+    };
+
+    Raytracer(int width, int height);  // Raytracer.cpp:781-788
+    ~Raytracer();
+
+    int LoadSceneJSON(const std::string scenePath);      // Raytracer.cpp:645-779
+    int Render(const std::string outputName);            // Raytracer.cpp:916-935
+    int FlushFrameBufferToPPM(std::string outputName);   // Raytracer.cpp:796-830
+    int InitializeRenderer();                            // Raytracer.cpp:895-915 (private there)
+
+    // Runtime knobs the reference hard-codes (defaults = the reference's values).
+    void SetAssetsRoot(const std::string& root) { mAssetsRoot = root; }
+    int SetDepth(int bounces);                       // Raytracer.h:563 (default 4)
+    int SetAmbientOcclusion(int samples, bool on);   // Raytracer.cpp:317 (128, on)
+    int SetRngEngine(int engine);                    // Raytracer.h:592 (minstd_rand0)
+    int SetRows(int row_begin, int row_end, int row_step = 1);
+    int SetWriteOutput(bool on) { mWriteOutput = on; return RT_SUCCESS; }
+
+    const Pixel* FrameBuffer() const { return mFrameBuffer.data(); }
+    const rt_render_params& Params() const { return mParams; }
+    const rt580::PackedScene& Packed() const { return mPacked; }
+    int LastStats(rt_render_stats& s) const;
+
+  private:
+    int mWidth, mHeight;
+    float mFov = 60.0f;  // Raytracer.cpp:786
+    std::string mAssetsRoot = ".";
+    std::vector<Pixel> mFrameBuffer;
+    rt580::Scene mScene;
+    rt580::PackedScene mPacked;
+    bool mSceneValid = false;
+    bool mUploaded = false;
+    bool mWriteOutput = true;
+    rt_render_params mParams;
+    int mDepth = 4, mAoSamples = 128, mAoOn = 1, mEngine = RT_RNG_MINSTD_RAND0;
+    int mRowBegin = 0, mRowEnd = -1, mRowStep = 1;
+};

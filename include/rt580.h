@@ -1,0 +1,202 @@
+/* rt580.h — C-ABI boundary between the reference's host class surface and the
+ * MI355X ray-trace kernels (POD types only; no C++ or torch types cross it).
+ *
+ * The reference (Xena99/580-Raytracer, "580 Raytracer/") renders inside
+ *   int Raytracer::Render(const std::string outputName)      Raytracer.cpp:916-935
+ * whose per-pixel loop (GenerateRay :832-858 -> Raycast :28-129 -> IntersectScene
+ * :473-526 / CalculateLocalColor :213-267 / CalculateAmbientOcclusion :315-330 /
+ * ComputeFresnel :131-166 / CalculateRefraction :168-203) is replaced by
+ * rt_gpu_render(). The scene that LoadSceneJSON (:645-779) + LoadMesh (:589-643)
+ * build is flattened on the host (reference arithmetic, Raytracer.cpp:528-586,
+ * :348-409, :895-915) and handed over once by rt_gpu_upload_scene().
+ *
+ * Status convention is the reference's (Raytracer.h:8-10):
+ *   RT_SUCCESS 0, RT_FAILURE 1, RT_INVALID_ARG 2.
+ * No function throws or aborts; HIP/RCCL errors map to RT_FAILURE and a message
+ * on stderr (also retrievable with rt_gpu_last_error()).
+ */
+#ifndef RT580_H
+#define RT580_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT580_ABI_VERSION 1
+
+#ifndef RT_SUCCESS
+#define RT_SUCCESS 0
+#define RT_FAILURE 1
+#define RT_INVALID_ARG 2
+#endif
+
+/* Primitive kinds, in the reference's Mesh::Type order (Raytracer.h:477-480). */
+#define RT_PRIM_TRIANGLE 0
+#define RT_PRIM_SPHERE 1
+
+/* Light kinds (Raytracer.h:520-524). */
+#define RT_LIGHT_DIRECTIONAL 0
+#define RT_LIGHT_POINT 1
+#define RT_LIGHT_AMBIENT 2
+
+/* RNG engines for the AO sampler (member mGenerator, Raytracer.h:592). */
+#define RT_RNG_MINSTD_RAND0 0 /* libstdc++ std::default_random_engine, seed 1 */
+#define RT_RNG_MT19937 1      /* MSVC std::default_random_engine, seed 5489  */
+
+/* One primitive in the reference's intersection order (shapes in JSON order,
+ * triangles in mesh-file order, Raytracer.cpp:476-521), world space, with the
+ * ray-invariant part of IntersectTriangle/IntersectSphere precomputed.
+ * 64 bytes; read wave-uniformly by the kernels.
+ *   triangle: p0 = v0, p1 = v1, p2 = v2 (TransformPoint, Raytracer.cpp:353-355),
+ *             nrm = normalize(cross(v1-v0, v2-v0))            (:362-365),
+ *             d = -dot(nrm, v0)                               (:377),
+ *             area = CalcTriangleAreaSigned(v0,v1,v2,nrm)     (:389, :937-942)
+ *   sphere:   p0 = model-matrix translation (GetTranslation, Raytracer.h:212),
+ *             d = radius*radius                               (:423)          */
+typedef struct rt_prim {
+    float p0[3];
+    float d;
+    float p1[3];
+    float area;
+    float p2[3];
+    int32_t kind; /* RT_PRIM_* */
+    float nrm[3];
+    int32_t shape; /* index into the material table (owning shape) */
+} rt_prim;
+
+/* Shading side table, read only for the winning hit (one per primitive). */
+typedef struct rt_prim_shade {
+    float hit_nrm[3]; /* triangle: normalize(nrm) (Raytracer.cpp:402-403); sphere: unused */
+    float vn0[3];     /* object-space vertex normals (Raytracer.cpp:227), triangles only */
+    float vn1[3];
+    float vn2[3];
+    float pad[4];
+} rt_prim_shade;
+
+/* Material of a shape (Raytracer.h:442-463). refractiveIndex is never read from
+ * JSON by the reference and stays 2.5 (Raytracer.h:460). */
+typedef struct rt_material {
+    float cs[3];
+    float ka, kd, ks, kt;
+    float spec_exp; /* "n" */
+    float ior;      /* 2.5 */
+    float pad[3];
+} rt_material;
+
+/* A light in JSON order (Raytracer.cpp:744-771). For directional lights the
+ * host also stores L = normalize(-direction) (Raytracer.cpp:59,65,220-221) and
+ * L2 = normalize(L) (the shadow Ray constructor, Raytracer.h:431-433). */
+typedef struct rt_light {
+    int32_t kind; /* RT_LIGHT_* */
+    float color[3];
+    float intensity;
+    float position[3];
+    float dir[3];    /* normalized to - from */
+    float L[3];      /* directional: normalize(-dir) */
+    float L2[3];     /* directional: normalize(L)    */
+    float pad[1];
+} rt_light;
+
+typedef struct rt_scene_soa {
+    int32_t abi_version; /* RT580_ABI_VERSION */
+    int32_t n_prims;
+    const rt_prim* prims;
+    const rt_prim_shade* shade;
+    int32_t n_materials;
+    const rt_material* materials;
+    int32_t n_lights;
+    const rt_light* lights;
+} rt_scene_soa;
+
+/* Per-Render() constants, computed on the host with the reference arithmetic. */
+typedef struct rt_render_params {
+    int32_t abi_version;
+    int32_t width, height;   /* mDisplay->xRes/yRes (Raytracer.cpp:781-786) */
+    int32_t depth;           /* Raycast bounces, default 4 (Raytracer.h:563) */
+    int32_t ao_samples;      /* numSamples, default 128 (Raytracer.cpp:317) */
+    int32_t ao_enabled;      /* 0 => CalculateAmbientOcclusion returns 1.0f */
+    int32_t rng_engine;      /* RT_RNG_* */
+    uint32_t rng_seed;       /* engine seed: 1 (minstd_rand0) / 5489 (mt19937) */
+    int32_t view_inverse_ok; /* Matrix::Inverse(viewMatrix) succeeded (:850) */
+    float view_inv[9];       /* rows 0..2, cols 0..2 of inverse(viewMatrix) */
+    float cam_from[3];       /* camera.from: ray origin and specular eye */
+    double ndc_kx;           /* (double)aspect * tan(ToRadian(fov/2)) (:836-839) */
+    double ndc_ky;           /* tan(ToRadian(fov/2))                  (:840)      */
+    float ao_angle_max;      /* (float)(2*PI): uniform_real_distribution b (:270) */
+    int32_t row_begin;       /* rows row_begin, row_begin+row_step, ... < row_end */
+    int32_t row_end;         /* are rendered by this call (full frame: 0, height, 1); */
+    int32_t row_step;        /* rank r of G renders row_begin=r, row_step=G        */
+} rt_render_params;
+
+typedef struct rt_render_stats {
+    uint64_t rays_total;       /* IntersectScene calls of the frame */
+    uint64_t rays_primary;     /* camera rays */
+    uint64_t rays_secondary;   /* reflection + refraction */
+    uint64_t rays_shadow;      /* directional + point shadow rays */
+    uint64_t rays_ao;          /* AO rays */
+    uint64_t ao_calls;         /* CalculateAmbientOcclusion calls */
+    double ms_count;           /* count/offset pass (HIP events) */
+    double ms_scan;
+    double ms_render;          /* shading megakernel */
+    double ms_total;           /* first launch -> framebuffer on host */
+} rt_render_stats;
+
+/* Select the device (device < 0: $LOCAL_RANK or 0) and create streams/events. */
+int rt_gpu_init(int device);
+/* Upload (replace) the flattened scene; buffers stay resident in HBM. */
+int rt_gpu_upload_scene(const rt_scene_soa* scene);
+/* Use this HIP stream (hipStream_t) for all work; NULL: the shim's own stream. */
+int rt_gpu_set_stream(void* hip_stream);
+/* Render the rows selected by params into fb_out (host, Pixel layout: int16
+ * r,g,b interleaved; the selected rows packed in order, each `width` pixels).
+ * Single-rank: the RNG offsets are scanned on the device. Blocking. */
+int rt_gpu_render(const rt_render_params* params, int16_t* fb_out);
+/* Same, leaving the framebuffer in HBM (device pointer valid until the next
+ * call); asynchronous on the shim's stream. */
+int rt_gpu_render_device(const rt_render_params* params, int16_t** fb_device);
+/* Multi-rank split of rt_gpu_render_device. Buffers are
+ * caller-owned device memory (e.g. torch tensors on this device); the work is
+ * queued on the shim's stream (see rt_gpu_set_stream).
+ *  phase 1: AO calls of each selected row -> row_calls_device (uint32[n_rows]);
+ *  caller:  all-gather the per-row counts of every rank, exclusive-scan them in
+ *           raster order, keep its own rows' bases (uint64[n_rows]);
+ *  phase 2: shade the selected rows with those RNG bases -> fb_device
+ *           (int16[n_rows*width*3]). Phase 2 reuses phase 1's per-pixel counts:
+ *           call it with the same params, before any other count/render. */
+int rt_gpu_count_rows(const rt_render_params* params, uint32_t* row_calls_device);
+int rt_gpu_shade_rows(const rt_render_params* params, const uint64_t* row_base_device,
+                      int16_t* fb_device);
+/* Counters and HIP-event timings of the last render. */
+int rt_gpu_last_stats(rt_render_stats* stats);
+/* Last error message (static storage). */
+const char* rt_gpu_last_error(void);
+void rt_gpu_shutdown(void);
+
+/* ---- Reference class surface as a C ABI (what an FFI/ctypes binding calls) ----
+ * Mirrors Raytracer(int,int) / LoadSceneJSON / InitializeRenderer / Render /
+ * FlushFrameBufferToPPM (Raytracer.h:572-588, :604). */
+typedef struct rt580_raytracer rt580_raytracer;
+rt580_raytracer* rt580_create(int width, int height);
+void rt580_destroy(rt580_raytracer* rt);
+/* assets_root: directory that contains "Assets/" (the reference uses the CWD). */
+int rt580_set_assets_root(rt580_raytracer* rt, const char* assets_root);
+int rt580_load_scene_json(rt580_raytracer* rt, const char* scene_path);
+int rt580_initialize_renderer(rt580_raytracer* rt);
+int rt580_render(rt580_raytracer* rt, const char* output_ppm); /* "" / NULL: no file */
+int rt580_flush_ppm(rt580_raytracer* rt, const char* output_ppm);
+/* Runtime knobs (reference defaults: depth 4, 128 AO samples, AO on, minstd_rand0). */
+int rt580_set_depth(rt580_raytracer* rt, int depth);
+int rt580_set_ao(rt580_raytracer* rt, int samples, int enabled);
+int rt580_set_rng(rt580_raytracer* rt, int engine);
+int rt580_set_rows(rt580_raytracer* rt, int row_begin, int row_end);
+const int16_t* rt580_framebuffer(rt580_raytracer* rt); /* Pixel[w*h] */
+int rt580_get_render_params(rt580_raytracer* rt, rt_render_params* out);
+int rt580_get_scene(rt580_raytracer* rt, rt_scene_soa* out); /* views valid until next load */
+int rt580_last_stats(rt580_raytracer* rt, rt_render_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT580_H */

@@ -1,0 +1,736 @@
+// rt_oracle.cpp — CPU restatement of the reference ray tracer (see rt_oracle.h).
+// TEST INFRASTRUCTURE ONLY. Compile with -ffp-contract=off (oracle/Makefile):
+// every float expression below must round exactly like the reference's.
+#include "rt_oracle.h"
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <random>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+// JSON tokenizer shared with the product loader (pure syntax; the scene
+// semantics below are restated independently from Raytracer.cpp:589-779).
+#include "../580-raytracer_amd/csrc/json_min.h"
+
+namespace ora {
+
+static const double kPI = 3.14159265;          // Raytracer.h:11
+static const double kEPS = 1e-6;               // Raytracer.h:12
+static const float kOFFSET = (float)0.2;       // SHADOW_CLIPPING_OFFSET, Raytracer.h:13 (used as float arg)
+
+// ---------------------------------------------------------------- Vector3 (Raytracer.h:39-149)
+struct V3 {
+    float x = 0, y = 0, z = 0;
+    V3() {}
+    V3(float a, float b, float c) : x(a), y(b), z(c) {}
+    V3 operator*(float s) const { return {x * s, y * s, z * s}; }
+    V3 operator*(const V3& o) const { return {x * o.x, y * o.y, z * o.z}; }
+    V3 operator-(const V3& o) const { return {x - o.x, y - o.y, z - o.z}; }
+    V3 operator+(const V3& o) const { return {x + o.x, y + o.y, z + o.z}; }
+    V3 operator-() const { return {-x, -y, -z}; }
+    void normalize() {  // Raytracer.h:109-116
+        float len = std::sqrt(x * x + y * y + z * z);
+        if (len > 0) { x /= len; y /= len; z /= len; }
+    }
+    float length() const { return std::sqrt(x * x + y * y + z * z); }
+    static V3 cross(const V3& a, const V3& b) {
+        return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+    }
+    float dot(const V3& o) const { return x * o.x + y * o.y + z * o.z; }
+    static V3 reflect(const V3& I, const V3& N) {  // Raytracer.h:143-148
+        float d = I.dot(N);
+        d *= 2;
+        return I - N * d;
+    }
+};
+
+// ---------------------------------------------------------------- Matrix (Raytracer.h:168-371)
+struct M4 {
+    float m[4][4];
+    M4 operator*(const M4& o) const {
+        M4 r;
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+                r.m[i][j] = 0;
+                for (int k = 0; k < 4; ++k) r.m[i][j] += m[i][k] * o.m[k][j];
+            }
+        return r;
+    }
+    V3 translation() const { return {m[0][3], m[1][3], m[2][3]}; }
+    V3 xform_dir(const V3& d) const {
+        return {m[0][0] * d.x + m[0][1] * d.y + m[0][2] * d.z,
+                m[1][0] * d.x + m[1][1] * d.y + m[1][2] * d.z,
+                m[2][0] * d.x + m[2][1] * d.y + m[2][2] * d.z};
+    }
+    V3 xform_point(const V3& p) const {  // Raytracer.h:234-248
+        float x = m[0][0] * p.x + m[0][1] * p.y + m[0][2] * p.z + m[0][3];
+        float y = m[1][0] * p.x + m[1][1] * p.y + m[1][2] * p.z + m[1][3];
+        float z = m[2][0] * p.x + m[2][1] * p.y + m[2][2] * p.z + m[2][3];
+        float w = m[3][0] * p.x + m[3][1] * p.y + m[3][2] * p.z + m[3][3];
+        if (w != 1.0f) { x /= w; y /= w; z /= w; }
+        return {x, y, z};
+    }
+    static void identity(M4& a) {  // LoadIdentityMatrix, Raytracer.cpp:872-878
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) a.m[i][j] = (i == j) ? 1.0f : 0.0f;
+    }
+    static float det3(const M4& a) {  // Raytracer.h:251-255
+        return a.m[0][0] * (a.m[1][1] * a.m[2][2] - a.m[1][2] * a.m[2][1]) -
+               a.m[0][1] * (a.m[1][0] * a.m[2][2] - a.m[1][2] * a.m[2][0]) +
+               a.m[0][2] * (a.m[1][0] * a.m[2][1] - a.m[1][1] * a.m[2][0]);
+    }
+    static float det4(const M4& a) {  // Raytracer.h:257-274
+        float det = 0;
+        for (int i = 0; i < 4; i++) {
+            M4 sub;
+            std::memset(&sub, 0, sizeof sub);
+            for (int j = 1; j < 4; j++)
+                for (int k = 0; k < 4; k++) {
+                    if (k < i) sub.m[j - 1][k] = a.m[j][k];
+                    else if (k > i) sub.m[j - 1][k - 1] = a.m[j][k];
+                }
+            det += (i % 2 == 0 ? 1 : -1) * a.m[0][i] * det3(sub);
+        }
+        return det;
+    }
+    static bool inverse(const M4& a, M4& r) {  // Raytracer.h:276-296, :354-370
+        float det = det4(a);
+        if (std::fabs(det) < 1e-10) return false;
+        M4 adj;
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) {
+                M4 sub;
+                std::memset(&sub, 0, sizeof sub);
+                int si = 0;
+                for (int k = 0; k < 4; k++) {
+                    if (k == i) continue;
+                    int sj = 0;
+                    for (int l = 0; l < 4; l++) {
+                        if (l == j) continue;
+                        sub.m[si][sj] = a.m[k][l];
+                        sj++;
+                    }
+                    si++;
+                }
+                float c = det3(sub);
+                if ((i + j) % 2 != 0) c = -c;
+                adj.m[j][i] = c;
+            }
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) r.m[i][j] = adj.m[i][j] / det;
+        return true;
+    }
+};
+
+// ---------------------------------------------------------------- Pixel (Raytracer.h:373-418)
+// static_cast<short>(float) as g++ emits it on x86-64: cvttss2si to int32
+// (NaN / out of range -> INT32_MIN), then the low 16 bits.
+static inline short f2s(float f) {
+    int32_t i;
+    if (!(f > -2147483904.0f && f < 2147483648.0f)) i = INT32_MIN;
+    else i = (int32_t)f;
+    return (short)(uint16_t)(uint32_t)i;
+}
+struct Pix {
+    short r = 0, g = 0, b = 0;
+    Pix() {}
+    Pix(short a, short c, short d) : r(a), g(c), b(d) {}
+    explicit Pix(const V3& v) : r(f2s(v.x * 255)), g(f2s(v.y * 255)), b(f2s(v.z * 255)) {}  // clamp() result discarded (:380)
+    Pix clamp() const {
+        Pix o;
+        o.r = r > 255 ? 255 : (r < 0 ? 0 : r);
+        o.g = g > 255 ? 255 : (g < 0 ? 0 : g);
+        o.b = b > 255 ? 255 : (b < 0 ? 0 : b);
+        return o;
+    }
+    Pix operator*(float s) const { return Pix(f2s(r * s), f2s(g * s), f2s(b * s)).clamp(); }
+    Pix operator+(const Pix& o) const { return Pix((short)(r + o.r), (short)(g + o.g), (short)(b + o.b)); }
+};
+
+// ---------------------------------------------------------------- scene
+struct Material {  // Raytracer.h:442-463
+    V3 cs{1, 1, 1};
+    float ka = 0.5f, kd = 0.75f, ks = 0.95f, kt = 0.95f, ior = 2.5f, n = 32.0f;
+};
+struct Tri { V3 p[3], nrm[3]; };
+struct Mesh { int type = 0; std::vector<Tri> tris; float radius = 0; };  // value-initialised (:605)
+struct Shape { Material mat; V3 S{1, 1, 1}, R, T; int mesh = -1; M4 model; };
+struct Light { int type = -1; V3 color, position, direction; float intensity = 0; };
+enum { LDIR = 0, LPOINT = 1, LAMB = 2 };
+struct Camera { V3 from, to; };
+struct Scene {
+    std::vector<Shape> shapes;
+    std::vector<Mesh> meshes;
+    std::vector<Light> lights;
+    Camera cam;
+};
+
+static std::string read_file(const std::string& p, bool& ok) {
+    std::ifstream f(p, std::ios::binary);
+    ok = f.is_open();
+    std::stringstream ss;
+    if (ok) ss << f.rdbuf();
+    return ss.str();
+}
+
+static float ToRadian(float deg) { return (float)(deg * (kPI / 180)); }  // Raytracer.h:581-583
+
+// ComputeModelMatrix, Raytracer.cpp:528-586. g++ merges cos/sin of one
+// argument into glibc sincos (checked in the reference binary), so do we.
+static M4 model_matrix(const Shape& s) {
+    M4 S, RX, RY, RZ, T;
+    M4::identity(S);
+    S.m[0][0] = s.S.x; S.m[1][1] = s.S.y; S.m[2][2] = s.S.z; S.m[3][3] = 1.0f;
+    double sx, cx, sy, cy, sz, cz;
+    ::sincos((double)ToRadian(s.R.x), &sx, &cx);
+    ::sincos((double)ToRadian(s.R.y), &sy, &cy);
+    ::sincos((double)ToRadian(s.R.z), &sz, &cz);
+    M4::identity(RX);
+    RX.m[1][1] = (float)cx; RX.m[1][2] = (float)-sx; RX.m[2][1] = (float)sx; RX.m[2][2] = (float)cx;
+    M4::identity(RY);
+    RY.m[0][0] = (float)cy; RY.m[0][2] = (float)sy; RY.m[2][0] = (float)-sy; RY.m[2][2] = (float)cy;
+    M4::identity(RZ);
+    RZ.m[0][0] = (float)cz; RZ.m[0][1] = (float)-sz; RZ.m[1][0] = (float)sz; RZ.m[1][1] = (float)cz;
+    M4 R = RZ * RY * RX;
+    M4::identity(T);
+    T.m[0][3] = s.T.x; T.m[1][3] = s.T.y; T.m[2][3] = s.T.z;
+    return S * R * T;
+}
+
+static V3 vec3(const json_min::Value& a) { return {a.at(0).as_float(), a.at(1).as_float(), a.at(2).as_float()}; }
+
+// LoadMesh, Raytracer.cpp:589-643
+static int load_mesh(Scene& sc, std::map<std::string, int>& cache, const std::string& root,
+                     const std::string& name, int& idx) {
+    auto it = cache.find(name);
+    if (it != cache.end()) { idx = it->second; return 0; }
+    bool ok;
+    std::string text = read_file(root + "/Assets/" + name + ".json", ok);
+    if (!ok) { std::fprintf(stderr, "oracle: mesh %s not found\n", name.c_str()); idx = -1; return 1; }
+    json_min::Value j = json_min::parse(text);
+    Mesh mesh;
+    std::string type = j.at("data").at(0).at("type").as_string();
+    for (const json_min::Value* item : j.at("data").items()) {
+        if (type == "polygon") {
+            mesh.type = 0;
+            Tri t;
+            for (int i = 0; i < 3; i++) {
+                const json_min::Value& v = item->at("v" + std::to_string(i));
+                t.p[i] = vec3(v.at("v"));
+                t.nrm[i] = vec3(v.at("n"));
+                (void)v.at("t").at(0).as_float(); (void)v.at("t").at(1).as_float();
+            }
+            mesh.tris.push_back(t);
+        } else if (type == "sphere") {
+            mesh.type = 1;
+            mesh.radius = item->at("radius").as_float();
+        }
+    }
+    sc.meshes.push_back(mesh);
+    idx = (int)sc.meshes.size() - 1;
+    cache[name] = idx;
+    return 0;
+}
+
+// LoadSceneJSON, Raytracer.cpp:645-779
+static int load_scene(Scene& sc, const std::string& root, const std::string& path) {
+    bool ok;
+    std::string text = read_file(root + "/Assets/" + path, ok);
+    if (!ok) { std::fprintf(stderr, "oracle: cannot open %s\n", path.c_str()); return 1; }
+    int status = 0;
+    try {
+        json_min::Value j = json_min::parse(text);
+        const json_min::Value& s = j.at("scene");
+        std::map<std::string, int> cache;
+        if (s.contains("shapes"))
+            for (const json_min::Value* sv : s.at("shapes").items()) {
+                Shape shp;
+                (void)sv->at("id").as_string();
+                std::string geo = sv->at("geometry").as_string();
+                const json_min::Value& m = sv->at("material");
+                shp.mat.cs = vec3(m.at("Cs"));
+                shp.mat.ka = m.at("Ka").as_float();
+                shp.mat.kd = m.at("Kd").as_float();
+                shp.mat.ks = m.at("Ks").as_float();
+                shp.mat.kt = m.at("Kt").as_float();
+                shp.mat.n = m.at("n").as_float();
+                for (const json_min::Value* t : sv->at("transforms").items()) {
+                    if (t->contains("Rx")) shp.R.x = t->at("Rx").as_float();
+                    if (t->contains("Ry")) shp.R.y = t->at("Ry").as_float();
+                    if (t->contains("Rz")) shp.R.z = t->at("Rz").as_float();
+                    if (t->contains("S") && t->at("S").is_array()) shp.S = vec3(t->at("S"));
+                    if (t->contains("T") && t->at("T").is_array()) shp.T = vec3(t->at("T"));
+                }
+                status |= load_mesh(sc, cache, root, geo, shp.mesh);
+                shp.model = model_matrix(shp);
+                sc.shapes.push_back(shp);
+            }
+        if (s.contains("camera")) {
+            const json_min::Value& c = s.at("camera");
+            sc.cam.from = vec3(c.at("from"));
+            sc.cam.to = vec3(c.at("to"));
+            for (int i = 0; i < 6; i++) (void)c.at("bounds").at(i).as_float();
+            (void)c.at("resolution").at(0).as_int(); (void)c.at("resolution").at(1).as_int();
+        }
+        if (s.contains("lights"))
+            for (const json_min::Value* lv : s.at("lights").items()) {
+                Light l;
+                l.color = vec3(lv->at("color"));
+                l.intensity = lv->at("intensity").as_float();
+                std::string t = lv->at("type").as_string();
+                if (t == "directional") {
+                    V3 from = vec3(lv->at("from")), to = vec3(lv->at("to"));
+                    l.direction = to - from;
+                    l.direction.normalize();
+                    l.type = LDIR;
+                } else if (t == "ambient") {
+                    l.type = LAMB;
+                } else if (t == "point") {
+                    l.type = LPOINT;
+                    l.position = vec3(lv->at("position"));
+                } else {
+                    std::fprintf(stderr, "oracle: unsupported light type %s\n", t.c_str());
+                    return 1;  // reference: lightType left uninitialised (UB)
+                }
+                sc.lights.push_back(l);
+            }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle: scene error: %s\n", e.what());
+        return 1;
+    }
+    return status;
+}
+
+// ---------------------------------------------------------------- RNG (member mGenerator, Raytracer.h:592)
+// libstdc++ 11: minstd_rand0 = linear_congruential_engine<uint_fast32_t,16807,0,2^31-1>, seed 1;
+// uniform_real_distribution<float>::operator() = generate_canonical<float,24>() * (b-a) + a
+// (random.h, random.tcc:3348-3378). MSVC: mt19937, seed 5489.
+struct DrawSource {
+    int engine = 0;
+    std::vector<uint32_t> stream;  // engine 1: pre-generated outputs
+    static uint64_t mulmod(uint64_t a, uint64_t b) { return (a * b) % 2147483647ull; }
+    static uint64_t powmod(uint64_t a, uint64_t e) {
+        uint64_t r = 1;
+        while (e) { if (e & 1) r = mulmod(r, a); a = mulmod(a, a); e >>= 1; }
+        return r;
+    }
+};
+struct RngCursor {  // one thread's position in the global draw stream
+    const DrawSource* src;
+    uint64_t index = 0;  // draws consumed so far
+    uint64_t state = 1;  // minstd state after `index` draws
+    void seek(uint64_t k) {
+        index = k;
+        if (src->engine == 0) state = DrawSource::powmod(16807, k % 2147483646ull);
+    }
+    float canonical() {
+        float ret;
+        if (src->engine == 0) {
+            state = (state * 16807ull) % 2147483647ull;
+            ret = (float)(unsigned long)(state - 1) / 2147483648.0f;
+        } else {
+            uint32_t x = src->stream[index];
+            ret = (float)(unsigned long)x / 4294967296.0f;
+        }
+        index++;
+        if (ret >= 1.0f) ret = std::nextafter(1.0f, 0.0f);
+        return ret;
+    }
+    float uniform(float a, float b) { return canonical() * (b - a) + a; }
+};
+
+// ---------------------------------------------------------------- tracer
+struct Ray {
+    V3 o, d;
+    Ray() {}
+    Ray(const V3& origin, const V3& dir) : o(origin), d(dir) { d.normalize(); }  // Raytracer.h:431-433
+};
+struct Hit {
+    int type = 0;
+    V3 p, n;
+    float t = 0;
+    const Tri* tri = nullptr;
+    const Material* mat = nullptr;
+    float a = 0, b = 0, g = 0;
+};
+struct Counters { uint64_t primary = 0, secondary = 0, shadow = 0, ao = 0, ao_calls = 0, tree_hits = 0; };
+
+struct Tracer {
+    const Scene* sc;
+    int depth, ao_n, ao_on, n_amb;
+    float ao_bmax;  // (float)(2 * PI)
+
+    static float CalcArea(const V3& A, const V3& B, const V3& C, const V3& N) {  // Raytracer.cpp:937-942
+        V3 ab = B - A, ac = C - A;
+        V3 c = V3::cross(ab, ac);
+        return (float)(0.5 * c.dot(N));
+    }
+    // IntersectTriangle, Raytracer.cpp:348-409 (world vertices from the cached model matrix)
+    static bool tri_hit(const Ray& r, const Tri& tri, const M4& M, Hit& h) {
+        V3 v0 = M.xform_point(tri.p[0]), v1 = M.xform_point(tri.p[1]), v2 = M.xform_point(tri.p[2]);
+        V3 e1 = v1 - v0, e2 = v2 - v0;
+        V3 N = V3::cross(e1, e2);
+        N.normalize();
+        float nd = N.dot(r.d);
+        if (std::abs(nd - 0.0f) < kEPS) return false;  // NearlyEquals, Raytracer.cpp:16-18
+        float D = -N.dot(v0);
+        float t = -(N.dot(r.o) + D) / nd;
+        if (t <= kEPS) return false;
+        V3 P = r.o + r.d * t;
+        float area = CalcArea(v0, v1, v2, N);
+        float a = CalcArea(P, v1, v2, N) / area;
+        float b = CalcArea(v0, P, v2, N) / area;
+        float g = CalcArea(v0, v1, P, N) / area;
+        if (a < 0 || b < 0 || g < 0) return false;
+        h.p = P; h.type = 0; h.n = N; h.n.normalize(); h.t = t; h.a = a; h.b = b; h.g = g;
+        return true;
+    }
+    // IntersectSphere, Raytracer.cpp:419-464
+    static bool sph_hit(const Ray& r, float radius, const M4& M, Hit& h) {
+        V3 oc = r.o - M.translation();
+        float b = 2.0f * r.d.dot(oc);
+        float c = oc.dot(oc) - (radius * radius);
+        float disc = (b * b) - (4 * 1.0f * c);
+        if (disc < kEPS) return false;
+        float sq = std::sqrt(disc);
+        float t0 = (-b + sq) / (float)2, t1 = (-b - sq) / (float)2;
+        bool g0 = t0 > kEPS, g1 = t1 > kEPS;
+        if (!g0 && !g1) return false;
+        if (!g0) h.t = t1;
+        else if (!g1) h.t = t0;
+        else h.t = std::fmin(t0, t1);
+        h.p = r.o + (r.d * h.t);
+        h.n = h.p - M.translation();
+        h.n.normalize();
+        h.type = 1;
+        return true;
+    }
+    // IntersectScene, Raytracer.cpp:473-526
+    bool intersect(const Ray& r, Hit& out) const {
+        Hit best;
+        bool found = false;
+        for (const Shape& s : sc->shapes) {
+            const Mesh& m = sc->meshes[s.mesh];
+            if (m.type == 0) {
+                for (const Tri& t : m.tris) {
+                    Hit h;
+                    if (tri_hit(r, t, s.model, h) && (!found || h.t < best.t)) {
+                        found = true; best = h; best.tri = &t; best.mat = &s.mat;
+                    }
+                }
+            } else {
+                Hit h;
+                if (sph_hit(r, m.radius, s.model, h) && (!found || h.t < best.t)) {
+                    found = true; best = h; best.mat = &s.mat;
+                }
+            }
+        }
+        if (found) out = best;
+        return found;
+    }
+
+    // CalculateAmbientOcclusion + RandomInHemisphere + RandomUnitVector, Raytracer.cpp:269-330
+    float ambient_occlusion(const V3& hp, const V3& n, RngCursor& rng, Counters& c) const {
+        c.ao_calls++;
+        if (!ao_on) return 1.0f;
+        float occ = 0.0f;
+        for (int i = 0; i < ao_n; i++) {
+            float z = rng.uniform(-1.0f, 1.0f);
+            float a = rng.uniform(0.0f, ao_bmax);
+            float r = std::sqrt(1 - z * z);
+            double s, co;
+            ::sincos((double)a, &s, &co);  // cos(a), sin(a) as g++ compiles them
+            V3 v((float)((double)r * co), (float)((double)r * s), z);
+            v.normalize();
+            if (!(v.dot(n) > 0.0)) v = -v;
+            Ray ray(hp + v * kOFFSET, v);
+            Hit h;
+            c.ao++;
+            if (intersect(ray, h)) occ += 1.0f;
+        }
+        return 1.0f - ((float)occ / (float)ao_n);
+    }
+
+    static float fmax0(float x) { return (float)std::fmax((double)x, 0.0); }
+    static float clipf(float x, int lo, int hi) { if (x < lo) return (float)lo; if (x > hi) return (float)hi; return x; }
+
+    // CalculateLocalColor, Raytracer.cpp:213-267
+    Pix local_color(const Hit& h, const Light& l, const Material& m) const {
+        V3 L;
+        if (l.type == LPOINT) { L = l.position - h.p; L.normalize(); }
+        else { L = l.direction * -1; L.normalize(); }
+        V3 n;
+        if (h.type == 0) {
+            n = (h.tri->nrm[0] * h.a + h.tri->nrm[1] * h.b) + h.tri->nrm[2] * h.g;  // InterpolateVector3 :333-338
+            n.normalize();
+        } else {
+            n = h.n;
+        }
+        n.normalize();
+        float ds = fmax0(L.dot(n));
+        V3 diff = l.color * ds * l.intensity;
+        V3 R = V3::reflect(L, n);
+        R.normalize();
+        V3 V = sc->cam.from - h.p;
+        V.normalize();
+        float ss = fmax0(V.dot(R));
+        ss = powf(ss, m.n);
+        V3 spec = l.color * ss * l.intensity;
+        V3 lighting = diff * m.kd + spec * m.ks;
+        V3 col = m.cs * lighting;
+        col.x = clipf(col.x, 0, 1); col.y = clipf(col.y, 0, 1); col.z = clipf(col.z, 0, 1);
+        return Pix(col);
+    }
+    // CalculateRefraction, Raytracer.cpp:168-203
+    static V3 refraction(const V3& I, const V3& N, float ior) {
+        float cosi = I.dot(N);
+        if (cosi < -1) cosi = -1;
+        else if (cosi > 1) cosi = 1;
+        float n1 = 1, n2 = ior;
+        V3 n = N;
+        if (cosi < 0) cosi = -1 * cosi;
+        else { float t = n1; n1 = n2; n2 = t; n = -N; }
+        float eta = n1 / n2;
+        float k = 1 - eta * eta * (1 - cosi * cosi);
+        if (k < 0) return V3(0, 0, 0);
+        return I * eta + n * (eta * cosi - std::sqrt(k));
+    }
+    // ComputeFresnel, Raytracer.cpp:131-166
+    static void fresnel(float ior, const V3& N, const V3& I, float& kr, float& kt) {
+        float cosi = clipf(I.dot(N), -1, 1);
+        bool inside = cosi > 0;
+        float ei = 1, et = ior;
+        if (inside) { std::swap(ei, et); cosi = -cosi; }
+        float sint = ei / et * std::sqrt(std::max(0.f, 1 - cosi * cosi));
+        if (sint >= 1) { kr = 1; kt = 0; }
+        else {
+            float cost = std::sqrt(std::max(0.f, 1 - sint * sint));
+            cosi = std::fabs(cosi);
+            float Rs = ((et * cosi) - (ei * cost)) / ((et * cosi) + (ei * cost));
+            float Rp = ((ei * cosi) - (et * cost)) / ((ei * cosi) + (et * cost));
+            kr = (Rs * Rs + Rp * Rp) / 2;
+            kt = 1 - kr;
+        }
+    }
+
+    // Raycast, Raytracer.cpp:28-129
+    Pix raycast(const Ray& ray, int bounces, RngCursor* rng, Counters& c, bool count_only) const {
+        Hit info;
+        if (!intersect(ray, info)) return Pix(254, 64, 205);  // BG_COLOR, Raytracer.h:597
+        c.tree_hits++;
+        const Material& m = *info.mat;
+        Pix local(0, 0, 0);
+        for (const Light& l : sc->lights) {
+            if (l.type == LAMB) {
+                if (count_only) { c.ao_calls++; c.ao += ao_on ? ao_n : 0; continue; }
+                V3 amb = m.cs * m.ka * l.color * l.intensity;
+                amb = amb * ambient_occlusion(info.p, info.n, *rng, c);
+                local = local + Pix(amb);
+                continue;
+            }
+            V3 L;
+            if (l.type == LDIR) L = -(l.direction);
+            else L = (l.position - info.p);
+            L.normalize();
+            Ray lr(info.p + L * kOFFSET, L);
+            float dist = (l.position - info.p).length();
+            c.shadow++;
+            if (count_only) continue;
+            Hit lh;
+            if (!intersect(lr, lh) || (lh.t > dist && l.type == LPOINT)) local = local + local_color(info, l, m);
+        }
+        if (bounces > 0) {
+            float kr, kt;
+            Pix refl, refr;
+            if (m.ks > 0) {
+                V3 d = V3::reflect(ray.d, info.n);
+                d.normalize();
+                Ray rr(info.p + d * kOFFSET, d);
+                c.secondary++;
+                refl = raycast(rr, bounces - 1, rng, c, count_only);
+            }
+            if (m.kt > 0) {
+                V3 d = refraction(ray.d, info.n, m.ior);
+                Ray tr(info.p + d * kOFFSET, d);
+                c.secondary++;
+                refr = raycast(tr, bounces - 1, rng, c, count_only);
+            }
+            fresnel(m.ior, info.n, ray.d, kr, kt);
+            Pix fr = refl * kr * m.ks;
+            Pix ft = refr * kt * m.kt;
+            float alb = 1 - m.ks - m.kt;
+            alb = std::max(alb, 0.0f);
+            local = (local * alb) + (fr * m.ks) + (ft * m.kt);
+        }
+        return local.clamp();
+    }
+};
+
+struct Camera2 {
+    bool inv_ok = false;
+    M4 inv;
+    V3 from;
+    double kx = 0, ky = 0;
+    int w = 0, h = 0;
+};
+
+// InitializeRenderer + CalculateViewMatrix, Raytracer.cpp:861-870, :895-915; GenerateRay constants :832-858
+static Camera2 init_camera(const Scene& sc, int w, int h) {
+    Camera2 c;
+    V3 n = sc.cam.from - sc.cam.to;
+    n.normalize();
+    V3 up(0, 1, 0);
+    V3 u = V3::cross(up, n);
+    u.normalize();
+    V3 v = V3::cross(n, u);
+    v.normalize();
+    V3 r = sc.cam.from;
+    M4 view;
+    view.m[0][0] = u.x; view.m[0][1] = u.y; view.m[0][2] = u.z; view.m[0][3] = -r.dot(u);
+    view.m[1][0] = v.x; view.m[1][1] = v.y; view.m[1][2] = v.z; view.m[1][3] = -r.dot(v);
+    view.m[2][0] = n.x; view.m[2][1] = n.y; view.m[2][2] = n.z; view.m[2][3] = -r.dot(n);
+    view.m[3][0] = 0; view.m[3][1] = 0; view.m[3][2] = 0; view.m[3][3] = 1;
+    c.inv_ok = M4::inverse(view, c.inv);
+    c.from = sc.cam.from;
+    float fov = 60.0f;  // Raytracer.cpp:786
+    float aspect = (float)w / (float)h;
+    double tn = std::tan((double)ToRadian(fov / 2));
+    c.kx = aspect * tn;
+    c.ky = tn;
+    c.w = w; c.h = h;
+    return c;
+}
+
+static Ray generate_ray(const Camera2& c, int x, int y) {  // GenerateRay, Raytracer.cpp:832-858
+    double ndcx = (2.0 * x) / c.w - 1;
+    double ndcy = 1 - (2.0 * y) / c.h;
+    ndcx *= c.kx;
+    ndcy *= c.ky;
+    Ray r;
+    r.o = c.from;
+    V3 d((float)ndcx, (float)ndcy, -1.0f);
+    if (c.inv_ok) {
+        r.d = c.inv.xform_dir(d);
+        r.d.normalize();
+    }
+    return r;
+}
+
+}  // namespace ora
+
+using namespace ora;
+
+extern "C" int oracle_render(const char* assets_root, const char* scene, int w, int h, int depth,
+                             int ao_samples, int ao_enabled, int engine, int threads, int row_begin,
+                             int row_end, int16_t* fb, uint64_t* counters, uint64_t* rays_per_row) {
+    if (w <= 0 || h <= 0 || depth < 0 || ao_samples <= 0 || row_begin < 0 || row_end > h || row_begin > row_end)
+        return 2;
+    Scene sc;
+    if (load_scene(sc, assets_root, scene) != 0) return 1;
+    for (const Shape& s : sc.shapes)
+        if (s.mesh < 0) return 1;
+    Camera2 cam = init_camera(sc, w, h);
+    Tracer tr;
+    tr.sc = &sc;
+    tr.depth = depth;
+    tr.ao_n = ao_samples;
+    tr.ao_on = ao_enabled;
+    tr.ao_bmax = (float)(2 * kPI);
+    tr.n_amb = 0;
+    for (auto& l : sc.lights) tr.n_amb += l.type == LAMB;
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    if (threads <= 0) threads = 1;
+
+    // Pass 1: AO calls per pixel for every pixel in [0, row_end) (raster prefix).
+    const int nrows_all = row_end;
+    std::vector<uint32_t> calls((size_t)nrows_all * w);
+    {
+        std::atomic<int> next{0};
+        auto work = [&] {
+            for (;;) {
+                int y = next.fetch_add(1);
+                if (y >= nrows_all) break;
+                for (int x = 0; x < w; x++) {
+                    Counters c;
+                    tr.raycast(generate_ray(cam, x, y), depth, nullptr, c, true);
+                    calls[(size_t)y * w + x] = (uint32_t)c.ao_calls;
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; t++) th.emplace_back(work);
+        for (auto& t : th) t.join();
+    }
+    std::vector<uint64_t> base((size_t)nrows_all * w + 1, 0);
+    for (size_t i = 0; i < calls.size(); i++) base[i + 1] = base[i] + calls[i];
+    DrawSource src;
+    src.engine = engine;
+    const uint64_t per_call = 2ull * (uint64_t)ao_samples;
+    if (engine == 1 && ao_enabled) {
+        uint64_t total = base.back() * per_call;
+        src.stream.resize(total);
+        std::mt19937 g;  // default seed 5489
+        for (uint64_t i = 0; i < total; i++) src.stream[i] = (uint32_t)g();
+    }
+    // Pass 2: render rows [row_begin, row_end).
+    std::vector<Counters> rowc((size_t)(row_end - row_begin));
+    {
+        std::atomic<int> next{row_begin};
+        auto work = [&] {
+            RngCursor rng;
+            rng.src = &src;
+            for (;;) {
+                int y = next.fetch_add(1);
+                if (y >= row_end) break;
+                Counters& c = rowc[y - row_begin];
+                for (int x = 0; x < w; x++) {
+                    size_t pi = (size_t)y * w + x;
+                    rng.seek(ao_enabled ? base[pi] * per_call : 0);
+                    Ray r = generate_ray(cam, x, y);
+                    c.primary++;
+                    Pix p = tr.raycast(r, depth, &rng, c, fb == nullptr);
+                    if (fb) {
+                        int16_t* o = fb + ((size_t)(y - row_begin) * w + x) * 3;
+                        o[0] = p.r; o[1] = p.g; o[2] = p.b;
+                    }
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; t++) th.emplace_back(work);
+        for (auto& t : th) t.join();
+    }
+    Counters tot;
+    for (size_t i = 0; i < rowc.size(); i++) {
+        const Counters& c = rowc[i];
+        uint64_t row_total = c.primary + c.secondary + c.shadow + c.ao;
+        if (rays_per_row) rays_per_row[i] = row_total;
+        tot.primary += c.primary; tot.secondary += c.secondary; tot.shadow += c.shadow;
+        tot.ao += c.ao; tot.ao_calls += c.ao_calls;
+    }
+    if (counters) {
+        counters[0] = tot.primary + tot.secondary + tot.shadow + tot.ao;
+        counters[1] = tot.primary; counters[2] = tot.secondary; counters[3] = tot.shadow;
+        counters[4] = tot.ao; counters[5] = tot.ao_calls;
+    }
+    return 0;
+}
+
+// FlushFrameBufferToPPM, Raytracer.cpp:796-830
+extern "C" int oracle_write_ppm(const char* path, int w, int h, const int16_t* fb) {
+    std::ofstream out(path, std::ios::binary);
+    if (!out.is_open()) return 1;
+    out << "P6\n" << w << " " << h << "\n255\n";
+    for (size_t i = 0; i < (size_t)w * h * 3; i++) {
+        unsigned char c = static_cast<unsigned char>(std::pow(fb[i] / 255.0f, 1.0f / 2.2f) * 255.0f);
+        out.put((char)c);
+    }
+    return 0;
+}

@@ -1,0 +1,40 @@
+// rt_oracle.h — CPU restatement of the reference's per-pixel ray-trace path.
+//
+// TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load or run this; the product (580-raytracer_amd/) never
+// links it. It is the parity checker for the HIP path on configurations larger
+// than the committed golden images, and is itself pinned against the reference
+// (oracle/_ref builds of /root/reference, golden PPMs in tests/golden/).
+//
+// Reference: /root/reference/580 Raytracer/Raytracer.{h,cpp} (MSVC C++, single
+// threaded). Restated here, function by function (file:line in each definition),
+// with two changes that do not alter a single output bit:
+//   * the model matrix of each shape (ComputeModelMatrix, Raytracer.cpp:528-586)
+//     is computed once per shape instead of once per shape per IntersectScene
+//     call (Raytracer.cpp:480), and the unused Matrix::Inverse per triangle test
+//     (Raytracer.cpp:350-351) and per pixel (:850) is computed once;
+//   * rows may be rendered on several threads: the single serial RNG stream
+//     (member mGenerator, Raytracer.h:592) is addressed by absolute draw index,
+//     found with a count pass + prefix sum over the raster order.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// counters[0..5] = rays_total, primary, secondary, shadow, ao, ao_calls
+// fb: (row_end-row_begin)*w*3 int16 (Pixel layout), may be NULL (count only).
+// rays_per_row: optional (row_end-row_begin) uint64 totals.
+// engine: 0 = minstd_rand0 (libstdc++ default_random_engine), 1 = mt19937
+// Returns 0 on success, 1 on failure (message on stderr).
+int oracle_render(const char* assets_root, const char* scene, int w, int h, int depth,
+                  int ao_samples, int ao_enabled, int engine, int threads, int row_begin,
+                  int row_end, int16_t* fb, uint64_t* counters, uint64_t* rays_per_row);
+
+// Writes the reference's P6 output (FlushFrameBufferToPPM, Raytracer.cpp:796-830).
+int oracle_write_ppm(const char* path, int w, int h, const int16_t* fb);
+
+#ifdef __cplusplus
+}
+#endif

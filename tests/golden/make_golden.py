@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures from the REFERENCE ITSELF (oracle/_ref builds of
+/root/reference/580 Raytracer/Raytracer.cpp; see oracle/Makefile). Run in the
+build container only (the reference does not exist on the GPU box):
+
+    make -C oracle ref && python tests/golden/make_golden.py [--big]
+
+Writes tests/golden/ppm/<name>.ppm (small renders, kept verbatim) and
+tests/golden/manifest.json (parameters, sha256, ray-free metadata). --big adds
+sha256-only entries for the BASELINE configurations (minutes of CPU each).
+Every entry records the exact reference binary and command line used.
+"""
+import gzip
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(REPO, "oracle", "_ref")
+ROOT = os.path.join(REF, "root")
+REF_OUTPUT_PPM = "/root/reference/580 Raytracer/output.ppm"
+
+# name, scene, w, h, depth, ao_n, ao_on, engine
+SMALL = []
+for scene, tag in [("simpleSphereScene.json", "sss"), ("simpleSphereSceneAO.json", "sssao"),
+                   ("simpleScene.json", "tri")]:
+    for depth in (0, 1, 4):
+        for ao_n, ao_on in ((128, 0), (4, 1), (16, 1), (128, 1)):
+            aotag = "aooff" if not ao_on else "ao%d" % ao_n
+            SMALL.append(("%s_d%d_%s" % (tag, depth, aotag), scene, 61, 47, depth, ao_n, ao_on, "minstd"))
+SMALL += [
+    ("sss_d2_ao16_mt", "simpleSphereScene.json", 61, 47, 2, 16, 1, "mt19937"),
+    ("sss_d8_ao4", "simpleSphereScene.json", 64, 64, 8, 4, 1, "minstd"),
+    ("sss_d4_ao128_pristine", "simpleSphereScene.json", 40, 30, -1, 128, 1, "minstd"),
+    ("teapots_d0_aooff", "scene.json", 48, 36, 0, 128, 0, "minstd"),
+    ("teapots_d2_ao4", "scene.json", 64, 48, 2, 4, 1, "minstd"),
+    ("teapots_d4_ao16_mt", "scene.json", 32, 24, 4, 16, 1, "mt19937"),
+    ("teapots_d1_ao128", "scene.json", 24, 18, 1, 128, 1, "minstd"),
+    ("sss_wide_d1_ao4", "simpleSphereScene.json", 97, 13, 1, 4, 1, "minstd"),
+    ("sss_tall_d1_aooff", "simpleSphereScene.json", 7, 53, 1, 128, 0, "minstd"),
+    ("sss_1x1_d4_ao16", "simpleSphereScene.json", 1, 1, 4, 16, 1, "minstd"),
+]
+BIG = [
+    # BASELINE config 1 and 2, the reference's committed output.ppm configuration,
+    # and the reference main() as shipped (500x500, Render(): depth 4, AO 128)
+    ("config1_500_d1_aooff", "simpleSphereScene.json", 500, 500, 1, 128, 0, "minstd"),
+    ("main_500_d4_ao128", "simpleSphereScene.json", 500, 500, -1, 128, 1, "minstd"),
+    ("config2_1080p_d4_ao64", "simpleSphereScene.json", 1920, 1080, 4, 64, 1, "minstd"),
+]
+
+
+def binary(ao_n, ao_on, engine):
+    pristine = ao_n == 128 and ao_on
+    name = "rt_ref" if pristine else "rt_ref_param"
+    if engine == "mt19937":
+        name += "_mt"
+    return os.path.join(REF, name)
+
+
+def run(entry, keep_ppm):
+    name, scene, w, h, depth, ao_n, ao_on, engine = entry
+    exe = binary(ao_n, ao_on, engine)
+    out = os.path.join("/tmp", "golden_%s.ppm" % name)
+    cmd = [exe, ROOT, scene, str(w), str(h), str(depth), out, str(ao_n), str(int(not ao_on))]
+    t0 = time.time()
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        raise SystemExit("reference failed: %s\n%s" % (" ".join(cmd), p.stderr))
+    data = open(out, "rb").read()
+    rec = {
+        "name": name, "scene": scene, "width": w, "height": h,
+        "depth": 4 if depth < 0 else depth, "via_render": depth < 0,
+        "ao_samples": ao_n, "ao_enabled": bool(ao_on), "rng": engine,
+        "sha256": hashlib.sha256(data).hexdigest(),
+        "reference_binary": os.path.basename(exe),
+        "reference_seconds": round(time.time() - t0, 3),
+    }
+    if keep_ppm:
+        dst = os.path.join(HERE, "ppm", name + ".ppm")
+        shutil.copyfile(out, dst)
+        rec["ppm"] = "ppm/%s.ppm" % name
+    os.remove(out)
+    print(name, rec["sha256"][:16], rec["reference_seconds"], "s", flush=True)
+    return rec
+
+
+def main():
+    big = "--big" in sys.argv
+    os.makedirs(os.path.join(HERE, "ppm"), exist_ok=True)
+    man_path = os.path.join(HERE, "manifest.json")
+    man = json.load(open(man_path)) if os.path.exists(man_path) else {"entries": []}
+    have = {e["name"]: e for e in man["entries"]}
+    todo = [(e, True) for e in SMALL] + ([(e, False) for e in BIG] if big else [])
+    for e, keep in todo:
+        if e[0] in have and (not keep or os.path.exists(os.path.join(HERE, have[e[0]].get("ppm", "-")))):
+            continue
+        have[e[0]] = run(e, keep)
+        man["entries"] = sorted(have.values(), key=lambda r: r["name"])
+        json.dump(man, open(man_path, "w"), indent=1)
+    # The reference's own committed render (mt19937, depth 0, AO 128, 500x500;
+    # provenance established in SURVEY.md §4) — kept gzipped as a data fixture.
+    if os.path.exists(REF_OUTPUT_PPM):
+        data = open(REF_OUTPUT_PPM, "rb").read()
+        with gzip.GzipFile(os.path.join(HERE, "reference_output.ppm.gz"), "wb", mtime=0) as f:
+            f.write(data)
+        man["reference_output_ppm"] = {
+            "file": "reference_output.ppm.gz", "sha256": hashlib.sha256(data).hexdigest(),
+            "scene": "simpleSphereScene.json", "width": 500, "height": 500, "depth": 0,
+            "ao_samples": 128, "ao_enabled": True, "rng": "mt19937",
+            "source": "580 Raytracer/output.ppm (committed by the reference authors)"}
+    json.dump(man, open(man_path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

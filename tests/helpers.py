@@ -1,0 +1,100 @@
+"""Shared test utilities: repository paths, golden manifest, the product's
+ctypes binding (580-raytracer_amd/rt580.py) and the oracle's (oracle/_build)."""
+import ctypes
+import functools
+import gzip
+import hashlib
+import importlib.util
+import json
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+ASSETS_ROOT = GOLDEN  # contains Assets/ (reference scene fixtures + synthetic scenes)
+PKG = os.path.join(REPO, "580-raytracer_amd")
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "librt_oracle.so")
+REFERENCE = "/root/reference/580 Raytracer"
+
+
+@functools.lru_cache(None)
+def rt580():
+    spec = importlib.util.spec_from_file_location("rt580", os.path.join(PKG, "rt580.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@functools.lru_cache(None)
+def manifest():
+    return json.load(open(os.path.join(GOLDEN, "manifest.json")))
+
+
+def golden_entries(with_ppm=True):
+    return [e for e in manifest()["entries"] if ("ppm" in e) == with_ppm]
+
+
+def golden_ppm(entry):
+    return open(os.path.join(GOLDEN, entry["ppm"]), "rb").read()
+
+
+def reference_output_ppm():
+    ro = manifest()["reference_output_ppm"]
+    with gzip.open(os.path.join(GOLDEN, ro["file"]), "rb") as f:
+        data = f.read()
+    assert hashlib.sha256(data).hexdigest() == ro["sha256"]
+    return ro, data
+
+
+def sha256(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def ppm_pixels(data):
+    """(h, w, 3) uint8 array from P6 bytes."""
+    parts = data.split(b"\n", 3)
+    assert parts[0] == b"P6"
+    w, h = map(int, parts[1].split())
+    return np.frombuffer(parts[3], dtype=np.uint8).reshape(h, w, 3)
+
+
+def diff_summary(a, b):
+    pa, pb = ppm_pixels(a), ppm_pixels(b)
+    if pa.shape != pb.shape:
+        return "shape %s vs %s" % (pa.shape, pb.shape)
+    d = np.abs(pa.astype(int) - pb.astype(int))
+    bad = np.argwhere(d.max(axis=2) > 0)
+    return "%d/%d pixels differ, max |d|=%d, first at (y,x)=%s" % (
+        len(bad), pa.shape[0] * pa.shape[1], d.max(), bad[:5].tolist())
+
+
+def build_oracle():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "oracle"], check=True)
+
+
+@functools.lru_cache(None)
+def oracle_lib():
+    build_oracle()
+    lib = ctypes.CDLL(ORACLE_LIB)
+    lib.oracle_render.restype = ctypes.c_int
+    lib.oracle_render.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 9 + \
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    return lib
+
+
+def oracle_render(scene, w, h, depth, ao_samples=128, ao_enabled=True, engine=0, threads=0,
+                  rows=None, root=ASSETS_ROOT):
+    """CPU restatement render -> (int16 (nrows, w, 3) framebuffer, counters dict)."""
+    lib = oracle_lib()
+    r0, r1 = rows if rows else (0, h)
+    fb = np.zeros((r1 - r0, w, 3), dtype=np.int16)
+    cnt = np.zeros(6, dtype=np.uint64)
+    st = lib.oracle_render(os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples,
+                           int(ao_enabled), engine, threads, r0, r1,
+                           fb.ctypes.data, cnt.ctypes.data, None)
+    assert st == 0, "oracle_render failed"
+    keys = ["rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"]
+    return fb, dict(zip(keys, (int(x) for x in cnt)))

@@ -1,0 +1,81 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's own
+outputs (golden PPMs made by oracle/_ref from /root/reference, the reference's
+committed output.ppm) and against the CPU restatement (oracle) on the same
+inputs. Bit-exact PPM bytes are required (integer-quantized output; the
+north_star's 1e-4 fp32 tolerance is below one 8-bit step)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def render_gpu(scene, w, h, depth, ao_samples, ao_enabled, rng=0, rows=None):
+    rt580 = helpers.rt580()
+    rt = rt580.Raytracer(w, h, helpers.ASSETS_ROOT)
+    assert rt.LoadSceneJSON(scene) == 0
+    rt.set_depth(depth)
+    rt.set_ao(ao_samples, ao_enabled)
+    rt.set_rng(rng)
+    if rows:
+        rt.set_rows(*rows)
+    st = rt.Render("")
+    assert st == 0, rt580.load().rt_gpu_last_error()
+    fb, stats = rt.framebuffer(), rt.stats()
+    rt.close()
+    return fb, stats
+
+
+@pytest.mark.parametrize("entry", helpers.golden_entries(True), ids=lambda e: e["name"])
+def test_golden_small(entry):
+    rng = 1 if entry["rng"] == "mt19937" else 0
+    fb, _ = render_gpu(entry["scene"], entry["width"], entry["height"], entry["depth"],
+                       entry["ao_samples"], entry["ao_enabled"], rng)
+    got = helpers.rt580().ppm_bytes(fb)
+    want = helpers.golden_ppm(entry)
+    assert got == want, helpers.diff_summary(got, want)
+
+
+def test_reference_output_ppm():
+    """The reference's committed 580 Raytracer/output.ppm (mt19937, depth 0, AO 128)."""
+    ro, want = helpers.reference_output_ppm()
+    fb, st = render_gpu(ro["scene"], ro["width"], ro["height"], ro["depth"], ro["ao_samples"],
+                        ro["ao_enabled"], rng=1)
+    got = helpers.rt580().ppm_bytes(fb)
+    assert got == want, helpers.diff_summary(got, want)
+    assert st["rays_total"] == 20368711  # oracle count for this configuration
+
+
+@pytest.mark.parametrize("entry", helpers.golden_entries(False), ids=lambda e: e["name"])
+def test_golden_big_sha(entry):
+    fb, st = render_gpu(entry["scene"], entry["width"], entry["height"], entry["depth"],
+                        entry["ao_samples"], entry["ao_enabled"])
+    got = helpers.rt580().ppm_bytes(fb)
+    assert helpers.sha256(got) == entry["sha256"]
+    if entry["name"].startswith("config2"):
+        assert st["rays_total"] == 124827951
+    if entry["name"].startswith("config1"):
+        assert st["rays_total"] == 601801
+
+
+@pytest.mark.parametrize("rows", [(0, 1), (5, 17), (30, 47), (46, 47)])
+def test_row_subset_matches_full_frame(rows):
+    full, _ = render_gpu("simpleSphereScene.json", 61, 47, 3, 8, True)
+    part, _ = render_gpu("simpleSphereScene.json", 61, 47, 3, 8, True, rows=rows)
+    assert np.array_equal(part[rows[0]:rows[1]], full[rows[0]:rows[1]])
+
+
+@pytest.mark.parametrize("scene,w,h,depth,ao", [
+    ("simpleSphereScene.json", 160, 120, 6, 32),
+    ("scene.json", 96, 72, 3, 8),
+    ("simpleSphereSceneAO.json", 128, 96, 8, 16),
+])
+def test_against_oracle(scene, w, h, depth, ao):
+    fb, st = render_gpu(scene, w, h, depth, ao, True)
+    ref, cnt = helpers.oracle_render(scene, w, h, depth, ao, True)
+    assert np.array_equal(fb, ref), "%d pixels differ" % int((fb != ref).any(axis=2).sum())
+    for k in ("rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"):
+        assert st[k] == cnt[k], k

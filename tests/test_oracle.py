@@ -1,0 +1,53 @@
+"""The CPU restatement (oracle/) pinned against the reference's own outputs:
+golden PPMs produced by the reference binary (tests/golden/make_golden.py),
+the reference's committed output.ppm, and the BASELINE hashes."""
+import filecmp
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import helpers
+
+
+@pytest.mark.parametrize("entry", helpers.golden_entries(True), ids=lambda e: e["name"])
+def test_oracle_matches_reference_golden(entry):
+    rng = 1 if entry["rng"] == "mt19937" else 0
+    fb, _ = helpers.oracle_render(entry["scene"], entry["width"], entry["height"], entry["depth"],
+                                  entry["ao_samples"], entry["ao_enabled"], rng)
+    got = helpers.rt580().ppm_bytes(fb)
+    assert got == helpers.golden_ppm(entry), helpers.diff_summary(got, helpers.golden_ppm(entry))
+
+
+def test_oracle_matches_reference_output_ppm():
+    ro, want = helpers.reference_output_ppm()
+    fb, cnt = helpers.oracle_render(ro["scene"], ro["width"], ro["height"], ro["depth"],
+                                    ro["ao_samples"], ro["ao_enabled"], engine=1)
+    assert helpers.rt580().ppm_bytes(fb) == want
+    assert cnt["rays_total"] == 20368711
+
+
+@pytest.mark.parametrize("name", ["config1_500_d1_aooff", "main_500_d4_ao128"])
+def test_oracle_big_hashes(name):
+    e = next(x for x in helpers.golden_entries(False) if x["name"] == name)
+    fb, cnt = helpers.oracle_render(e["scene"], e["width"], e["height"], e["depth"],
+                                    e["ao_samples"], e["ao_enabled"])
+    assert helpers.sha256(helpers.rt580().ppm_bytes(fb)) == e["sha256"]
+    if name.startswith("config1"):
+        assert cnt["rays_total"] == 601801
+
+
+def test_oracle_row_subsets_and_threads_agree():
+    full, c1 = helpers.oracle_render("simpleSphereScene.json", 64, 40, 4, 8, True, threads=1)
+    full8, c8 = helpers.oracle_render("simpleSphereScene.json", 64, 40, 4, 8, True, threads=8)
+    assert np.array_equal(full, full8) and c1 == c8
+    part, _ = helpers.oracle_render("simpleSphereScene.json", 64, 40, 4, 8, True, rows=(13, 29))
+    assert np.array_equal(part, full[13:29])
+
+
+@pytest.mark.skipif(not os.path.isdir(helpers.REFERENCE), reason="reference not mounted")
+def test_scene_fixtures_are_the_reference_assets():
+    ref = os.path.join(helpers.REFERENCE, "Assets")
+    for f in os.listdir(ref):
+        assert filecmp.cmp(os.path.join(ref, f), os.path.join(helpers.GOLDEN, "Assets", f), shallow=False), f
