@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <random>
 #include <string>
 #include <vector>
@@ -28,7 +29,12 @@ struct State {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_default[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t* ev = ev_default;       // events of the frame being enqueued
+    // bench profiling: one event quadruple per frame, summed at read time
+    bool profiling = false;
+    int prof_frames = 0;
+    std::vector<std::array<hipEvent_t, 4>> prof_pool;
     // scene
     DevBuf prims, shade, mats, lights;
     int n_prims = 0, n_lights = 0, n_ambient = 0, n_nonambient = 0;
@@ -177,6 +183,22 @@ int shade(const rt_render_params* p, int n_rows, const uint64_t* row_base_dev, i
     return RT_SUCCESS;
 }
 
+// Select the event quadruple for a new frame (profiling: a fresh slot per frame).
+int begin_frame() {
+    if (!g.profiling) {
+        g.ev = g.ev_default;
+        return RT_SUCCESS;
+    }
+    if ((int)g.prof_pool.size() <= g.prof_frames) {
+        std::array<hipEvent_t, 4> q;
+        for (auto& e : q) HIP_TRY(hipEventCreate(&e));
+        g.prof_pool.push_back(q);
+    }
+    g.ev = g.prof_pool[g.prof_frames].data();
+    g.prof_frames++;
+    return RT_SUCCESS;
+}
+
 }  // namespace
 
 extern "C" {
@@ -195,7 +217,8 @@ int rt_gpu_init(int device) {
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&g.own_stream, hipStreamNonBlocking));
     g.stream = g.own_stream;
-    for (auto& ev : g.ev) HIP_TRY(hipEventCreate(&ev));
+    for (auto& ev : g.ev_default) HIP_TRY(hipEventCreate(&ev));
+    g.ev = g.ev_default;
     upload_minstd_table(g.stream);
     HIP_TRY(hipGetLastError());
     g.inited = true;
@@ -252,6 +275,7 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
     if (!row_calls_device) return fail("row_calls_device is NULL");
     HIP_TRY(hipSetDevice(g.device));
     int n_rows = n_selected_rows(p);
+    if (begin_frame()) return RT_FAILURE;
     HIP_TRY(hipEventRecord(g.ev[0], g.stream));
     if (run_count(p, p->row_begin, p->row_step, n_rows, g.pix_calls, g.row_calls, g.row_tree, g.row_hits))
         return RT_FAILURE;
@@ -281,6 +305,7 @@ int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     HIP_TRY(hipSetDevice(g.device));
     const int n_rows = n_selected_rows(p);
     const bool prefix = p->row_begin == 0 && p->row_step == 1;
+    if (begin_frame()) return RT_FAILURE;
     HIP_TRY(hipEventRecord(g.ev[0], g.stream));
     // RNG offsets: the count pass must cover every row that precedes a selected row.
     if (ensure(g.row_base, (size_t)n_rows * 8 + 8)) return RT_FAILURE;
@@ -356,6 +381,32 @@ int rt_gpu_last_stats(rt_render_stats* st) {
     return RT_SUCCESS;
 }
 
+int rt_gpu_profile(int enable) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    g.profiling = enable != 0;
+    g.prof_frames = 0;
+    g.ev = g.ev_default;
+    return RT_SUCCESS;
+}
+
+int rt_gpu_profile_read(double* ms_count, double* ms_scan, double* ms_render, int* frames) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    double c = 0, s = 0, r = 0;
+    for (int i = 0; i < g.prof_frames; i++) {
+        float a = 0, b = 0, d = 0;
+        HIP_TRY(hipEventElapsedTime(&a, g.prof_pool[i][0], g.prof_pool[i][1]));
+        HIP_TRY(hipEventElapsedTime(&b, g.prof_pool[i][1], g.prof_pool[i][2]));
+        HIP_TRY(hipEventElapsedTime(&d, g.prof_pool[i][2], g.prof_pool[i][3]));
+        c += a; s += b; r += d;
+    }
+    if (ms_count) *ms_count = c;
+    if (ms_scan) *ms_scan = s;
+    if (ms_render) *ms_render = r;
+    if (frames) *frames = g.prof_frames;
+    return RT_SUCCESS;
+}
+
 const char* rt_gpu_last_error(void) { return g_err; }
 
 void rt_gpu_shutdown(void) {
@@ -366,8 +417,10 @@ void rt_gpu_shutdown(void) {
                       &g.row_tree, &g.row_hits, &g.row_base, &g.row_base_all, &g.fb, &g.mt_stream,
                       &g.cnt_calls_all, &g.cnt_tree_all, &g.cnt_hits_all, &g.cnt_pix_all})
         release(*b);
-    for (auto& ev : g.ev)
+    for (auto& ev : g.ev_default)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto& q : g.prof_pool)
+        for (auto& ev : q) (void)hipEventDestroy(ev);
     if (g.own_stream) (void)hipStreamDestroy(g.own_stream);
     g = State();
 }

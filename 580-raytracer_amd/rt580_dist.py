@@ -1,0 +1,81 @@
+"""Row-interleaved multi-rank rendering of one frame.
+
+One process per GPU. Rank r of G renders rows r, r+G, r+2G, ... (interleaved
+rows balance the work: sky rows are cheap). The reference draws every AO sample
+from ONE serial RNG stream in raster order (Raytracer.h:592, Raytracer.cpp:269-330),
+so a pixel's RNG position depends on the AO calls of all earlier pixels. The
+one exchange step is therefore:
+
+  1. each rank counts the AO calls of its rows           (backend.count)
+  2. all_gather of the per-row counts (H x int32)         (RCCL over xGMI / gloo)
+  3. every rank scans the full row vector in raster order -> its rows' RNG bases
+  4. each rank shades its rows                            (backend.shade)
+  5. gather of the int16 row tiles to rank 0, de-interleave
+
+Backends: GpuRows (lib580rt.so through the C ABI, device tensors) and, for the
+CPU tests of this logic with gloo, OracleRows in tests/.
+"""
+import ctypes
+
+
+def n_local_rows(height, rank, world):
+    return len(range(rank, height, world))
+
+
+def n_max_rows(height, world):
+    return (height + world - 1) // world
+
+
+class GpuRows:
+    """Phase 1/2 of the C-ABI split (rt_gpu_count_rows / rt_gpu_shade_rows)."""
+
+    def __init__(self, rt580, params, torch, device):
+        self.rt580, self.lib, self.torch, self.device = rt580, rt580.load(), torch, device
+        self.params = params
+        self.width, self.height = params.width, params.height
+
+    def _p(self, rank, world):
+        p = self.rt580.RenderParams.from_buffer_copy(self.params)
+        p.row_begin, p.row_end, p.row_step = rank, self.height, world
+        return p
+
+    def count(self, rank, world):
+        t = self.torch
+        out = t.zeros(n_max_rows(self.height, world), dtype=t.int32, device=self.device)
+        self._pc = self._p(rank, world)
+        self.rt580.check(self.lib.rt_gpu_count_rows(ctypes.byref(self._pc), out.data_ptr()), "rt_gpu_count_rows")
+        return out
+
+    def shade(self, rank, world, local_base):
+        t = self.torch
+        fb = t.empty(n_max_rows(self.height, world) * self.width * 3, dtype=t.int16, device=self.device)
+        self.rt580.check(self.lib.rt_gpu_shade_rows(ctypes.byref(self._pc), local_base.data_ptr(), fb.data_ptr()),
+                         "rt_gpu_shade_rows")
+        return fb
+
+
+def render_frame(backend, dist, torch, height, width, rank, world, gather=True):
+    """Render one frame across `world` ranks; returns the (H, W, 3) int16 frame
+    on rank 0 (None elsewhere, or the local tile when gather=False)."""
+    n_max = n_max_rows(height, world)
+    counts = backend.count(rank, world)                       # int32[n_max], zero padded
+    gathered = [torch.empty_like(counts) for _ in range(world)]
+    dist.all_gather(gathered, counts)
+    # row y lives on rank y % G at local index y // G
+    full = torch.stack(gathered, dim=1).reshape(-1)[:height].to(torch.int64)
+    base = torch.cumsum(full, 0) - full                       # exclusive scan, raster order
+    local = base[rank::world]
+    local_base = torch.zeros(n_max, dtype=torch.int64, device=counts.device)
+    local_base[:local.numel()] = local
+    fb = backend.shade(rank, world, local_base)               # int16[n_max*W*3]
+    if not gather:
+        return fb
+    # int16 has no RCCL/gloo dtype: the tiles travel as their bytes
+    fb_bytes = fb.view(torch.uint8)
+    if rank == 0:
+        tiles = [torch.empty_like(fb_bytes) for _ in range(world)]
+        dist.gather(fb_bytes, gather_list=tiles, dst=0)
+        frame = torch.stack([t.view(torch.int16).view(n_max, width, 3) for t in tiles], dim=1)
+        return frame.reshape(n_max * world, width, 3)[:height]
+    dist.gather(fb_bytes, dst=0)
+    return None

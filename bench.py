@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X per-pixel ray-trace path (BASELINE.json metric:
+"Mrays/sec + ms/frame at 1920x1080, depth=4, 64 AO samples; 1/2/4/8 GPU").
+
+A step = one frame of BASELINE config 2 (simpleSphereScene.json, 1920x1080,
+depth 4, 64 AO samples; the reference's scene file, synthetic = none needed)
+rendered from scratch: count pass + RNG-offset scan + shading kernel (+ for
+N > 1 the all-gather of per-row AO counts and the RCCL gather of the row tiles
+to rank 0). The scene is resident in HBM; the framebuffer stays in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line (metric, value = whole-job Mrays/s, ms_per_step,
+roofline of the shading kernel, cpu_baseline = the reference itself timed on
+this host's cores on a bounded sample).
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+SCENE, WIDTH, HEIGHT, DEPTH, AO = "simpleSphereScene.json", 1920, 1080, 4, 64
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# CPU baseline sample: the same scene/depth/AO at 1/16 of the pixels (480x270),
+# rendered by the reference binary (oracle/_ref) on one core.
+CPU_SAMPLE = (480, 270)
+
+
+def env_int(k, d):
+    try:
+        return int(os.environ.get(k, d))
+    except ValueError:
+        return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import helpers
+
+    rank, world = env_int("RANK", 0), env_int("WORLD_SIZE", 1)
+    local_rank = env_int("LOCAL_RANK", 0)
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    rt580.check(lib.rt_gpu_init(local_rank), "rt_gpu_init")
+    stream = torch.cuda.current_stream(device)
+    rt580.check(lib.rt_gpu_set_stream(ctypes.c_void_p(stream.cuda_stream)), "rt_gpu_set_stream")
+
+    rt = rt580.Raytracer(WIDTH, HEIGHT, helpers.ASSETS_ROOT)
+    assert rt.LoadSceneJSON(SCENE) == 0, "LoadSceneJSON failed"
+    rt.set_depth(DEPTH)
+    rt.set_ao(AO, True)
+    assert rt.InitializeRenderer() == 0
+    params = rt.render_params()
+    scene = rt.scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(scene)), "rt_gpu_upload_scene")
+    prims = [scene.prims[i] for i in range(scene.n_prims)]
+    n_tri = sum(1 for p in prims if p.kind == 0)
+    n_sph = len(prims) - n_tri
+
+    fbp = ctypes.c_void_p()
+    dist_mod = helpers.rt580_dist() if world > 1 else None
+    backend = dist_mod.GpuRows(rt580, params, torch, device) if world > 1 else None
+
+    def step():
+        if world == 1:
+            rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(fbp)), "rt_gpu_render_device")
+        else:
+            dist_mod.render_frame(backend, dist, torch, HEIGHT, WIDTH, rank, world)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # rays of one frame (this rank's rows), from the count pass of the last frame
+    st = rt580.RenderStats()
+    rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "rt_gpu_last_stats")
+    local = st.as_dict()
+
+    rt580.check(lib.rt_gpu_profile(1), "rt_gpu_profile")
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    c_ms, s_ms, r_ms, frames = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    rt580.check(lib.rt_gpu_profile_read(ctypes.byref(c_ms), ctypes.byref(s_ms), ctypes.byref(r_ms),
+                                        ctypes.byref(frames)), "rt_gpu_profile_read")
+    rt580.check(lib.rt_gpu_profile(0), "rt_gpu_profile")
+
+    rays_local = int(local["rays_total"])
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        r = torch.tensor([rays_local], dtype=torch.int64, device=device)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays_frame = int(r.item())
+    else:
+        rays_frame = rays_local
+
+    if rank == 0:
+        value = rays_frame * args.steps / dt / 1e6
+        bytes_per_ray = 56 * n_tri + 16 * n_sph  # SoA primitive records, no reuse
+        render_ms = r_ms.value / max(frames.value, 1)
+        achieved = rays_local * bytes_per_ray / (render_ms * 1e-3) / 1e9 if render_ms > 0 else 0.0
+        out = {
+            "metric": "Mrays/sec (+ ms/frame) at 1920x1080, depth=4, 64 AO samples",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "reference scene file Assets/simpleSphereScene.json (no dataset needed)",
+            "config": {
+                "workload": "BASELINE config 2: simpleSphereScene.json 1920x1080 depth=4 AO=64",
+                "scene": SCENE, "width": WIDTH, "height": HEIGHT, "depth": DEPTH, "ao_samples": AO,
+                "rng": "minstd_rand0 (libstdc++ default_random_engine)",
+                "rays_per_frame": rays_frame,
+                "parallelism": "interleaved rows x%d + RCCL all_gather/gather" % world if world > 1 else "1 GPU",
+            },
+            "kernel_ms_per_frame": {
+                "count": round(c_ms.value / max(frames.value, 1), 4),
+                "scan": round(s_ms.value / max(frames.value, 1), 4),
+                "render": round(render_ms, 4),
+            },
+            "roofline": {
+                "kernel": "render_kernel",
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": measured_traffic(),
+                "bytes_per_ray": bytes_per_ray,
+                "note": "algorithmic scene-stream bytes (56*T + 16*S per ray, SURVEY §8d) x rays of one "
+                        "launch / mean render_kernel duration (HIP events on its stream); the kernel itself "
+                        "is VALU-bound (scene of %d prims stays in scalar cache)" % len(prims),
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(lib, rt580, helpers, params)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def measured_traffic():
+    """HBM bytes per render_kernel launch from the committed rocprofv3 --pmc
+    summary (profiles/), corrected per MI355X_MICROARCH.md §HBM; None if absent."""
+    path = os.path.join(REPO, "profiles", "pmc_render_kernel.json")
+    if os.path.exists(path):
+        try:
+            return json.load(open(path)).get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            return None
+    return None
+
+
+def cpu_baseline(lib, rt580, helpers, params):
+    """The reference binary (oracle/_ref, built from /root/reference's own
+    sources) on one core, on a bounded sample of the same workload."""
+    w, h = CPU_SAMPLE
+    exe = os.path.join(REPO, "oracle", "_ref", "rt_ref_param")
+    root = os.path.join(REPO, "oracle", "_ref", "root")
+    # rays of the sample frame: the GPU count pass of the same configuration
+    rt = rt580.Raytracer(w, h, helpers.ASSETS_ROOT)
+    assert rt.LoadSceneJSON(SCENE) == 0
+    rt.set_depth(DEPTH)
+    rt.set_ao(AO, True)
+    assert rt.InitializeRenderer() == 0
+    p = rt.render_params()
+    fb = (ctypes.c_int16 * (w * h * 3))()
+    rt580.check(lib.rt_gpu_render(ctypes.byref(p), fb), "rt_gpu_render (sample)")
+    st = rt580.RenderStats()
+    rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "stats")
+    rays = int(st.rays_total)
+    kind = "reference"
+    if os.path.exists(exe):
+        t0 = time.perf_counter()
+        pr = subprocess.run(["taskset", "-c", "0", exe, root, SCENE, str(w), str(h), str(DEPTH), "/dev/null",
+                             str(AO), "0"], capture_output=True, text=True)
+        wall = time.perf_counter() - t0
+        secs = wall
+        for line in pr.stderr.splitlines():
+            if line.startswith("render_seconds="):
+                secs = float(line.split()[0].split("=")[1])
+        if pr.returncode != 0:
+            return {"value": None, "error": pr.stderr[-300:]}
+    else:
+        kind = "port"
+        t0 = time.perf_counter()
+        _, cnt = helpers.oracle_render(SCENE, w, h, DEPTH, AO, True, threads=1)
+        secs = time.perf_counter() - t0
+        rays = cnt["rays_total"]
+    cpu = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(rays / secs / 1e6, 4),
+        "unit": "Mrays/s",
+        "cores": 1,
+        "kind": kind,
+        "seconds": round(secs, 3),
+        "rays": rays,
+        "cpu": cpu,
+        "sample": "%s %dx%d depth=%d AO=%d (1/16 of config 2's pixels), single thread, "
+                  "oracle/_ref/rt_ref_param = reference Raytracer.cpp with the AO count as a parameter"
+                  % (SCENE, w, h, DEPTH, AO),
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -170,6 +170,11 @@ int rt_gpu_shade_rows(const rt_render_params* params, const uint64_t* row_base_d
                       int16_t* fb_device);
 /* Counters and HIP-event timings of the last render. */
 int rt_gpu_last_stats(rt_render_stats* stats);
+/* Bench profiling: with enable=1 every following frame records its own HIP
+ * events (count pass, scan, render kernel) on the shim's stream; profile_read
+ * synchronizes and returns the sums over those frames. */
+int rt_gpu_profile(int enable);
+int rt_gpu_profile_read(double* ms_count, double* ms_scan, double* ms_render, int* frames);
 /* Last error message (static storage). */
 const char* rt_gpu_last_error(void);
 void rt_gpu_shutdown(void);

@@ -723,6 +723,77 @@ extern "C" int oracle_render(const char* assets_root, const char* scene, int w, 
     return 0;
 }
 
+// ---- row-level entry points (the multi-rank split of SURVEY §8e, for tests) ----
+namespace {
+struct Loaded {
+    Scene sc;
+    Camera2 cam;
+    Tracer tr;
+};
+int load_all(Loaded& L, const char* root, const char* scene, int w, int h, int depth, int ao_n, int ao_on) {
+    if (w <= 0 || h <= 0 || depth < 0 || ao_n <= 0) return 2;
+    if (load_scene(L.sc, root, scene) != 0) return 1;
+    for (const Shape& s : L.sc.shapes)
+        if (s.mesh < 0) return 1;
+    L.cam = init_camera(L.sc, w, h);
+    L.tr.sc = &L.sc;
+    L.tr.depth = depth;
+    L.tr.ao_n = ao_n;
+    L.tr.ao_on = ao_on;
+    L.tr.ao_bmax = (float)(2 * kPI);
+    L.tr.n_amb = 0;
+    return 0;
+}
+}  // namespace
+
+// AO calls of rows row_begin + k*row_step (k < n_rows) -> out[k].
+extern "C" int oracle_count_rows(const char* root, const char* scene, int w, int h, int depth, int ao_n,
+                                 int ao_on, int row_begin, int row_step, int n_rows, uint32_t* out) {
+    Loaded L;
+    int st = load_all(L, root, scene, w, h, depth, ao_n, ao_on);
+    if (st) return st;
+    for (int k = 0; k < n_rows; k++) {
+        int y = row_begin + k * row_step;
+        uint64_t calls = 0;
+        for (int x = 0; x < w; x++) {
+            Counters c;
+            L.tr.raycast(generate_ray(L.cam, x, y), depth, nullptr, c, true);
+            calls += c.ao_calls;
+        }
+        out[k] = (uint32_t)calls;
+    }
+    return 0;
+}
+
+// Shade the same rows given each row's absolute first AO-call index (minstd_rand0).
+extern "C" int oracle_shade_rows(const char* root, const char* scene, int w, int h, int depth, int ao_n,
+                                 int ao_on, int row_begin, int row_step, int n_rows, const uint64_t* row_base,
+                                 int16_t* fb) {
+    Loaded L;
+    int st = load_all(L, root, scene, w, h, depth, ao_n, ao_on);
+    if (st) return st;
+    DrawSource src;
+    src.engine = 0;
+    RngCursor rng;
+    rng.src = &src;
+    const uint64_t per_call = 2ull * (uint64_t)ao_n;
+    for (int k = 0; k < n_rows; k++) {
+        int y = row_begin + k * row_step;
+        uint64_t call = row_base[k];
+        for (int x = 0; x < w; x++) {
+            Counters cc;
+            L.tr.raycast(generate_ray(L.cam, x, y), depth, nullptr, cc, true);  // this pixel's AO calls
+            rng.seek(ao_on ? call * per_call : 0);
+            Counters c;
+            Pix p = L.tr.raycast(generate_ray(L.cam, x, y), depth, &rng, c, false);
+            int16_t* o = fb + ((size_t)k * w + x) * 3;
+            o[0] = p.r; o[1] = p.g; o[2] = p.b;
+            call += cc.ao_calls;
+        }
+    }
+    return 0;
+}
+
 // FlushFrameBufferToPPM, Raytracer.cpp:796-830
 extern "C" int oracle_write_ppm(const char* path, int w, int h, const int16_t* fb) {
     std::ofstream out(path, std::ios::binary);

@@ -32,6 +32,15 @@ int oracle_render(const char* assets_root, const char* scene, int w, int h, int 
                   int ao_samples, int ao_enabled, int engine, int threads, int row_begin,
                   int row_end, int16_t* fb, uint64_t* counters, uint64_t* rays_per_row);
 
+// Multi-rank split for the distributed-logic tests: AO calls per
+// selected row, then shading of those rows given each row's RNG base (the
+// absolute index of its first AO call). Rows: row_begin + k*row_step, k < n_rows.
+int oracle_count_rows(const char* assets_root, const char* scene, int w, int h, int depth, int ao_samples,
+                      int ao_enabled, int row_begin, int row_step, int n_rows, uint32_t* out);
+int oracle_shade_rows(const char* assets_root, const char* scene, int w, int h, int depth, int ao_samples,
+                      int ao_enabled, int row_begin, int row_step, int n_rows, const uint64_t* row_base,
+                      int16_t* fb);
+
 // Writes the reference's P6 output (FlushFrameBufferToPPM, Raytracer.cpp:796-830).
 int oracle_write_ppm(const char* path, int w, int h, const int16_t* fb);
 

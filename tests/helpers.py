@@ -98,3 +98,42 @@ def oracle_render(scene, w, h, depth, ao_samples=128, ao_enabled=True, engine=0,
     assert st == 0, "oracle_render failed"
     keys = ["rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"]
     return fb, dict(zip(keys, (int(x) for x in cnt)))
+
+
+@functools.lru_cache(None)
+def rt580_dist():
+    spec = importlib.util.spec_from_file_location("rt580_dist", os.path.join(PKG, "rt580_dist.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+class OracleRows:
+    """CPU backend of rt580_dist.render_frame (count/shade rows with the oracle),
+    used to test the multi-rank exchange logic under gloo without a GPU."""
+
+    def __init__(self, scene, w, h, depth, ao_samples, ao_enabled=True, root=ASSETS_ROOT):
+        import torch
+        self.torch = torch
+        self.args = (os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples, int(ao_enabled))
+        self.width, self.height = w, h
+        lib = oracle_lib()
+        lib.oracle_count_rows.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 8 + [ctypes.c_void_p]
+        lib.oracle_shade_rows.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 8 + \
+            [ctypes.c_void_p, ctypes.c_void_p]
+        self.lib = lib
+
+    def count(self, rank, world):
+        d = rt580_dist()
+        n_loc, n_max = d.n_local_rows(self.height, rank, world), d.n_max_rows(self.height, world)
+        out = np.zeros(n_max, dtype=np.uint32)
+        assert self.lib.oracle_count_rows(*self.args, rank, world, n_loc, out.ctypes.data) == 0
+        return self.torch.from_numpy(out.astype(np.int32))
+
+    def shade(self, rank, world, local_base):
+        d = rt580_dist()
+        n_loc, n_max = d.n_local_rows(self.height, rank, world), d.n_max_rows(self.height, world)
+        base = np.ascontiguousarray(local_base.numpy().astype(np.uint64))
+        fb = np.zeros(n_max * self.width * 3, dtype=np.int16)
+        assert self.lib.oracle_shade_rows(*self.args, rank, world, n_loc, base.ctypes.data, fb.ctypes.data) == 0
+        return self.torch.from_numpy(fb)
