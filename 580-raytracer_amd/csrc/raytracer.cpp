@@ -28,7 +28,7 @@ int Raytracer::LoadSceneJSON(const std::string scenePath) {
         if (s.mesh < 0) return RT_FAILURE;
     rt580::pack_scene(mScene, mPacked);
     mSceneValid = true;
-    std::cout << "Scene parsing completed!\n";  // Raytracer.cpp:772
+    std::cerr << "Scene parsing completed!\n";  // Raytracer.cpp:772 (stderr: keep stdout for results)
     return RT_SUCCESS;
 }
 

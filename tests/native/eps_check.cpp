@@ -1,0 +1,42 @@
+// Exhaustive check over all 2^32 float bit patterns that the float-only EPSILON
+// comparisons of rt_math.h equal the reference's double comparisons:
+//   (double)x < 1e-6  (Raytracer.cpp:17, :427),  (double)x <= 1e-6 (:382),
+//   (double)x > 1e-6  (GreaterThanZero, Raytracer.h:558-560),
+// and that rt_f2s matches the x86-64 cvttss2si-based static_cast<short>(float).
+#include "../../580-raytracer_amd/csrc/rt_math.h"
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+static inline int32_t cvttss2si(float f) {
+    int32_t r;
+    __asm__("cvttss2si %1, %0" : "=r"(r) : "x"(f));
+    return r;
+}
+
+int main() {
+    std::atomic<long> bad{0};
+    unsigned nt = std::thread::hardware_concurrency();
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++)
+        th.emplace_back([&, t] {
+            long b = 0;
+            uint64_t lo = (1ull << 32) * t / nt, hi = (1ull << 32) * (t + 1) / nt;
+            for (uint64_t u = lo; u < hi; u++) {
+                uint32_t v = (uint32_t)u;
+                float x;
+                std::memcpy(&x, &v, 4);
+                double d = x;
+                if (rt_lt_eps(x) != (d < 1e-6)) b++;
+                if (rt_lt_eps(x) != (d <= 1e-6)) b++;
+                if (rt_gt_eps(x) != (d > 1e-6)) b++;
+                if (rt_f2s(x) != (int32_t)(int16_t)(uint16_t)(uint32_t)cvttss2si(x)) b++;
+            }
+            bad += b;
+        });
+    for (auto& x : th) x.join();
+    std::printf("mismatches=%ld\n", bad.load());
+    return bad.load() ? 1 : 0;
+}

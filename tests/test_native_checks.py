@@ -1,0 +1,49 @@
+"""CPU checks of the bit-exactness building blocks used by the HIP kernels:
+the glibc powf/sincos restatements (rt_libm.h) against this machine's glibc,
+exhaustively over the inputs the reference's path can produce, and the float
+EPSILON comparisons / float->short conversion of rt_math.h over all 2^32 floats."""
+import os
+import subprocess
+
+import pytest
+
+import helpers
+
+NATIVE = os.path.join(helpers.REPO, "tests", "native")
+BUILD = os.path.join(NATIVE, "_build")
+FLAGS = ["-O2", "-std=c++17", "-ffp-contract=off", "-pthread"]
+
+
+def _build(name):
+    os.makedirs(BUILD, exist_ok=True)
+    exe = os.path.join(BUILD, name)
+    src = os.path.join(NATIVE, name + ".cpp")
+    subprocess.run(["g++"] + FLAGS + ["-o", exe, src], check=True)
+    return exe
+
+
+def _run(exe, *args):
+    p = subprocess.run([exe] + list(args), capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "mismatches=0" in p.stdout
+    return p.stdout
+
+
+def test_sincos_exhaustive_over_ao_angles():
+    """Every float angle in [0, 2*pi): the AO sampler's domain (Raytracer.cpp:270-278)."""
+    out = _run(_build("libm_check"), "sincos")
+    assert "checked=1086918619" in out
+
+
+def test_powf_exhaustive_over_scene_exponents():
+    """Every float x in [0, 1.0001] for each specular exponent in the scene assets
+    (Raytracer.cpp:253; fmax(dot(V,R),0) of unit vectors)."""
+    _run(_build("libm_check"), "powf", "2", "5", "10", "20", "700", "900")
+
+
+def test_powf_random_pairs():
+    _run(_build("libm_check"), "powf_random", "20000000")
+
+
+def test_eps_compares_and_float_to_short_all_floats():
+    _run(_build("eps_check"))
