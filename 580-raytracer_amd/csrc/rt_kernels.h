@@ -1,12 +1,12 @@
-// rt_kernels.h — device-side views and launchers (rt_kernels.hip), used by rt_shim.cpp.
+// rt_kernels.h — device-side views, per-frame workspace and launchers
+// (rt_kernels.hip), used by rt_shim.cpp.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/rt580.h"
 
-// Deepest recursion supported by the fixed-size frame stack (reference default 4;
-// BASELINE config 5 uses 8).
+// Deepest recursion supported (reference default 4; BASELINE config 5 uses 8).
 #define RT_MAX_DEPTH 16
 
 namespace rt580 {
@@ -18,6 +18,7 @@ struct DevScene {
     const rt_light* lights;
     int n_prims;
     int n_lights;
+    int n_ambient;
 };
 
 struct DevFrame {
@@ -25,23 +26,68 @@ struct DevFrame {
     uint32_t rng_seed;
     int row_begin, row_step, n_rows;  // local row k is frame row row_begin + k*row_step
     int view_inverse_ok;
-    int n_ambient;
     float view_inv[9];
     float cam_from[3];
     float ao_angle_max;
     double ndc_kx, ndc_ky;
-    const uint32_t* mt_stream;  // RT_RNG_MT19937 draws (absolute index), else null
+};
+
+// One node of the reflect/refract recursion tree (a Raycast call). 64 bytes.
+struct NodeRec {
+    float hp[3];          // hit point (hitInfo.hitPoint)
+    float n[3];           // geometric normal (hitInfo.normal)
+    int32_t child[2];     // reflection / refraction child node ids, -1: none
+    int32_t local_rg;     // non-ambient local colour: r | g << 16 (int16 each)
+    int32_t local_b_flags;// b | flags << 16
+    float kr, kt;         // ComputeFresnel
+    int32_t shape;        // material index
+    uint32_t call0;       // first AO call (local index) of this node
+    int32_t pad[2];
+};
+#define RT_NODE_HIT 1
+#define RT_NODE_LEAF 2  // bounces == 0: no combine
+
+// A queued tree ray (child of a node of the previous level). 32 bytes.
+struct RayItem {
+    float o[3];
+    float d[3];
+    int32_t pixel;  // local pixel index
+    int32_t pad;
+};
+
+// Per-frame device workspace (owned by the shim, sized by capacity).
+struct DevWork {
+    NodeRec* nodes;        // [node_cap]
+    RayItem* rays;         // [node_cap] (indexed by node id; level 0 is implicit)
+    uint32_t* lvl;         // [2 * (RT_MAX_DEPTH + 2)]: counts then bases
+    uint32_t* needed;      // [1] highest node id requested + 1 (overflow check)
+    uint32_t* pix_hits;    // [npix]
+    uint32_t* pix_nodes;   // [npix]
+    uint32_t* pix_prefix;  // [npix] in-row exclusive prefix of AO calls
+    uint32_t* row_calls;   // [n_rows]
+    uint32_t* row_hits;    // [n_rows]
+    uint32_t* row_nodes;   // [n_rows]
+    uint64_t* row_base_local;  // [n_rows] exclusive scan of this call's rows
+    uint64_t* totals;      // [2]: total local AO calls, spare
+    uint32_t* call_node;   // [call_cap]
+    uint64_t* call_rng;    // [call_cap] minstd state at the call's first draw / mt19937 global call index
+    uint32_t* occ;         // [call_cap] occluded samples
+    const uint32_t* mt_stream;  // mt19937 draws (absolute index), else null
+    uint32_t node_cap;
+    uint32_t call_cap;
 };
 
 void upload_minstd_table(hipStream_t s);
-hipError_t launch_count(const DevScene& S, const DevFrame& F, uint32_t* pix_calls, uint32_t* row_calls,
-                        uint32_t* row_tree, uint32_t* row_hits, hipStream_t s);
-hipError_t launch_row_base(const uint32_t* row_calls, int n_rows, uint64_t* row_base, hipStream_t s);
-hipError_t launch_pixel_base(const uint32_t* pix_calls, int width, int n_rows, const uint64_t* row_base,
-                             uint64_t* pix_base, hipStream_t s);
-hipError_t launch_render(const DevScene& S, const DevFrame& F, const uint64_t* pix_base, int16_t* fb,
-                         hipStream_t s);
-hipError_t launch_select_rows(const uint64_t* all_base, int row_begin, int row_step, int n_rows,
-                              uint64_t* sel_base, hipStream_t s);
+// Breadth-first trace of all levels: nodes, shading except AO, per-pixel counters.
+hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s);
+// Per-row AO-call totals + in-row prefixes, then the local row scan.
+hipError_t launch_row_counts(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s);
+// AO-call numbering (RNG positions) from the global row bases (nullptr: local scan).
+hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, const uint64_t* row_base_global,
+                       hipStream_t s);
+hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s);
+hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s);
+hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows,
+                            int16_t* dst, hipStream_t s);
 
 }  // namespace rt580

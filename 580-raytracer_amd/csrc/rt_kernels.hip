@@ -5,73 +5,70 @@
 //   CalculateAmbientOcclusion (:269-330) / ComputeFresnel (:131-166) /
 //   CalculateRefraction (:168-203).
 //
-// Pipeline for one frame (or one rank's interleaved rows):
-//   1. count_kernel   one thread per pixel walks the reflect/refract tree with
-//                     closest-hit queries only and counts the AO calls (hit nodes x
-//                     ambient lights) and rays; per-row totals by wave-reduced atomics.
-//   2. row_base_kernel exclusive scan of per-row AO calls (raster order) -> the
-//                     absolute index of each row's first AO call in the reference's
-//                     single serial RNG stream (skipped when the caller supplies it,
-//                     e.g. after an all-gather of per-row counts across ranks).
-//   3. render_kernel  one thread per pixel: in-row prefix of AO calls (wave scan +
-//                     LDS), RNG skip-ahead, iterative fixed-depth reflect/refract
-//                     stack, shading, AO, int16 Pixel blend; writes Pixel[w] rows.
+// Wavefront organisation of one frame (or one rank's interleaved rows):
+//   trace_kernel x (depth+1)  breadth-first over the levels of Raycast's binary
+//        recursion tree: level 0 = camera rays, level L+1 = the reflection and
+//        refraction children of level L's hits, kept in compacted queues (wave-
+//        aggregated atomics). Each tree ray: closest hit, shadow rays, the
+//        non-ambient local colour, Fresnel, children -> one NodeRec.
+//   row_counts_kernel / row_scan_kernel  AO calls per pixel (hits x ambient
+//        lights) -> in-row prefixes, per-row totals, scan over this call's rows.
+//   rank_kernel   per pixel: pre-order walk of the pixel's tree numbers its AO
+//        calls exactly as the reference's serial RNG consumes them (raster order,
+//        then pre-order, then lights) and records each call's RNG position.
+//   ao_kernel     flat over (AO call, sample): every lane one hemisphere sample,
+//        any-hit against the scene; perfectly balanced (95% of all rays).
+//   resolve_kernel per pixel: post-order int16 blend of the tree (the blend is
+//        non-linear, so it runs bottom-up after AO is known).
+// Scene loops stage primitives in LDS tiles read uniformly by the workgroup.
 //
-// Bit-exactness rules: compiled with -ffp-contract=off; fp32
-// division/sqrt correctly rounded (hipcc default); denormals preserved; glibc
-// powf/sincos restated in rt_libm.h; double only where the reference is double.
+// Bit-exactness rules: -ffp-contract=off; correctly rounded fp32
+// division/sqrt (hipcc default); denormals preserved; glibc powf/sincos restated
+// in rt_libm.h; double precision only where the reference uses double.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/rt580.h"
+#include "rt_kernels.h"
 #include "rt_libm.h"
 #include "rt_math.h"
-#include "rt_kernels.h"
 
 namespace rt580 {
+
+#define TB 256    // threads per workgroup (4 waves)
+#define TILE 64   // primitives per LDS tile (4 KiB)
+#define LVL_BASE (RT_MAX_DEPTH + 2)
 
 // ---------------------------------------------------------------- RNG
 // minstd_rand0: x' = 16807 x mod (2^31-1), seed 1 (libstdc++ default_random_engine).
 __device__ __forceinline__ uint32_t mersenne31_mul(uint32_t a, uint32_t b) {
-    uint64_t p = (uint64_t)a * (uint64_t)b;              // < 2^62
-    uint64_t r = (p & 0x7fffffffull) + (p >> 31);         // < 2^32
-    r = (r & 0x7fffffffull) + (r >> 31);                  // <= 2^31
+    uint64_t p = (uint64_t)a * (uint64_t)b;       // < 2^62
+    uint64_t r = (p & 0x7fffffffull) + (p >> 31);  // < 2^32
+    r = (r & 0x7fffffffull) + (r >> 31);           // <= 2^31
     uint32_t v = (uint32_t)r;
     return v >= 0x7fffffffu ? v - 0x7fffffffu : v;
 }
 
-// a^(2^i) mod m, i = 0..30, for O(31) skip-ahead (filled by the host).
-__constant__ uint32_t c_minstd_pow2[32];
+__constant__ uint32_t c_minstd_pow2[32];   // 16807^(2^i) mod m
+__constant__ uint32_t c_minstd_j1[512];    // 16807^(2s+1) mod m: state offset of sample s's first draw
 
-__device__ __forceinline__ uint32_t minstd_jump(uint32_t state, uint64_t k) {
-    k %= 2147483646ull;  // period of a primitive root mod 2^31-1
+__device__ __forceinline__ uint32_t minstd_pow(uint32_t state, uint64_t k) {
+    k %= 2147483646ull;  // period: 16807 is a primitive root mod 2^31-1
     uint32_t s = state;
     for (int i = 0; i < 31; i++)
         if ((k >> i) & 1ull) s = mersenne31_mul(s, c_minstd_pow2[i]);
     return s;
 }
 
-struct Rng {
-    uint64_t index;       // draws consumed (absolute position in the global stream)
-    uint32_t state;       // minstd state after `index` draws
-    int engine;
-    const uint32_t* mt;   // mt19937 outputs (engine 1)
-
-    __device__ __forceinline__ float canonical() {
-        float ret;
-        if (engine == RT_RNG_MINSTD_RAND0) {
-            state = mersenne31_mul(state, 16807u);
-            ret = (float)(state - 1u) / 2147483648.0f;   // generate_canonical<float,24>, r = 2^31-2
-        } else {
-            ret = (float)mt[index] / 4294967296.0f;      // r = 2^32
-        }
-        index++;
-        if (ret >= 1.0f) ret = 0x1.fffffep-1f;           // nextafter(1, 0)
-        return ret;
-    }
-    // uniform_real_distribution<float>::operator(): canonical * (b - a) + a
-    __device__ __forceinline__ float uniform(float a, float b) { return canonical() * (b - a) + a; }
-};
+// generate_canonical<float,24> (libstdc++ random.tcc:3348-3378) for one draw.
+__device__ __forceinline__ float canon_minstd(uint32_t x) {  // r = 2^31-2 -> tmp = 2^31 (float)
+    float r = (float)(x - 1u) / 2147483648.0f;
+    return r >= 1.0f ? 0x1.fffffep-1f : r;
+}
+__device__ __forceinline__ float canon_mt(uint32_t x) {      // r = 2^32
+    float r = (float)x / 4294967296.0f;
+    return r >= 1.0f ? 0x1.fffffep-1f : r;
+}
 
 // ---------------------------------------------------------------- scene queries
 struct Hit {
@@ -86,18 +83,15 @@ __device__ __forceinline__ bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& 
                                          float& g) {
     rv3 N = ld3(P.nrm);
     float nd = v3_dot(N, d);
-    if (rt_lt_eps(fabsf(nd))) return false;            // NearlyEquals(nd, 0)
+    if (rt_lt_eps(fabsf(nd))) return false;  // NearlyEquals(nd, 0)
     t = -(v3_dot(N, o) + P.d) / nd;
-    if (rt_lt_eps(t)) return false;                     // t <= EPSILON
+    if (rt_lt_eps(t)) return false;           // t <= EPSILON
     rv3 Pp = v3_add(o, v3_scale(d, t));
     rv3 v0 = ld3(P.p0), v1 = ld3(P.p1), v2 = ld3(P.p2);
     // CalcTriangleAreaSigned (Raytracer.cpp:937-942): 0.5 * dot(cross(B-A, C-A), N)
-    float aa = 0.5f * v3_dot(v3_cross(v3_sub(v1, Pp), v3_sub(v2, Pp)), N);
-    a = aa / P.area;
-    float bb = 0.5f * v3_dot(v3_cross(v3_sub(Pp, v0), v3_sub(v2, v0)), N);
-    b = bb / P.area;
-    float gg = 0.5f * v3_dot(v3_cross(v3_sub(v1, v0), v3_sub(Pp, v0)), N);
-    g = gg / P.area;
+    a = (0.5f * v3_dot(v3_cross(v3_sub(v1, Pp), v3_sub(v2, Pp)), N)) / P.area;
+    b = (0.5f * v3_dot(v3_cross(v3_sub(Pp, v0), v3_sub(v2, v0)), N)) / P.area;
+    g = (0.5f * v3_dot(v3_cross(v3_sub(v1, v0), v3_sub(Pp, v0)), N)) / P.area;
     return !(a < 0 || b < 0 || g < 0);
 }
 
@@ -119,31 +113,60 @@ __device__ __forceinline__ bool sph_test(const rt_prim& P, rv3 o, rv3 d, float& 
     return true;
 }
 
-// IntersectScene, closest hit: primitives in the reference's order, the first
-// hit is taken unconditionally and later ones only if strictly closer (:487-498).
-__device__ bool closest_hit(const DevScene& S, rv3 o, rv3 d, Hit& h) {
+// Stage primitives [base, base+n) in LDS (every thread of the workgroup calls it).
+__device__ __forceinline__ void load_tile(const rt_prim* __restrict__ prims, int base, int n, rt_prim* tile) {
+    const float4* src = reinterpret_cast<const float4*>(prims + base);
+    float4* dst = reinterpret_cast<float4*>(tile);
+    for (int i = threadIdx.x; i < n * 4; i += blockDim.x) dst[i] = src[i];
+}
+
+// IntersectScene, closest hit (Raytracer.cpp:473-526): primitives in the
+// reference's order; the first hit is taken unconditionally, later ones only if
+// strictly closer. Workgroup-uniform call; `active` lanes test.
+__device__ bool closest_hit(const DevScene& S, rt_prim* tile, bool active, rv3 o, rv3 d, Hit& h) {
     bool found = false;
-    for (int i = 0; i < S.n_prims; i++) {
-        const rt_prim P = S.prims[i];
-        float t, a = 0, b = 0, g = 0;
-        bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
-        if (hit && (!found || t < h.t)) {
-            found = true;
-            h.t = t; h.a = a; h.b = b; h.g = g; h.prim = i;
+    for (int base = 0; base < S.n_prims; base += TILE) {
+        const int n = min(TILE, S.n_prims - base);
+        __syncthreads();
+        load_tile(S.prims, base, n, tile);
+        __syncthreads();
+        if (active) {
+            for (int j = 0; j < n; j++) {
+                const rt_prim& P = tile[j];
+                float t, a = 0, b = 0, g = 0;
+                bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+                if (hit && (!found || t < h.t)) {
+                    found = true;
+                    h.t = t; h.a = a; h.b = b; h.g = g; h.prim = base + j;
+                }
+            }
         }
     }
     return found;
 }
 
-// IntersectScene when only the boolean is used (directional shadows, AO rays).
-__device__ bool any_hit(const DevScene& S, rv3 o, rv3 d) {
-    for (int i = 0; i < S.n_prims; i++) {
-        const rt_prim P = S.prims[i];
-        float t, a, b, g;
-        bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
-        if (hit) return true;
+// IntersectScene where only the boolean is read (directional shadows, AO rays):
+// any hit, with a workgroup-wide early exit once every active lane has hit.
+__device__ bool any_hit(const DevScene& S, rt_prim* tile, bool active, rv3 o, rv3 d) {
+    bool hit = false;
+    for (int base = 0; base < S.n_prims; base += TILE) {
+        const int n = min(TILE, S.n_prims - base);
+        __syncthreads();
+        load_tile(S.prims, base, n, tile);
+        __syncthreads();
+        if (active && !hit) {
+            for (int j = 0; j < n; j++) {
+                const rt_prim& P = tile[j];
+                float t, a, b, g;
+                if (P.kind == RT_PRIM_TRIANGLE ? tri_test(P, o, d, t, a, b, g) : sph_test(P, o, d, t)) {
+                    hit = true;
+                    break;
+                }
+            }
+        }
+        if (base + TILE < S.n_prims && __syncthreads_and(!active || hit)) break;
     }
-    return false;
+    return hit;
 }
 
 // ---------------------------------------------------------------- camera
@@ -161,15 +184,14 @@ __device__ __forceinline__ void generate_ray(const DevFrame& F, int x, int y, rv
                             m[3] * dir.x + m[4] * dir.y + m[5] * dir.z,
                             m[6] * dir.x + m[7] * dir.y + m[8] * dir.z));
     } else {
-        d = v3(0, 0, 0);
+        d = v3(0, 0, 0);  // the reference leaves the direction zeroed (:854-857)
     }
 }
 
 // ---------------------------------------------------------------- shading
 struct HitInfo {
     rv3 p, n;  // world hit point, geometric normal (hitInfo.normal)
-    int prim;
-    int kind;
+    int prim, kind;
     float a, b, g;
 };
 
@@ -208,58 +230,6 @@ __device__ rpix local_color(const DevScene& S, const DevFrame& F, const HitInfo&
     col.y = rt_clipf(col.y, 0.0f, 1.0f);
     col.z = rt_clipf(col.z, 0.0f, 1.0f);
     return px_from(col);
-}
-
-// CalculateAmbientOcclusion (Raytracer.cpp:315-330) with RandomInHemisphere (:283-292)
-// and RandomUnitVector (:269-281).
-__device__ float ambient_occlusion(const DevScene& S, const DevFrame& F, rv3 hp, rv3 n, Rng& rng) {
-    float occ = 0.0f;
-    for (int i = 0; i < F.ao_samples; i++) {
-        float z = rng.uniform(-1.0f, 1.0f);
-        float ang = rng.uniform(0.0f, F.ao_angle_max);
-        float r = sqrtf(1 - z * z);
-        double sa, ca;
-        rt_glibc_sincos((double)ang, &sa, &ca);
-        rv3 v = v3_normalize(v3((float)((double)r * ca), (float)((double)r * sa), z));
-        if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
-        rv3 o = v3_add(hp, v3_scale(v, 0.2f));
-        rv3 d = v3_normalize(v);  // Ray constructor
-        if (any_hit(S, o, d)) occ += 1.0f;
-    }
-    return 1.0f - ((float)occ / (float)F.ao_samples);
-}
-
-// Raycast's light loop (Raytracer.cpp:39-82). Returns the (unclamped) local color.
-__device__ rpix shade_lights(const DevScene& S, const DevFrame& F, const HitInfo& h, const rt_material& m,
-                             Rng& rng) {
-    rpix local = px(0, 0, 0);
-    for (int li = 0; li < S.n_lights; li++) {
-        const rt_light l = S.lights[li];
-        if (l.kind == RT_LIGHT_AMBIENT) {
-            rv3 amb = v3_scale(v3_mul(v3_scale(ld3(m.cs), m.ka), ld3(l.color)), l.intensity);
-            float ao = F.ao_enabled ? ambient_occlusion(S, F, h.p, h.n, rng) : 1.0f;
-            amb = v3_scale(amb, ao);
-            local = px_add(local, px_from(amb));
-            continue;
-        }
-        rv3 L, L2;
-        bool occluded;
-        if (l.kind == RT_LIGHT_DIRECTIONAL) {
-            L = ld3(l.L);
-            L2 = ld3(l.L2);
-            occluded = any_hit(S, v3_add(h.p, v3_scale(L, 0.2f)), L2);
-        } else {
-            rv3 tl = v3_sub(ld3(l.position), h.p);
-            L = v3_normalize(tl);
-            L2 = v3_normalize(L);
-            float dist = v3_length(tl);
-            Hit sh;
-            bool hit = closest_hit(S, v3_add(h.p, v3_scale(L, 0.2f)), L2, sh);
-            occluded = hit && !(sh.t > dist);
-        }
-        if (!occluded) local = px_add(local, local_color(S, F, h, l, m, L));
-    }
-    return local;
 }
 
 // CalculateRefraction (Raytracer.cpp:168-203)
@@ -302,261 +272,499 @@ __device__ __forceinline__ void fresnel(float ior, rv3 N, rv3 I, float& kr, floa
     }
 }
 
-// One pending node of the reflect/refract recursion (Raycast is a binary tree,
-// evaluated bottom-up because the int16 blend is non-linear).
-struct Frame {
-    rpix local, refl;
-    float kr, kt, ks, ktm;
-    rv3 ro, rd;      // refraction child ray (if ktm > 0)
-    int stage;       // 1: reflection child pending, 2: refraction child pending
-};
-
 // Raycast's blend (Raytracer.cpp:114-128)
-__device__ __forceinline__ rpix combine(const Frame& f, rpix refr) {
-    rpix fR = px_mul(px_mul(f.refl, f.kr), f.ks);
-    rpix fT = px_mul(px_mul(refr, f.kt), f.ktm);
-    float alb = 1 - f.ks - f.ktm;
-    alb = alb > 0.0f ? alb : 0.0f;   // std::max(alb, 0.0f)
-    rpix out = px_add(px_add(px_mul(f.local, alb), px_mul(fR, f.ks)), px_mul(fT, f.ktm));
-    return px_clamp(out);
+__device__ __forceinline__ rpix combine(rpix local, rpix refl, rpix refr, float kr, float kt, float ks, float ktm) {
+    rpix fR = px_mul(px_mul(refl, kr), ks);
+    rpix fT = px_mul(px_mul(refr, kt), ktm);
+    float alb = 1 - ks - ktm;
+    alb = alb > 0.0f ? alb : 0.0f;  // std::max(alb, 0.0f)
+    return px_clamp(px_add(px_add(px_mul(local, alb), px_mul(fR, ks)), px_mul(fT, ktm)));
 }
 
-struct Tally {
-    uint32_t hits, tree_rays;
+// ---------------------------------------------------------------- wave utilities
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// Allocate one slot per set flag (two flags per lane) from *counter, one atomic per wave.
+__device__ __forceinline__ void wave_alloc2(uint32_t* counter, bool fa, bool fb, uint32_t& sa, uint32_t& sb) {
+    const uint64_t ma = __ballot(fa), mb = __ballot(fb);
+    const uint32_t na = (uint32_t)__popcll(ma), nb = (uint32_t)__popcll(mb);
+    const uint64_t active = __ballot(1);
+    const int leader = __ffsll((unsigned long long)active) - 1;
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == leader && na + nb) base = atomicAdd(counter, na + nb);
+    base = __shfl(base, leader);
+    const uint64_t lt = lanemask_lt();
+    sa = base + (uint32_t)__popcll(ma & lt);
+    sb = base + na + (uint32_t)__popcll(mb & lt);
+}
+
+// ---------------------------------------------------------------- trace (one tree level)
+__device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { return F.row_begin + lr * F.row_step; }
+
+__global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level) {
+    __shared__ rt_prim tile[TILE];
+    const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
+    const uint32_t count = level == 0 ? npix : W.lvl[level];
+    const uint32_t base_id = level == 0 ? 0u : W.lvl[LVL_BASE + level];
+    const uint32_t next_base = base_id + count;
+    if (blockIdx.x == 0 && threadIdx.x == 0) W.lvl[LVL_BASE + level + 1] = next_base;
+    const int bounces = F.depth - level;
+
+    for (uint32_t b0 = blockIdx.x * TB; b0 < count; b0 += gridDim.x * TB) {
+        const uint32_t item = b0 + threadIdx.x;
+        const bool active = item < count;
+        const uint32_t node = base_id + item;
+        rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+        int pixel = 0;
+        if (active) {
+            if (level == 0) {
+                pixel = (int)item;
+                const int lr = pixel / F.width;
+                generate_ray(F, pixel - lr * F.width, pixel_frame_row(F, lr), o, d);
+            } else {
+                const RayItem r = W.rays[node];
+                o = v3(r.o[0], r.o[1], r.o[2]);
+                d = v3(r.d[0], r.d[1], r.d[2]);
+                pixel = r.pixel;
+            }
+        }
+        Hit h;
+        const bool hit = closest_hit(S, tile, active, o, d, h);
+
+        HitInfo hi;
+        rt_material m;
+        hi.p = hi.n = v3(0, 0, 0);
+        hi.kind = 0;
+        m.ks = m.kt = 0.0f;
+        m.ior = 2.5f;
+        int shape = 0;
+        if (hit) {
+            resolve_hit(S, o, d, h, hi);
+            shape = S.prims[h.prim].shape;
+            m = S.mats[shape];
+        }
+        // Raycast's light loop (Raytracer.cpp:39-82) without the ambient terms
+        // (those need AO; int16 wrap-around addition commutes, so they are added
+        // in resolve_kernel).
+        rpix local = px(0, 0, 0);
+        for (int li = 0; li < S.n_lights; li++) {
+            const rt_light l = S.lights[li];
+            if (l.kind == RT_LIGHT_AMBIENT) continue;
+            rv3 L = v3(0, 0, 0), L2 = v3(0, 0, 0), so = v3(0, 0, 0);
+            float dist = 0.0f;
+            if (hit) {
+                if (l.kind == RT_LIGHT_DIRECTIONAL) {
+                    L = ld3(l.L);
+                    L2 = ld3(l.L2);
+                } else {
+                    rv3 tl = v3_sub(ld3(l.position), hi.p);
+                    L = v3_normalize(tl);
+                    L2 = v3_normalize(L);
+                    dist = v3_length(tl);
+                }
+                so = v3_add(hi.p, v3_scale(L, 0.2f));
+            }
+            bool occluded;
+            if (l.kind == RT_LIGHT_DIRECTIONAL) {
+                occluded = any_hit(S, tile, hit, so, L2);
+            } else {
+                Hit sh;
+                const bool shit = closest_hit(S, tile, hit, so, L2, sh);
+                occluded = shit && !(sh.t > dist);
+            }
+            if (hit && !occluded) local = px_add(local, local_color(S, F, hi, l, m, L));
+        }
+        // children (Raytracer.cpp:87-112)
+        bool want_refl = false, want_refr = false;
+        RayItem crefl, crefr;
+        float kr = 0.0f, kt = 0.0f;
+        if (hit && bounces > 0) {
+            fresnel(m.ior, hi.n, d, kr, kt);
+            if (m.ks > 0) {
+                rv3 rd = v3_normalize(v3_reflect(d, hi.n));
+                rv3 ro = v3_add(hi.p, v3_scale(rd, 0.2f));
+                rd = v3_normalize(rd);
+                crefl.o[0] = ro.x; crefl.o[1] = ro.y; crefl.o[2] = ro.z;
+                crefl.d[0] = rd.x; crefl.d[1] = rd.y; crefl.d[2] = rd.z;
+                crefl.pixel = pixel;
+                crefl.pad = 0;
+                want_refl = true;
+            }
+            if (m.kt > 0) {
+                rv3 td = refraction_dir(d, hi.n, m.ior);
+                rv3 to = v3_add(hi.p, v3_scale(td, 0.2f));
+                td = v3_normalize(td);
+                crefr.o[0] = to.x; crefr.o[1] = to.y; crefr.o[2] = to.z;
+                crefr.d[0] = td.x; crefr.d[1] = td.y; crefr.d[2] = td.z;
+                crefr.pixel = pixel;
+                crefr.pad = 0;
+                want_refr = true;
+            }
+        }
+        uint32_t sa, sb;
+        wave_alloc2(&W.lvl[level + 1], want_refl, want_refr, sa, sb);
+        int32_t child0 = -1, child1 = -1;
+        if (want_refl) {
+            const uint32_t id = next_base + sa;
+            if (id < W.node_cap) { W.rays[id] = crefl; child0 = (int32_t)id; }
+            else atomicMax(W.needed, id + 1);
+        }
+        if (want_refr) {
+            const uint32_t id = next_base + sb;
+            if (id < W.node_cap) { W.rays[id] = crefr; child1 = (int32_t)id; }
+            else atomicMax(W.needed, id + 1);
+        }
+        if (active) {
+            NodeRec rec;
+            rec.hp[0] = hi.p.x; rec.hp[1] = hi.p.y; rec.hp[2] = hi.p.z;
+            rec.n[0] = hi.n.x; rec.n[1] = hi.n.y; rec.n[2] = hi.n.z;
+            rec.child[0] = child0;
+            rec.child[1] = child1;
+            const int flags = (hit ? RT_NODE_HIT : 0) | (bounces == 0 ? RT_NODE_LEAF : 0);
+            rec.local_rg = (int32_t)(((uint32_t)local.r & 0xffffu) | ((uint32_t)local.g << 16));
+            rec.local_b_flags = (int32_t)(((uint32_t)local.b & 0xffffu) | ((uint32_t)flags << 16));
+            rec.kr = kr;
+            rec.kt = kt;
+            rec.shape = shape;
+            rec.call0 = 0;
+            rec.pad[0] = rec.pad[1] = 0;
+            W.nodes[node] = rec;
+            if (level == 0) {
+                W.pix_hits[pixel] = hit ? 1u : 0u;
+                W.pix_nodes[pixel] = 1u;
+            } else {
+                if (hit) atomicAdd(&W.pix_hits[pixel], 1u);
+                atomicAdd(&W.pix_nodes[pixel], 1u);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- AO-call bookkeeping
+// One workgroup per local row: AO calls per pixel (hits x ambient lights), their
+// in-row exclusive prefix, and the row's totals.
+__global__ void __launch_bounds__(1024) row_counts_kernel(DevScene S, DevFrame F, DevWork W) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t carry, hsum, nsum;
+    const int lr = blockIdx.x;
+    const uint32_t off = (uint32_t)lr * (uint32_t)F.width;
+    if (threadIdx.x == 0) { carry = 0; hsum = 0; nsum = 0; }
+    __syncthreads();
+    uint32_t my_h = 0, my_n = 0;
+    for (int x0 = 0; x0 < F.width; x0 += 1024) {
+        const int x = x0 + threadIdx.x;
+        uint32_t hits = 0, nodes = 0;
+        if (x < F.width) { hits = W.pix_hits[off + x]; nodes = W.pix_nodes[off + x]; }
+        my_h += hits;
+        my_n += nodes;
+        const uint32_t v = hits * (uint32_t)S.n_ambient;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int s = 1; s < 1024; s <<= 1) {
+            uint32_t add = threadIdx.x >= s ? part[threadIdx.x - s] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (x < F.width) W.pix_prefix[off + x] = carry + part[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += part[1023];
+        __syncthreads();
+    }
+    atomicAdd(&hsum, my_h);
+    atomicAdd(&nsum, my_n);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        W.row_calls[lr] = carry;
+        W.row_hits[lr] = hsum;
+        W.row_nodes[lr] = nsum;
+    }
+}
+
+// Exclusive scan of this call's per-row AO calls (one workgroup) + the total.
+__global__ void __launch_bounds__(1024) row_scan_kernel(DevFrame F, DevWork W) {
+    __shared__ uint64_t part[1024];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int b = 0; b < F.n_rows; b += 1024) {
+        const int i = b + threadIdx.x;
+        const uint64_t v = i < F.n_rows ? W.row_calls[i] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int s = 1; s < 1024; s <<= 1) {
+            uint64_t add = threadIdx.x >= s ? part[threadIdx.x - s] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (i < F.n_rows) W.row_base_local[i] = carry + part[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) W.totals[0] = carry;
+}
+
+// Per pixel: number the pixel's AO calls in the reference's draw order (pre-order
+// of the recursion tree, lights in JSON order) and record each call's RNG position.
+__global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWork W,
+                                                  const uint64_t* __restrict__ row_base_global) {
+    const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
+    const uint32_t p = blockIdx.x * TB + threadIdx.x;
+    if (p >= npix || S.n_ambient == 0) return;
+    if (W.pix_hits[p] == 0) return;
+    const int lr = (int)(p / (uint32_t)F.width);
+    const uint64_t lbase = W.row_base_local[lr] + W.pix_prefix[p];
+    const uint64_t gbase = (row_base_global ? row_base_global[lr] : W.row_base_local[lr]) + W.pix_prefix[p];
+    const uint64_t draws_per_call = 2ull * (uint64_t)F.ao_samples;
+    uint64_t rng = 0;
+    uint32_t step = 1;
+    if (F.rng_engine == RT_RNG_MINSTD_RAND0) {
+        rng = minstd_pow(F.rng_seed, gbase * draws_per_call);
+        step = minstd_pow(1u, draws_per_call);
+    } else {
+        rng = gbase;
+    }
+    int stack[2 * RT_MAX_DEPTH + 4];
+    int sp = 0;
+    stack[sp++] = (int)p;
+    uint32_t call = (uint32_t)lbase;
+    while (sp > 0) {
+        const int n = stack[--sp];
+        const NodeRec& nd = W.nodes[n];
+        const int flags = nd.local_b_flags >> 16;
+        if (!(flags & RT_NODE_HIT)) continue;
+        W.nodes[n].call0 = call;
+        for (int a = 0; a < S.n_ambient; a++) {
+            W.call_node[call] = (uint32_t)n;
+            W.call_rng[call] = rng;
+            W.occ[call] = 0;
+            call++;
+            if (F.rng_engine == RT_RNG_MINSTD_RAND0) rng = mersenne31_mul((uint32_t)rng, step);
+            else rng++;
+        }
+        if (nd.child[1] >= 0) stack[sp++] = nd.child[1];  // refraction after
+        if (nd.child[0] >= 0) stack[sp++] = nd.child[0];  // reflection first
+    }
+}
+
+// ---------------------------------------------------------------- AO
+// CalculateAmbientOcclusion (Raytracer.cpp:315-330) + RandomInHemisphere (:283-292)
+// + RandomUnitVector (:269-281): one lane per (call, sample).
+__global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork W) {
+    __shared__ rt_prim tile[TILE];
+    const uint32_t N = (uint32_t)F.ao_samples;
+    const uint64_t items = W.totals[0] * (uint64_t)N;
+    const bool pow2 = (N & (N - 1)) == 0;
+    const int log2n = 31 - __clz((int)N);
+    const bool wave_per_call = (N & 63u) == 0;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * TB; b0 < items; b0 += (uint64_t)gridDim.x * TB) {
+        const uint64_t item = b0 + threadIdx.x;
+        const bool active = item < items;
+        uint64_t c = 0;
+        uint32_t s = 0;
+        if (active) {
+            if (pow2) { c = item >> log2n; s = (uint32_t)(item & (N - 1)); }
+            else { c = item / N; s = (uint32_t)(item - c * N); }
+        }
+        rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+        if (active) {
+            const NodeRec& nd = W.nodes[W.call_node[c]];
+            const rv3 hp = ld3(nd.hp), n = ld3(nd.n);
+            float u0, u1;
+            if (F.rng_engine == RT_RNG_MINSTD_RAND0) {
+                uint32_t st = mersenne31_mul((uint32_t)W.call_rng[c], c_minstd_j1[s]);
+                u0 = canon_minstd(st);
+                st = mersenne31_mul(st, 16807u);
+                u1 = canon_minstd(st);
+            } else {
+                const uint64_t k = W.call_rng[c] * 2ull * (uint64_t)N + 2ull * s;
+                u0 = canon_mt(W.mt_stream[k]);
+                u1 = canon_mt(W.mt_stream[k + 1]);
+            }
+            // uniform_real_distribution<float>: canonical * (b - a) + a
+            const float z = u0 * (1.0f - (-1.0f)) + (-1.0f);
+            const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
+            const float r = sqrtf(1 - z * z);
+            double sa, ca;
+            rt_glibc_sincos((double)ang, &sa, &ca);
+            rv3 v = v3_normalize(v3((float)((double)r * ca), (float)((double)r * sa), z));
+            if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
+            o = v3_add(hp, v3_scale(v, 0.2f));
+            d = v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
+        }
+        const bool hit = any_hit(S, tile, active, o, d);
+        if (wave_per_call) {
+            const uint64_t m = __ballot(active && hit);
+            if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.occ[c], (uint32_t)__popcll(m));
+        } else if (active && hit) {
+            atomicAdd(&W.occ[c], 1u);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- resolve
+struct RFrame {
+    rpix local, refl;
+    float kr, kt, ks, ktm;
+    int node;
+    int stage;  // 1: reflection child pending, 2: refraction child pending
 };
 
-// Iterative Raycast over the recursion tree. COUNT: structure only (closest hits),
-// no lights, no AO, no RNG draws.
-template <bool COUNT>
-__device__ rpix trace_pixel(const DevScene& S, const DevFrame& F, rv3 o, rv3 d, Rng& rng, Tally& tally) {
-    Frame st[RT_MAX_DEPTH + 1];
+__device__ __forceinline__ rpix node_local(const DevScene& S, const DevFrame& F, const DevWork& W, const NodeRec& nd,
+                                           const rt_material& m) {
+    rpix local = px((int16_t)(nd.local_rg & 0xffff), (int16_t)(nd.local_rg >> 16), (int16_t)(nd.local_b_flags & 0xffff));
+    int a = 0;
+    for (int li = 0; li < S.n_lights; li++) {
+        const rt_light l = S.lights[li];
+        if (l.kind != RT_LIGHT_AMBIENT) continue;
+        rv3 amb = v3_scale(v3_mul(v3_scale(ld3(m.cs), m.ka), ld3(l.color)), l.intensity);
+        float ao = 1.0f;
+        if (F.ao_enabled) ao = 1.0f - ((float)W.occ[nd.call0 + a] / (float)F.ao_samples);
+        amb = v3_scale(amb, ao);
+        local = px_add(local, px_from(amb));
+        a++;
+    }
+    return local;
+}
+
+__global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, DevWork W, int16_t* __restrict__ fb) {
+    const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
+    const uint32_t p = blockIdx.x * TB + threadIdx.x;
+    if (p >= npix) return;
+    RFrame st[RT_MAX_DEPTH + 1];
     int lvl = 0;
+    int cur = (int)p;
     rpix ret;
     for (;;) {
-        // ---- evaluate the node (o, d) at level lvl with bounces = depth - lvl
-        const int bounces = F.depth - lvl;
-        Hit h;
-        tally.tree_rays++;
+        const NodeRec nd = W.nodes[cur];
+        const int flags = nd.local_b_flags >> 16;
         bool descended = false;
-        if (!closest_hit(S, o, d, h)) {
+        if (!(flags & RT_NODE_HIT)) {
             ret = px(254, 64, 205);  // BG_COLOR (Raytracer.h:597)
         } else {
-            tally.hits++;
-            HitInfo hi;
-            resolve_hit(S, o, d, h, hi);
-            const rt_material m = S.mats[S.prims[h.prim].shape];
-            rpix local = px(0, 0, 0);
-            if (!COUNT) local = shade_lights(S, F, hi, m, rng);
-            if (bounces == 0) {
+            const rt_material m = S.mats[nd.shape];
+            const rpix local = node_local(S, F, W, nd, m);
+            if (flags & RT_NODE_LEAF) {
                 ret = px_clamp(local);
             } else {
-                Frame& f = st[lvl];
+                RFrame& f = st[lvl];
                 f.local = local;
                 f.refl = px(0, 0, 0);
-                f.ks = m.ks;
-                f.ktm = m.kt;
-                fresnel(m.ior, hi.n, d, f.kr, f.kt);
-                if (m.kt > 0) {
-                    rv3 td = refraction_dir(d, hi.n, m.ior);
-                    f.ro = v3_add(hi.p, v3_scale(td, 0.2f));
-                    f.rd = v3_normalize(td);
-                }
-                if (m.ks > 0) {
-                    rv3 rd = v3_normalize(v3_reflect(d, hi.n));
-                    o = v3_add(hi.p, v3_scale(rd, 0.2f));
-                    d = v3_normalize(rd);
-                    f.stage = 1;
-                    lvl++;
-                    descended = true;
-                } else if (m.kt > 0) {
-                    o = f.ro;
-                    d = f.rd;
-                    f.stage = 2;
-                    lvl++;
-                    descended = true;
+                f.kr = nd.kr; f.kt = nd.kt; f.ks = m.ks; f.ktm = m.kt;
+                f.node = cur;
+                if (nd.child[0] >= 0) {
+                    f.stage = 1; cur = nd.child[0]; lvl++; descended = true;
+                } else if (nd.child[1] >= 0) {
+                    f.stage = 2; cur = nd.child[1]; lvl++; descended = true;
                 } else {
-                    ret = combine(f, px(0, 0, 0));
+                    ret = combine(local, px(0, 0, 0), px(0, 0, 0), f.kr, f.kt, f.ks, f.ktm);
                 }
             }
         }
         if (descended) continue;
-        // ---- return `ret` to the parents
         bool resumed = false;
         while (lvl > 0) {
-            Frame& p = st[lvl - 1];
-            if (p.stage == 1) {
-                p.refl = ret;
-                if (p.ktm > 0) {
-                    p.stage = 2;
-                    o = p.ro;
-                    d = p.rd;
-                    resumed = true;  // same level: sibling subtree
-                    break;
-                }
-                ret = combine(p, px(0, 0, 0));
+            RFrame& pf = st[lvl - 1];
+            if (pf.stage == 1) {
+                pf.refl = ret;
+                const int c1 = W.nodes[pf.node].child[1];
+                if (c1 >= 0) { pf.stage = 2; cur = c1; resumed = true; break; }
+                ret = combine(pf.local, pf.refl, px(0, 0, 0), pf.kr, pf.kt, pf.ks, pf.ktm);
             } else {
-                ret = combine(p, ret);
+                ret = combine(pf.local, pf.refl, ret, pf.kr, pf.kt, pf.ks, pf.ktm);
             }
             lvl--;
         }
-        if (!resumed) return ret;
+        if (!resumed) break;
     }
+    fb[(size_t)p * 3 + 0] = (int16_t)ret.r;
+    fb[(size_t)p * 3 + 1] = (int16_t)ret.g;
+    fb[(size_t)p * 3 + 2] = (int16_t)ret.b;
 }
 
-// ---------------------------------------------------------------- kernels
-__device__ __forceinline__ int frame_row(const DevFrame& F, int local_row) {
-    return F.row_begin + local_row * F.row_step;
-}
-
-__global__ void __launch_bounds__(256) count_kernel(DevScene S, DevFrame F, uint32_t* __restrict__ pix_calls,
-                                                    uint32_t* __restrict__ row_calls,
-                                                    uint32_t* __restrict__ row_tree,
-                                                    uint32_t* __restrict__ row_hits) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t npix = (int64_t)F.n_rows * F.width;
-    if (idx >= npix) return;
-    const int lr = (int)(idx / F.width);
-    const int x = (int)(idx - (int64_t)lr * F.width);
-    rv3 o, d;
-    generate_ray(F, x, frame_row(F, lr), o, d);
-    Rng rng;
-    Tally t = {0, 0};
-    trace_pixel<true>(S, F, o, d, rng, t);
-    uint32_t calls = t.hits * (uint32_t)F.n_ambient;
-    pix_calls[idx] = calls;
-    atomicAdd(&row_calls[lr], calls);
-    atomicAdd(&row_tree[lr], t.tree_rays);
-    atomicAdd(&row_hits[lr], t.hits);
-}
-
-// Exclusive scan of per-row AO calls in raster order (one workgroup).
-__global__ void __launch_bounds__(1024) row_base_kernel(const uint32_t* __restrict__ row_calls, int n_rows,
-                                                        uint64_t* __restrict__ row_base) {
-    __shared__ uint64_t partial[1024];
-    __shared__ uint64_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < n_rows; base += 1024) {
-        int i = base + threadIdx.x;
-        uint64_t v = i < n_rows ? row_calls[i] : 0;
-        partial[threadIdx.x] = v;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {
-            uint64_t add = threadIdx.x >= off ? partial[threadIdx.x - off] : 0;
-            __syncthreads();
-            partial[threadIdx.x] += add;
-            __syncthreads();
-        }
-        if (i < n_rows) row_base[i] = carry + partial[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += partial[1023];
-        __syncthreads();
-    }
-}
-
-// One workgroup per local row: exclusive in-row prefix of AO calls + the row's
-// base -> absolute AO-call index of each pixel.
-__global__ void __launch_bounds__(1024) pixel_base_kernel(const uint32_t* __restrict__ pix_calls, int width,
-                                                          const uint64_t* __restrict__ row_base,
-                                                          uint64_t* __restrict__ pix_base) {
-    __shared__ uint32_t partial[1024];
-    __shared__ uint64_t carry;
-    const int lr = blockIdx.x;
-    const uint32_t* calls = pix_calls + (int64_t)lr * width;
-    uint64_t* out = pix_base + (int64_t)lr * width;
-    if (threadIdx.x == 0) carry = row_base[lr];
-    __syncthreads();
-    for (int base = 0; base < width; base += 1024) {
-        int i = base + threadIdx.x;
-        uint32_t v = i < width ? calls[i] : 0;
-        partial[threadIdx.x] = v;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {
-            uint32_t add = threadIdx.x >= off ? partial[threadIdx.x - off] : 0;
-            __syncthreads();
-            partial[threadIdx.x] += add;
-            __syncthreads();
-        }
-        if (i < width) out[i] = carry + partial[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += partial[1023];
-        __syncthreads();
-    }
-}
-
-__global__ void __launch_bounds__(256) render_kernel(DevScene S, DevFrame F, const uint64_t* __restrict__ pix_base,
-                                                     int16_t* __restrict__ fb) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t npix = (int64_t)F.n_rows * F.width;
-    if (idx >= npix) return;
-    const int lr = (int)(idx / F.width);
-    const int x = (int)(idx - (int64_t)lr * F.width);
-    rv3 o, d;
-    generate_ray(F, x, frame_row(F, lr), o, d);
-    Rng rng;
-    rng.engine = F.rng_engine;
-    rng.mt = F.mt_stream;
-    rng.index = F.ao_enabled ? pix_base[idx] * (uint64_t)(2 * F.ao_samples) : 0;
-    rng.state = F.rng_engine == RT_RNG_MINSTD_RAND0 ? minstd_jump(F.rng_seed, rng.index) : 0;
-    Tally t = {0, 0};
-    rpix p = trace_pixel<false>(S, F, o, d, rng, t);
-    fb[idx * 3 + 0] = (int16_t)p.r;
-    fb[idx * 3 + 1] = (int16_t)p.g;
-    fb[idx * 3 + 2] = (int16_t)p.b;
-}
-
-__global__ void select_rows_kernel(const uint64_t* __restrict__ all_base, int row_begin, int row_step,
-                                   int n_rows, uint64_t* __restrict__ sel_base) {
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n_rows) sel_base[k] = all_base[row_begin + k * row_step];
+__global__ void copy_rows_kernel(const int16_t* __restrict__ src, int width, int row_begin, int row_step, int n_rows,
+                                 int16_t* __restrict__ dst) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t per_row = (size_t)width * 3;
+    if (i >= per_row * (size_t)n_rows) return;
+    const size_t k = i / per_row, e = i - k * per_row;
+    dst[i] = src[(size_t)(row_begin + k * row_step) * per_row + e];
 }
 
 // ---------------------------------------------------------------- launchers
-hipError_t launch_select_rows(const uint64_t* all_base, int row_begin, int row_step, int n_rows,
-                              uint64_t* sel_base, hipStream_t s) {
-    if (n_rows == 0) return hipSuccess;
-    hipLaunchKernelGGL(select_rows_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, s, all_base, row_begin,
-                       row_step, n_rows, sel_base);
-    return hipGetLastError();
+static int grid_for(uint64_t items, int cap) {
+    uint64_t b = (items + TB - 1) / TB;
+    if (b < 1) b = 1;
+    return (int)(b < (uint64_t)cap ? b : (uint64_t)cap);
 }
 
 void upload_minstd_table(hipStream_t s) {
-    uint32_t t[32];
+    uint32_t pw[32];
     uint64_t a = 16807;
-    for (int i = 0; i < 32; i++) {
-        t[i] = (uint32_t)a;
-        a = (a * a) % 2147483647ull;
+    for (int i = 0; i < 32; i++) { pw[i] = (uint32_t)a; a = (a * a) % 2147483647ull; }
+    static uint32_t j1[512];
+    uint64_t x = 16807;  // a^(2s+1)
+    for (int i = 0; i < 512; i++) {
+        j1[i] = (uint32_t)x;
+        x = (x * 16807ull) % 2147483647ull;
+        x = (x * 16807ull) % 2147483647ull;
     }
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_pow2), t, sizeof t, 0, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_pow2), pw, sizeof pw, 0, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
 }
 
-hipError_t launch_count(const DevScene& S, const DevFrame& F, uint32_t* pix_calls, uint32_t* row_calls,
-                        uint32_t* row_tree, uint32_t* row_hits, hipStream_t s) {
-    int64_t npix = (int64_t)F.n_rows * F.width;
+hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
+    const uint64_t npix = (uint64_t)F.n_rows * F.width;
+    hipError_t e = hipMemsetAsync(W.lvl, 0, sizeof(uint32_t) * 2 * LVL_BASE, s);
+    if (e != hipSuccess) return e;
+    for (int level = 0; level <= F.depth; level++) {
+        // level 0 has exactly npix rays; deeper levels read their count on the device
+        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, 4096);
+        hipLaunchKernelGGL(trace_kernel, dim3(grid), dim3(TB), 0, s, S, F, W, level);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_row_counts(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
+    if (F.n_rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(row_counts_kernel, dim3(F.n_rows), dim3(1024), 0, s, S, F, W);
+    hipLaunchKernelGGL(row_scan_kernel, dim3(1), dim3(1024), 0, s, F, W);
+    return hipGetLastError();
+}
+
+hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, const uint64_t* row_base_global,
+                       hipStream_t s) {
+    const uint64_t npix = (uint64_t)F.n_rows * F.width;
+    if (npix == 0 || !F.ao_enabled || S.n_ambient == 0) return hipSuccess;
+    hipLaunchKernelGGL(rank_kernel, dim3((unsigned)((npix + TB - 1) / TB)), dim3(TB), 0, s, S, F, W, row_base_global);
+    return hipGetLastError();
+}
+
+hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
+    if (!F.ao_enabled || S.n_ambient == 0 || F.n_rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(ao_kernel, dim3(8192), dim3(TB), 0, s, S, F, W);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s) {
+    const uint64_t npix = (uint64_t)F.n_rows * F.width;
     if (npix == 0) return hipSuccess;
-    dim3 grid((unsigned)((npix + 255) / 256));
-    hipLaunchKernelGGL(count_kernel, grid, dim3(256), 0, s, S, F, pix_calls, row_calls, row_tree, row_hits);
+    hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)((npix + TB - 1) / TB)), dim3(TB), 0, s, S, F, W, fb);
     return hipGetLastError();
 }
 
-hipError_t launch_row_base(const uint32_t* row_calls, int n_rows, uint64_t* row_base, hipStream_t s) {
-    hipLaunchKernelGGL(row_base_kernel, dim3(1), dim3(1024), 0, s, row_calls, n_rows, row_base);
-    return hipGetLastError();
-}
-
-hipError_t launch_pixel_base(const uint32_t* pix_calls, int width, int n_rows, const uint64_t* row_base,
-                             uint64_t* pix_base, hipStream_t s) {
-    if (n_rows == 0) return hipSuccess;
-    hipLaunchKernelGGL(pixel_base_kernel, dim3(n_rows), dim3(1024), 0, s, pix_calls, width, row_base, pix_base);
-    return hipGetLastError();
-}
-
-hipError_t launch_render(const DevScene& S, const DevFrame& F, const uint64_t* pix_base, int16_t* fb,
-                         hipStream_t s) {
-    int64_t npix = (int64_t)F.n_rows * F.width;
-    if (npix == 0) return hipSuccess;
-    dim3 grid((unsigned)((npix + 255) / 256));
-    hipLaunchKernelGGL(render_kernel, grid, dim3(256), 0, s, S, F, pix_base, fb);
+hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows, int16_t* dst,
+                            hipStream_t s) {
+    const uint64_t n = (uint64_t)width * 3 * n_rows;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(copy_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, width, row_begin,
+                       row_step, n_rows, dst);
     return hipGetLastError();
 }
 

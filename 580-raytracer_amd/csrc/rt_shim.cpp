@@ -3,13 +3,12 @@
 // the reference's status codes (Raytracer.h:8-10). No exception crosses it.
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <array>
 #include <random>
-#include <string>
 #include <vector>
 
 #include "../../include/rt580.h"
@@ -24,28 +23,38 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+enum { EV_START, EV_TRACE, EV_RANK, EV_AO, EV_RESOLVE, EV_N };
+
 struct State {
     bool inited = false;
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ev_default[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t* ev = ev_default;       // events of the frame being enqueued
-    // bench profiling: one event quadruple per frame, summed at read time
+    std::array<hipEvent_t, EV_N> ev_default{};
+    hipEvent_t* ev = nullptr;  // events of the frame being enqueued
     bool profiling = false;
     int prof_frames = 0;
-    std::vector<std::array<hipEvent_t, 4>> prof_pool;
+    std::vector<std::array<hipEvent_t, EV_N>> prof_pool;
     // scene
     DevBuf prims, shade, mats, lights;
     int n_prims = 0, n_lights = 0, n_ambient = 0, n_nonambient = 0;
     bool have_scene = false;
-    // per-frame workspaces
-    DevBuf pix_calls, pix_base, row_calls, row_tree, row_hits, row_base, row_base_all, fb, mt_stream;
-    DevBuf cnt_calls_all, cnt_tree_all, cnt_hits_all, cnt_pix_all;
-    // last frame bookkeeping for stats
+    uint64_t scene_gen = 0;
+    // workspace
+    DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
+        row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream;
+    uint32_t node_cap = 0, call_cap = 0;
+    double node_factor = 4.0;         // node capacity per pixel (grown on overflow)
+    uint32_t* needed_host = nullptr;  // pinned
+    // capacity verification: a (params, scene) already rendered without overflow
+    rt_render_params verified{};
+    uint64_t verified_gen = ~0ull;
+    bool verified_valid = false;
+    // stats of the last traced rows
     int last_rows = 0, last_width = 0, last_ao_samples = 0, last_ao_enabled = 0;
     bool last_valid = false;
-    rt_render_params split_params;
+    // multi-rank split
+    rt_render_params split_params{};
     bool split_ready = false;
 };
 
@@ -70,8 +79,8 @@ int fail(const char* fmt, ...) {
 int ensure(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return RT_SUCCESS;
     if (b.p) { (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
-    if (bytes == 0) return RT_SUCCESS;
-    size_t want = bytes + bytes / 4;  // headroom for the next frame
+    if (bytes == 0) bytes = 64;
+    size_t want = bytes + bytes / 8 + 256;
     HIP_TRY(hipMalloc(&b.p, want));
     b.bytes = want;
     return RT_SUCCESS;
@@ -91,8 +100,9 @@ int n_selected_rows(const rt_render_params* p) {
 int check_params(const rt_render_params* p) {
     if (!p || p->abi_version != RT580_ABI_VERSION) return fail("bad rt_render_params / ABI version");
     if (p->width <= 0 || p->height <= 0) return fail("bad resolution %dx%d", p->width, p->height);
+    if ((int64_t)p->width * p->height > (int64_t)1 << 30) return fail("frame too large");
     if (p->depth < 0 || p->depth > RT_MAX_DEPTH) return fail("depth %d outside [0,%d]", p->depth, RT_MAX_DEPTH);
-    if (p->ao_samples <= 0) return fail("ao_samples must be > 0");
+    if (p->ao_samples <= 0 || p->ao_samples > 512) return fail("ao_samples must be in [1, 512]");
     if (p->rng_engine != RT_RNG_MINSTD_RAND0 && p->rng_engine != RT_RNG_MT19937) return fail("bad rng engine");
     if (p->row_begin < 0 || p->row_end > p->height || p->row_step <= 0) return fail("bad row selection");
     if (!g.inited) return fail("rt_gpu_init not called");
@@ -108,6 +118,7 @@ DevScene dev_scene() {
     s.lights = (const rt_light*)g.lights.p;
     s.n_prims = g.n_prims;
     s.n_lights = g.n_lights;
+    s.n_ambient = g.n_ambient;
     return s;
 }
 
@@ -125,56 +136,83 @@ DevFrame dev_frame(const rt_render_params* p, int row_begin, int row_step, int n
     f.row_step = row_step;
     f.n_rows = n_rows;
     f.view_inverse_ok = p->view_inverse_ok;
-    f.n_ambient = g.n_ambient;
     std::memcpy(f.view_inv, p->view_inv, sizeof f.view_inv);
     std::memcpy(f.cam_from, p->cam_from, sizeof f.cam_from);
     f.ao_angle_max = p->ao_angle_max;
     f.ndc_kx = p->ndc_kx;
     f.ndc_ky = p->ndc_ky;
-    f.mt_stream = (const uint32_t*)g.mt_stream.p;
     return f;
 }
 
-// Count pass over `n_rows` rows starting at row_begin with row_step, into the
-// given per-row / per-pixel buffers.
-int run_count(const rt_render_params* p, int row_begin, int row_step, int n_rows, DevBuf& pix, DevBuf& rc,
-              DevBuf& rt, DevBuf& rh) {
-    size_t npix = (size_t)n_rows * p->width;
-    if (ensure(pix, npix * 4) || ensure(rc, (size_t)n_rows * 4 + 4) || ensure(rt, (size_t)n_rows * 4 + 4) ||
-        ensure(rh, (size_t)n_rows * 4 + 4))
+DevWork dev_work() {
+    DevWork w;
+    w.nodes = (NodeRec*)g.nodes.p;
+    w.rays = (RayItem*)g.rays.p;
+    w.lvl = (uint32_t*)g.lvl.p;
+    w.needed = (uint32_t*)g.needed.p;
+    w.pix_hits = (uint32_t*)g.pix_hits.p;
+    w.pix_nodes = (uint32_t*)g.pix_nodes.p;
+    w.pix_prefix = (uint32_t*)g.pix_prefix.p;
+    w.row_calls = (uint32_t*)g.row_calls.p;
+    w.row_hits = (uint32_t*)g.row_hits.p;
+    w.row_nodes = (uint32_t*)g.row_nodes.p;
+    w.row_base_local = (uint64_t*)g.row_base_local.p;
+    w.totals = (uint64_t*)g.totals.p;
+    w.call_node = (uint32_t*)g.call_node.p;
+    w.call_rng = (uint64_t*)g.call_rng.p;
+    w.occ = (uint32_t*)g.occ.p;
+    w.mt_stream = (const uint32_t*)g.mt_stream.p;
+    w.node_cap = g.node_cap;
+    w.call_cap = g.call_cap;
+    return w;
+}
+
+int begin_frame() {
+    if (!g.profiling) {
+        g.ev = g.ev_default.data();
+        return RT_SUCCESS;
+    }
+    if ((int)g.prof_pool.size() <= g.prof_frames) {
+        std::array<hipEvent_t, EV_N> q;
+        for (auto& e : q) HIP_TRY(hipEventCreate(&e));
+        g.prof_pool.push_back(q);
+    }
+    g.ev = g.prof_pool[g.prof_frames].data();
+    g.prof_frames++;
+    return RT_SUCCESS;
+}
+
+// Size the workspace for n_rows x width pixels.
+int ensure_work(const rt_render_params* p, int n_rows) {
+    const uint64_t npix = (uint64_t)n_rows * p->width;
+    const uint64_t tree_max = (1ull << (p->depth + 1)) - 1;  // nodes of a full tree
+    const double f = g.node_factor < (double)tree_max ? g.node_factor : (double)tree_max;
+    uint64_t cap = (uint64_t)((double)npix * f) + 4096;
+    if (cap < npix) cap = npix;
+    if (cap > 0xffffff00ull) return fail("node capacity exceeds 2^32");
+    const uint64_t ccap = cap * (uint64_t)(g.n_ambient > 0 ? g.n_ambient : 1);
+    if (ccap > 0xffffff00ull) return fail("AO-call capacity exceeds 2^32");
+    if (ensure(g.nodes, cap * sizeof(NodeRec)) || ensure(g.rays, cap * sizeof(RayItem)) ||
+        ensure(g.lvl, 4 * (RT_MAX_DEPTH + 2) * sizeof(uint32_t)) || ensure(g.needed, 64) ||
+        ensure(g.pix_hits, npix * 4) || ensure(g.pix_nodes, npix * 4) || ensure(g.pix_prefix, npix * 4) ||
+        ensure(g.row_calls, (size_t)n_rows * 4) || ensure(g.row_hits, (size_t)n_rows * 4) ||
+        ensure(g.row_nodes, (size_t)n_rows * 4) || ensure(g.row_base_local, (size_t)n_rows * 8) ||
+        ensure(g.totals, 64) || ensure(g.call_node, ccap * 4) || ensure(g.call_rng, ccap * 8) ||
+        ensure(g.occ, ccap * 4))
         return RT_FAILURE;
-    HIP_TRY(hipMemsetAsync(rc.p, 0, (size_t)n_rows * 4, g.stream));
-    HIP_TRY(hipMemsetAsync(rt.p, 0, (size_t)n_rows * 4, g.stream));
-    HIP_TRY(hipMemsetAsync(rh.p, 0, (size_t)n_rows * 4, g.stream));
+    g.node_cap = (uint32_t)cap;
+    g.call_cap = (uint32_t)ccap;
+    return RT_SUCCESS;
+}
+
+// Phase 1: trace every level of the selected rows and count their AO calls.
+int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_rows) {
+    if (ensure_work(p, n_rows)) return RT_FAILURE;
+    HIP_TRY(hipMemsetAsync(g.needed.p, 0, 4, g.stream));
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
-    HIP_TRY(launch_count(dev_scene(), f, (uint32_t*)pix.p, (uint32_t*)rc.p, (uint32_t*)rt.p, (uint32_t*)rh.p,
-                         g.stream));
-    return RT_SUCCESS;
-}
-
-// mt19937: the reference's serial stream is generated on the host up to the
-// last draw this frame needs (no jump-ahead), then uploaded.
-int prepare_mt_stream(const rt_render_params* p, uint64_t total_calls) {
-    if (p->rng_engine != RT_RNG_MT19937 || !p->ao_enabled) return RT_SUCCESS;
-    uint64_t n = total_calls * 2ull * (uint64_t)p->ao_samples;
-    if (ensure(g.mt_stream, n * 4 + 4)) return RT_FAILURE;
-    std::vector<uint32_t> host(n);
-    std::mt19937 gen(p->rng_seed);
-    for (uint64_t i = 0; i < n; i++) host[i] = (uint32_t)gen();
-    HIP_TRY(hipMemcpyAsync(g.mt_stream.p, host.data(), n * 4, hipMemcpyHostToDevice, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
-    return RT_SUCCESS;
-}
-
-int shade(const rt_render_params* p, int n_rows, const uint64_t* row_base_dev, int16_t* fb_out) {
-    size_t npix = (size_t)n_rows * p->width;
-    if (ensure(g.pix_base, npix * 8 + 8)) return RT_FAILURE;
-    HIP_TRY(launch_pixel_base((const uint32_t*)g.pix_calls.p, p->width, n_rows, row_base_dev,
-                              (uint64_t*)g.pix_base.p, g.stream));
-    HIP_TRY(hipEventRecord(g.ev[2], g.stream));
-    DevFrame f = dev_frame(p, p->row_begin, p->row_step, n_rows);
-    HIP_TRY(launch_render(dev_scene(), f, (const uint64_t*)g.pix_base.p, fb_out, g.stream));
-    HIP_TRY(hipEventRecord(g.ev[3], g.stream));
+    HIP_TRY(launch_trace(dev_scene(), f, dev_work(), g.stream));
+    HIP_TRY(launch_row_counts(dev_scene(), f, dev_work(), g.stream));
+    HIP_TRY(hipEventRecord(g.ev[EV_TRACE], g.stream));
     g.last_rows = n_rows;
     g.last_width = p->width;
     g.last_ao_samples = p->ao_samples;
@@ -183,19 +221,57 @@ int shade(const rt_render_params* p, int n_rows, const uint64_t* row_base_dev, i
     return RT_SUCCESS;
 }
 
-// Select the event quadruple for a new frame (profiling: a fresh slot per frame).
-int begin_frame() {
-    if (!g.profiling) {
-        g.ev = g.ev_default;
+// mt19937: the reference's serial stream is generated on the host up to the
+// last draw this frame needs (no jump-ahead), then uploaded.
+int prepare_mt_stream(const rt_render_params* p) {
+    if (p->rng_engine != RT_RNG_MT19937 || !p->ao_enabled || g.n_ambient == 0) return RT_SUCCESS;
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, g.totals.p, 8, hipMemcpyDeviceToHost, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    const uint64_t n = total * 2ull * (uint64_t)p->ao_samples;
+    if (ensure(g.mt_stream, n * 4 + 8)) return RT_FAILURE;
+    std::vector<uint32_t> host(n);
+    std::mt19937 gen(p->rng_seed);
+    for (uint64_t i = 0; i < n; i++) host[i] = (uint32_t)gen();
+    if (n) HIP_TRY(hipMemcpyAsync(g.mt_stream.p, host.data(), n * 4, hipMemcpyHostToDevice, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    return RT_SUCCESS;
+}
+
+// Phase 2: number AO calls (RNG positions), AO, resolve into fb_out.
+int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_rows, const uint64_t* row_base_global,
+               int16_t* fb_out) {
+    DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
+    HIP_TRY(launch_rank(dev_scene(), f, dev_work(), row_base_global, g.stream));
+    HIP_TRY(hipEventRecord(g.ev[EV_RANK], g.stream));
+    if (prepare_mt_stream(p)) return RT_FAILURE;
+    DevWork w = dev_work();
+    HIP_TRY(launch_ao(dev_scene(), f, w, g.stream));
+    HIP_TRY(hipEventRecord(g.ev[EV_AO], g.stream));
+    HIP_TRY(launch_resolve(dev_scene(), f, w, fb_out, g.stream));
+    HIP_TRY(hipEventRecord(g.ev[EV_RESOLVE], g.stream));
+    return RT_SUCCESS;
+}
+
+// Node-capacity check. A (params, scene) pair that already rendered without
+// overflow never overflows again (the frame is deterministic); otherwise wait
+// for the frame and read the highest node id it requested.
+int check_capacity(const rt_render_params* p, bool& retry) {
+    retry = false;
+    if (g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0)
+        return RT_SUCCESS;
+    HIP_TRY(hipMemcpyAsync(g.needed_host, g.needed.p, 4, hipMemcpyDeviceToHost, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    const uint32_t need = *g.needed_host;
+    if (need > g.node_cap) {
+        const uint64_t npix = (uint64_t)g.last_rows * p->width;
+        g.node_factor = (double)need / (double)(npix ? npix : 1) * 1.25 + 0.5;
+        retry = true;
         return RT_SUCCESS;
     }
-    if ((int)g.prof_pool.size() <= g.prof_frames) {
-        std::array<hipEvent_t, 4> q;
-        for (auto& e : q) HIP_TRY(hipEventCreate(&e));
-        g.prof_pool.push_back(q);
-    }
-    g.ev = g.prof_pool[g.prof_frames].data();
-    g.prof_frames++;
+    g.verified = *p;
+    g.verified_gen = g.scene_gen;
+    g.verified_valid = true;
     return RT_SUCCESS;
 }
 
@@ -218,17 +294,19 @@ int rt_gpu_init(int device) {
     HIP_TRY(hipStreamCreateWithFlags(&g.own_stream, hipStreamNonBlocking));
     g.stream = g.own_stream;
     for (auto& ev : g.ev_default) HIP_TRY(hipEventCreate(&ev));
-    g.ev = g.ev_default;
+    g.ev = g.ev_default.data();
+    HIP_TRY(hipHostMalloc((void**)&g.needed_host, 64, hipHostMallocDefault));
     upload_minstd_table(g.stream);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(g.stream));
     g.inited = true;
     return RT_SUCCESS;
 }
 
 int rt_gpu_set_stream(void* s) {
     if (!g.inited) return fail("rt_gpu_init not called");
+    HIP_TRY(hipStreamSynchronize(g.stream));
     g.stream = s ? (hipStream_t)s : g.own_stream;
-    upload_minstd_table(g.stream);
     return RT_SUCCESS;
 }
 
@@ -236,6 +314,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     if (!g.inited && rt_gpu_init(-1) != RT_SUCCESS) return RT_FAILURE;
     if (!s || s->abi_version != RT580_ABI_VERSION) return fail("bad rt_scene_soa / ABI version");
     if (s->n_prims < 0 || s->n_lights < 0 || s->n_materials < 0) return fail("negative scene sizes");
+    if (s->n_prims > 0 && (!s->prims || !s->shade)) return fail("null primitive arrays");
     for (int i = 0; i < s->n_prims; i++)
         if (s->prims[i].shape < 0 || s->prims[i].shape >= s->n_materials ||
             (s->prims[i].kind != RT_PRIM_TRIANGLE && s->prims[i].kind != RT_PRIM_SPHERE))
@@ -244,6 +323,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         if (s->lights[i].kind < RT_LIGHT_DIRECTIONAL || s->lights[i].kind > RT_LIGHT_AMBIENT)
             return fail("light %d: bad kind", i);
     HIP_TRY(hipSetDevice(g.device));
+    HIP_TRY(hipStreamSynchronize(g.stream));
     if (ensure(g.prims, sizeof(rt_prim) * (size_t)s->n_prims + 64) ||
         ensure(g.shade, sizeof(rt_prim_shade) * (size_t)s->n_prims + 64) ||
         ensure(g.mats, sizeof(rt_material) * (size_t)s->n_materials + 64) ||
@@ -267,6 +347,52 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         else g.n_nonambient++;
     }
     g.have_scene = true;
+    g.scene_gen++;
+    return RT_SUCCESS;
+}
+
+int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
+    if (check_params(p)) return RT_FAILURE;
+    HIP_TRY(hipSetDevice(g.device));
+    const int n_sel = n_selected_rows(p);
+    const bool prefix = p->row_begin == 0 && p->row_step == 1;
+    // The RNG offsets need every row before a selected one: render the prefix
+    // [0, row_end) and copy the selected rows out when the selection is sparse.
+    const int n_rows = prefix ? n_sel : p->row_end;
+    for (int attempt = 0; attempt < 4; attempt++) {
+        if (begin_frame()) return RT_FAILURE;
+        HIP_TRY(hipEventRecord(g.ev[EV_START], g.stream));
+        if (trace_rows(p, 0, 1, n_rows)) return RT_FAILURE;
+        int16_t* out;
+        if (prefix) {
+            if (ensure(g.fb, (size_t)n_rows * p->width * 6)) return RT_FAILURE;
+            out = (int16_t*)g.fb.p;
+        } else {
+            if (ensure(g.fb_full, (size_t)n_rows * p->width * 6)) return RT_FAILURE;
+            out = (int16_t*)g.fb_full.p;
+        }
+        if (shade_rows(p, 0, 1, n_rows, nullptr, out)) return RT_FAILURE;
+        if (!prefix) {
+            if (ensure(g.fb, (size_t)n_sel * p->width * 6)) return RT_FAILURE;
+            HIP_TRY(launch_copy_rows(out, p->width, p->row_begin, p->row_step, n_sel, (int16_t*)g.fb.p, g.stream));
+        }
+        bool retry = false;
+        if (check_capacity(p, retry)) return RT_FAILURE;
+        if (!retry) {
+            if (fb_device) *fb_device = (int16_t*)g.fb.p;
+            return RT_SUCCESS;
+        }
+        if (g.profiling) g.prof_frames--;
+    }
+    return fail("node capacity could not be sized");
+}
+
+int rt_gpu_render(const rt_render_params* p, int16_t* fb_out) {
+    int16_t* dev = nullptr;
+    if (rt_gpu_render_device(p, &dev)) return RT_FAILURE;
+    const size_t bytes = (size_t)n_selected_rows(p) * p->width * 6;
+    if (bytes && fb_out) HIP_TRY(hipMemcpyAsync(fb_out, dev, bytes, hipMemcpyDeviceToHost, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
     return RT_SUCCESS;
 }
 
@@ -274,15 +400,20 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
     if (check_params(p)) return RT_FAILURE;
     if (!row_calls_device) return fail("row_calls_device is NULL");
     HIP_TRY(hipSetDevice(g.device));
-    int n_rows = n_selected_rows(p);
-    if (begin_frame()) return RT_FAILURE;
-    HIP_TRY(hipEventRecord(g.ev[0], g.stream));
-    if (run_count(p, p->row_begin, p->row_step, n_rows, g.pix_calls, g.row_calls, g.row_tree, g.row_hits))
-        return RT_FAILURE;
+    const int n_rows = n_selected_rows(p);
+    for (int attempt = 0; attempt < 4; attempt++) {
+        if (begin_frame()) return RT_FAILURE;
+        HIP_TRY(hipEventRecord(g.ev[EV_START], g.stream));
+        if (trace_rows(p, p->row_begin, p->row_step, n_rows)) return RT_FAILURE;
+        bool retry = false;
+        if (check_capacity(p, retry)) return RT_FAILURE;
+        if (!retry) break;
+        if (attempt == 3) return fail("node capacity could not be sized");
+        if (g.profiling) g.prof_frames--;
+    }
     if (n_rows)
         HIP_TRY(hipMemcpyAsync(row_calls_device, g.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToDevice,
                                g.stream));
-    HIP_TRY(hipEventRecord(g.ev[1], g.stream));
     g.split_params = *p;
     g.split_ready = true;
     return RT_SUCCESS;
@@ -297,60 +428,7 @@ int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device
         return fail("rt_gpu_shade_rows must follow rt_gpu_count_rows with the same params");
     HIP_TRY(hipSetDevice(g.device));
     g.split_ready = false;
-    return shade(p, n_selected_rows(p), row_base_device, fb_device);
-}
-
-int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
-    if (check_params(p)) return RT_FAILURE;
-    HIP_TRY(hipSetDevice(g.device));
-    const int n_rows = n_selected_rows(p);
-    const bool prefix = p->row_begin == 0 && p->row_step == 1;
-    if (begin_frame()) return RT_FAILURE;
-    HIP_TRY(hipEventRecord(g.ev[0], g.stream));
-    // RNG offsets: the count pass must cover every row that precedes a selected row.
-    if (ensure(g.row_base, (size_t)n_rows * 8 + 8)) return RT_FAILURE;
-    uint64_t total_calls = 0;
-    if (prefix) {
-        if (run_count(p, 0, 1, n_rows, g.pix_calls, g.row_calls, g.row_tree, g.row_hits)) return RT_FAILURE;
-        HIP_TRY(launch_row_base((const uint32_t*)g.row_calls.p, n_rows, (uint64_t*)g.row_base.p, g.stream));
-        if (p->rng_engine == RT_RNG_MT19937 && p->ao_enabled) {
-            std::vector<uint32_t> rc(n_rows);
-            HIP_TRY(hipMemcpyAsync(rc.data(), g.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToHost, g.stream));
-            HIP_TRY(hipStreamSynchronize(g.stream));
-            for (uint32_t c : rc) total_calls += c;
-        }
-    } else {
-        const int all_rows = p->row_end;
-        if (run_count(p, 0, 1, all_rows, g.cnt_pix_all, g.cnt_calls_all, g.cnt_tree_all, g.cnt_hits_all))
-            return RT_FAILURE;
-        if (ensure(g.row_base_all, (size_t)all_rows * 8 + 8)) return RT_FAILURE;
-        HIP_TRY(launch_row_base((const uint32_t*)g.cnt_calls_all.p, all_rows, (uint64_t*)g.row_base_all.p, g.stream));
-        HIP_TRY(launch_select_rows((const uint64_t*)g.row_base_all.p, p->row_begin, p->row_step, n_rows,
-                                   (uint64_t*)g.row_base.p, g.stream));
-        if (p->rng_engine == RT_RNG_MT19937 && p->ao_enabled) {
-            std::vector<uint32_t> rc(all_rows);
-            HIP_TRY(hipMemcpyAsync(rc.data(), g.cnt_calls_all.p, (size_t)all_rows * 4, hipMemcpyDeviceToHost, g.stream));
-            HIP_TRY(hipStreamSynchronize(g.stream));
-            for (uint32_t c : rc) total_calls += c;
-        }
-        if (run_count(p, p->row_begin, p->row_step, n_rows, g.pix_calls, g.row_calls, g.row_tree, g.row_hits))
-            return RT_FAILURE;
-    }
-    HIP_TRY(hipEventRecord(g.ev[1], g.stream));
-    if (prepare_mt_stream(p, total_calls)) return RT_FAILURE;
-    if (ensure(g.fb, (size_t)n_rows * p->width * 6 + 6)) return RT_FAILURE;
-    if (shade(p, n_rows, (const uint64_t*)g.row_base.p, (int16_t*)g.fb.p)) return RT_FAILURE;
-    if (fb_device) *fb_device = (int16_t*)g.fb.p;
-    return RT_SUCCESS;
-}
-
-int rt_gpu_render(const rt_render_params* p, int16_t* fb_out) {
-    int16_t* dev = nullptr;
-    if (rt_gpu_render_device(p, &dev)) return RT_FAILURE;
-    size_t bytes = (size_t)n_selected_rows(p) * p->width * 6;
-    if (bytes) HIP_TRY(hipMemcpyAsync(fb_out, dev, bytes, hipMemcpyDeviceToHost, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
-    return RT_SUCCESS;
+    return shade_rows(p, p->row_begin, p->row_step, n_selected_rows(p), row_base_device, fb_device);
 }
 
 int rt_gpu_last_stats(rt_render_stats* st) {
@@ -358,15 +436,15 @@ int rt_gpu_last_stats(rt_render_stats* st) {
     std::memset(st, 0, sizeof *st);
     if (!g.last_valid) return fail("no frame rendered yet");
     HIP_TRY(hipStreamSynchronize(g.stream));
-    int n = g.last_rows;
-    std::vector<uint32_t> rc(n), rt(n), rh(n);
+    const int n = g.last_rows;
+    std::vector<uint32_t> rc(n), rh(n), rn(n);
     if (n) {
         HIP_TRY(hipMemcpy(rc.data(), g.row_calls.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(rt.data(), g.row_tree.p, (size_t)n * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(rh.data(), g.row_hits.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(rn.data(), g.row_nodes.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     }
-    uint64_t calls = 0, tree = 0, hits = 0;
-    for (int i = 0; i < n; i++) { calls += rc[i]; tree += rt[i]; hits += rh[i]; }
+    uint64_t calls = 0, hits = 0, tree = 0;
+    for (int i = 0; i < n; i++) { calls += rc[i]; hits += rh[i]; tree += rn[i]; }
     st->rays_primary = (uint64_t)n * g.last_width;
     st->rays_secondary = tree - st->rays_primary;
     st->rays_shadow = hits * (uint64_t)g.n_nonambient;
@@ -374,35 +452,37 @@ int rt_gpu_last_stats(rt_render_stats* st) {
     st->rays_ao = g.last_ao_enabled ? calls * (uint64_t)g.last_ao_samples : 0;
     st->rays_total = tree + st->rays_shadow + st->rays_ao;
     float ms = 0;
-    if (hipEventElapsedTime(&ms, g.ev[0], g.ev[1]) == hipSuccess) st->ms_count = ms;
-    if (hipEventElapsedTime(&ms, g.ev[1], g.ev[2]) == hipSuccess) st->ms_scan = ms;
-    if (hipEventElapsedTime(&ms, g.ev[2], g.ev[3]) == hipSuccess) st->ms_render = ms;
-    if (hipEventElapsedTime(&ms, g.ev[0], g.ev[3]) == hipSuccess) st->ms_total = ms;
+    if (hipEventElapsedTime(&ms, g.ev[EV_START], g.ev[EV_TRACE]) == hipSuccess) st->ms_count = ms;
+    if (hipEventElapsedTime(&ms, g.ev[EV_TRACE], g.ev[EV_RANK]) == hipSuccess) st->ms_scan = ms;
+    if (hipEventElapsedTime(&ms, g.ev[EV_RANK], g.ev[EV_RESOLVE]) == hipSuccess) st->ms_render = ms;
+    if (hipEventElapsedTime(&ms, g.ev[EV_START], g.ev[EV_RESOLVE]) == hipSuccess) st->ms_total = ms;
     return RT_SUCCESS;
 }
 
 int rt_gpu_profile(int enable) {
     if (!g.inited) return fail("rt_gpu_init not called");
+    HIP_TRY(hipStreamSynchronize(g.stream));
     g.profiling = enable != 0;
     g.prof_frames = 0;
-    g.ev = g.ev_default;
+    g.ev = g.ev_default.data();
     return RT_SUCCESS;
 }
 
-int rt_gpu_profile_read(double* ms_count, double* ms_scan, double* ms_render, int* frames) {
+int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double* ms_resolve, int* frames) {
     if (!g.inited) return fail("rt_gpu_init not called");
     HIP_TRY(hipStreamSynchronize(g.stream));
-    double c = 0, s = 0, r = 0;
+    double t[4] = {0, 0, 0, 0};
     for (int i = 0; i < g.prof_frames; i++) {
-        float a = 0, b = 0, d = 0;
-        HIP_TRY(hipEventElapsedTime(&a, g.prof_pool[i][0], g.prof_pool[i][1]));
-        HIP_TRY(hipEventElapsedTime(&b, g.prof_pool[i][1], g.prof_pool[i][2]));
-        HIP_TRY(hipEventElapsedTime(&d, g.prof_pool[i][2], g.prof_pool[i][3]));
-        c += a; s += b; r += d;
+        for (int k = 0; k < 4; k++) {
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, g.prof_pool[i][k], g.prof_pool[i][k + 1]));
+            t[k] += ms;
+        }
     }
-    if (ms_count) *ms_count = c;
-    if (ms_scan) *ms_scan = s;
-    if (ms_render) *ms_render = r;
+    if (ms_trace) *ms_trace = t[0];
+    if (ms_rank) *ms_rank = t[1];
+    if (ms_ao) *ms_ao = t[2];
+    if (ms_resolve) *ms_resolve = t[3];
     if (frames) *frames = g.prof_frames;
     return RT_SUCCESS;
 }
@@ -413,14 +493,15 @@ void rt_gpu_shutdown(void) {
     if (!g.inited) return;
     (void)hipSetDevice(g.device);
     (void)hipStreamSynchronize(g.stream);
-    for (DevBuf* b : {&g.prims, &g.shade, &g.mats, &g.lights, &g.pix_calls, &g.pix_base, &g.row_calls,
-                      &g.row_tree, &g.row_hits, &g.row_base, &g.row_base_all, &g.fb, &g.mt_stream,
-                      &g.cnt_calls_all, &g.cnt_tree_all, &g.cnt_hits_all, &g.cnt_pix_all})
+    for (DevBuf* b : {&g.prims, &g.shade, &g.mats, &g.lights, &g.nodes, &g.rays, &g.lvl, &g.needed, &g.pix_hits,
+                      &g.pix_nodes, &g.pix_prefix, &g.row_calls, &g.row_hits, &g.row_nodes, &g.row_base_local,
+                      &g.totals, &g.call_node, &g.call_rng, &g.occ, &g.fb, &g.fb_full, &g.mt_stream})
         release(*b);
     for (auto& ev : g.ev_default)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& q : g.prof_pool)
         for (auto& ev : q) (void)hipEventDestroy(ev);
+    if (g.needed_host) (void)hipHostFree(g.needed_host);
     if (g.own_stream) (void)hipStreamDestroy(g.own_stream);
     g = State();
 }

@@ -109,9 +109,10 @@ def main():
     barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    c_ms, s_ms, r_ms, frames = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
-    rt580.check(lib.rt_gpu_profile_read(ctypes.byref(c_ms), ctypes.byref(s_ms), ctypes.byref(r_ms),
-                                        ctypes.byref(frames)), "rt_gpu_profile_read")
+    ms = [ctypes.c_double() for _ in range(4)]
+    frames = ctypes.c_int()
+    rt580.check(lib.rt_gpu_profile_read(*[ctypes.byref(m) for m in ms], ctypes.byref(frames)), "rt_gpu_profile_read")
+    per_frame = [m.value / max(frames.value, 1) for m in ms]  # trace, rank, ao, resolve
     rt580.check(lib.rt_gpu_profile(0), "rt_gpu_profile")
 
     rays_local = int(local["rays_total"])
@@ -128,8 +129,9 @@ def main():
     if rank == 0:
         value = rays_frame * args.steps / dt / 1e6
         bytes_per_ray = 56 * n_tri + 16 * n_sph  # SoA primitive records, no reuse
-        render_ms = r_ms.value / max(frames.value, 1)
-        achieved = rays_local * bytes_per_ray / (render_ms * 1e-3) / 1e9 if render_ms > 0 else 0.0
+        ao_ms = per_frame[2]
+        # dominant kernel: ao_kernel (one launch = this rank's AO rays of a frame)
+        achieved = int(local["rays_ao"]) * bytes_per_ray / (ao_ms * 1e-3) / 1e9 if ao_ms > 0 else 0.0
         out = {
             "metric": "Mrays/sec (+ ms/frame) at 1920x1080, depth=4, 64 AO samples",
             "value": round(value, 3),
@@ -151,12 +153,13 @@ def main():
                 "parallelism": "interleaved rows x%d + RCCL all_gather/gather" % world if world > 1 else "1 GPU",
             },
             "kernel_ms_per_frame": {
-                "count": round(c_ms.value / max(frames.value, 1), 4),
-                "scan": round(s_ms.value / max(frames.value, 1), 4),
-                "render": round(render_ms, 4),
+                "trace": round(per_frame[0], 4),
+                "rank": round(per_frame[1], 4),
+                "ao": round(per_frame[2], 4),
+                "resolve": round(per_frame[3], 4),
             },
             "roofline": {
-                "kernel": "render_kernel",
+                "kernel": "ao_kernel",
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
@@ -164,9 +167,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": measured_traffic(),
                 "bytes_per_ray": bytes_per_ray,
-                "note": "algorithmic scene-stream bytes (56*T + 16*S per ray, SURVEY §8d) x rays of one "
-                        "launch / mean render_kernel duration (HIP events on its stream); the kernel itself "
-                        "is VALU-bound (scene of %d prims stays in scalar cache)" % len(prims),
+                "rays_per_launch": int(local["rays_ao"]),
+                "note": "algorithmic scene-stream bytes (56*T + 16*S per ray, SURVEY §8d) x AO rays of one "
+                        "ao_kernel launch / its mean duration (HIP events on its stream); the kernel itself "
+                        "is VALU-bound (the %d-primitive scene is re-read from LDS, not HBM)" % len(prims),
             },
         }
         if world == 1 and not args.no_cpu_baseline:

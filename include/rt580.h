@@ -137,10 +137,10 @@ typedef struct rt_render_stats {
     uint64_t rays_shadow;      /* directional + point shadow rays */
     uint64_t rays_ao;          /* AO rays */
     uint64_t ao_calls;         /* CalculateAmbientOcclusion calls */
-    double ms_count;           /* count/offset pass (HIP events) */
-    double ms_scan;
-    double ms_render;          /* shading megakernel */
-    double ms_total;           /* first launch -> framebuffer on host */
+    double ms_count;           /* breadth-first trace + per-row AO-call counts (HIP events) */
+    double ms_scan;            /* AO-call numbering (RNG positions) */
+    double ms_render;          /* AO kernel + resolve kernel */
+    double ms_total;           /* first launch -> framebuffer in HBM */
 } rt_render_stats;
 
 /* Select the device (device < 0: $LOCAL_RANK or 0) and create streams/events. */
@@ -171,10 +171,12 @@ int rt_gpu_shade_rows(const rt_render_params* params, const uint64_t* row_base_d
 /* Counters and HIP-event timings of the last render. */
 int rt_gpu_last_stats(rt_render_stats* stats);
 /* Bench profiling: with enable=1 every following frame records its own HIP
- * events (count pass, scan, render kernel) on the shim's stream; profile_read
- * synchronizes and returns the sums over those frames. */
+ * events on the shim's stream; profile_read synchronizes and returns the sums
+ * over those frames of: the breadth-first trace of the recursion tree (+ per-row
+ * AO-call counts), the AO-call numbering (RNG positions), the AO kernel, and the
+ * resolve (int16 blend) kernel. */
 int rt_gpu_profile(int enable);
-int rt_gpu_profile_read(double* ms_count, double* ms_scan, double* ms_render, int* frames);
+int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double* ms_resolve, int* frames);
 /* Last error message (static storage). */
 const char* rt_gpu_last_error(void);
 void rt_gpu_shutdown(void);
