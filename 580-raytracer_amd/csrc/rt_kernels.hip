@@ -123,13 +123,17 @@ __device__ __forceinline__ void load_tile(const rt_prim* __restrict__ prims, int
 // IntersectScene, closest hit (Raytracer.cpp:473-526): primitives in the
 // reference's order; the first hit is taken unconditionally, later ones only if
 // strictly closer. Workgroup-uniform call; `active` lanes test.
-__device__ bool closest_hit(const DevScene& S, rt_prim* tile, bool active, rv3 o, rv3 d, Hit& h) {
+// With resident == true the whole scene (<= TILE primitives) is already in the
+// tile and no barrier is needed.
+__device__ bool closest_hit(const DevScene& S, rt_prim* tile, bool resident, bool active, rv3 o, rv3 d, Hit& h) {
     bool found = false;
     for (int base = 0; base < S.n_prims; base += TILE) {
         const int n = min(TILE, S.n_prims - base);
-        __syncthreads();
-        load_tile(S.prims, base, n, tile);
-        __syncthreads();
+        if (!resident) {
+            __syncthreads();
+            load_tile(S.prims, base, n, tile);
+            __syncthreads();
+        }
         if (active) {
             for (int j = 0; j < n; j++) {
                 const rt_prim& P = tile[j];
@@ -147,13 +151,15 @@ __device__ bool closest_hit(const DevScene& S, rt_prim* tile, bool active, rv3 o
 
 // IntersectScene where only the boolean is read (directional shadows, AO rays):
 // any hit, with a workgroup-wide early exit once every active lane has hit.
-__device__ bool any_hit(const DevScene& S, rt_prim* tile, bool active, rv3 o, rv3 d) {
+__device__ bool any_hit(const DevScene& S, rt_prim* tile, bool resident, bool active, rv3 o, rv3 d) {
     bool hit = false;
     for (int base = 0; base < S.n_prims; base += TILE) {
         const int n = min(TILE, S.n_prims - base);
-        __syncthreads();
-        load_tile(S.prims, base, n, tile);
-        __syncthreads();
+        if (!resident) {
+            __syncthreads();
+            load_tile(S.prims, base, n, tile);
+            __syncthreads();
+        }
         if (active && !hit) {
             for (int j = 0; j < n; j++) {
                 const rt_prim& P = tile[j];
@@ -167,6 +173,16 @@ __device__ bool any_hit(const DevScene& S, rt_prim* tile, bool active, rv3 o, rv
         if (base + TILE < S.n_prims && __syncthreads_and(!active || hit)) break;
     }
     return hit;
+}
+
+// Small scenes (<= TILE primitives) are staged once per workgroup and stay resident.
+__device__ __forceinline__ bool stage_resident(const DevScene& S, rt_prim* tile) {
+    const bool resident = S.n_prims <= TILE;
+    if (resident) {
+        load_tile(S.prims, 0, S.n_prims, tile);
+        __syncthreads();
+    }
+    return resident;
 }
 
 // ---------------------------------------------------------------- camera
@@ -312,6 +328,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
     const uint32_t next_base = base_id + count;
     if (blockIdx.x == 0 && threadIdx.x == 0) W.lvl[LVL_BASE + level + 1] = next_base;
     const int bounces = F.depth - level;
+    const bool resident = stage_resident(S, tile);
 
     for (uint32_t b0 = blockIdx.x * TB; b0 < count; b0 += gridDim.x * TB) {
         const uint32_t item = b0 + threadIdx.x;
@@ -332,7 +349,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             }
         }
         Hit h;
-        const bool hit = closest_hit(S, tile, active, o, d, h);
+        const bool hit = closest_hit(S, tile, resident, active, o, d, h);
 
         HitInfo hi;
         rt_material m;
@@ -369,10 +386,10 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             }
             bool occluded;
             if (l.kind == RT_LIGHT_DIRECTIONAL) {
-                occluded = any_hit(S, tile, hit, so, L2);
+                occluded = any_hit(S, tile, resident, hit, so, L2);
             } else {
                 Hit sh;
-                const bool shit = closest_hit(S, tile, hit, so, L2, sh);
+                const bool shit = closest_hit(S, tile, resident, hit, so, L2, sh);
                 occluded = shit && !(sh.t > dist);
             }
             if (hit && !occluded) local = px_add(local, local_color(S, F, hi, l, m, L));
@@ -562,6 +579,7 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
     const bool pow2 = (N & (N - 1)) == 0;
     const int log2n = 31 - __clz((int)N);
     const bool wave_per_call = (N & 63u) == 0;
+    const bool resident = stage_resident(S, tile);
     for (uint64_t b0 = (uint64_t)blockIdx.x * TB; b0 < items; b0 += (uint64_t)gridDim.x * TB) {
         const uint64_t item = b0 + threadIdx.x;
         const bool active = item < items;
@@ -591,13 +609,13 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
             const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
             const float r = sqrtf(1 - z * z);
             double sa, ca;
-            rt_glibc_sincos((double)ang, &sa, &ca);
+            rt_glibc_sincos_simd((double)ang, &sa, &ca);
             rv3 v = v3_normalize(v3((float)((double)r * ca), (float)((double)r * sa), z));
             if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
             o = v3_add(hp, v3_scale(v, 0.2f));
             d = v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
         }
-        const bool hit = any_hit(S, tile, active, o, d);
+        const bool hit = any_hit(S, tile, resident, active, o, d);
         if (wave_per_call) {
             const uint64_t m = __ballot(active && hit);
             if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.occ[c], (uint32_t)__popcll(m));

@@ -245,6 +245,44 @@ RT_HD int rt_sc_reduce(double x, double* a, double* da) {
     return n;
 }
 
+// Branch-light form of rt_glibc_sincos for SIMD execution: every range of
+// s_sincos.c ends in do_sin(a, da) and do_cos(a, da) on a range-specific (a, da),
+// followed by a swap / negation / copysign. Computing (a, da) per lane and then
+// ONE do_sin and ONE do_cos keeps a wavefront of random angles on a single path
+// (the divergent form runs up to three). Same operations on the same operands,
+// so the same bits (checked exhaustively against glibc, tests/native/libm_check.cpp).
+RT_HD void rt_glibc_sincos_simd(double x, double* sinx, double* cosx) {
+    const uint32_t k = (uint32_t)(rt_d2u(x) >> 32) & 0x7fffffffu;
+    double a = x, da = 0.0;
+    int mode;  // 0: small, 1: 0.855..2.426, 2: reduced
+    int n = 0;
+    if (k < 0x3feb6000u) {
+        mode = 0;
+    } else if (k < 0x400368fdu) {
+        mode = 1;
+        const double y = RT_SC_HP0 - fabs(x);
+        a = y + RT_SC_HP1;
+        da = (y - a) + RT_SC_HP1;
+    } else {
+        mode = 2;
+        n = rt_sc_reduce(x, &a, &da) & 3;
+        if (n == 1 || n == 2) { a = -a; da = -da; }
+    }
+    const double S = rt_sc_do_sin(a, da);
+    const double C = rt_sc_do_cos(a, da);
+    double sv, cv;
+    if (mode == 0) { sv = S; cv = C; }
+    else if (mode == 1) { sv = copysign(C, x); cv = S; }
+    else {
+        const double Cn = (n & 2) ? -C : C;
+        if (n & 1) { cv = S; sv = Cn; } else { sv = S; cv = Cn; }
+    }
+    if (k < 0x3e400000u) { sv = x; cv = 1.0; }              // |x| < 2^-27
+    if (k >= 0x419921fbu) { sv = cv = (x - x) / (x - x); }  // outside the path's domain
+    *sinx = sv;
+    *cosx = cv;
+}
+
 // Valid for |x| < 105414350 (the reference only passes angles in [0, 2*pi)).
 // Larger finite |x| would need __branred; it returns NaN there so a misuse is loud.
 RT_HD void rt_glibc_sincos(double x, double* sinx, double* cosx) {

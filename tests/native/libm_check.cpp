@@ -42,11 +42,14 @@ int main(int argc, char** argv) {
             long bad = 0;
             for (uint64_t u = lo; u < hi; u++) {
                 double a = (double)rt_u2f((uint32_t)u);
-                double s0, c0, s1, c1;
+                double s0, c0, s1, c1, s2, c2;
                 sincos(a, &s0, &c0);
                 rt_glibc_sincos(a, &s1, &c1);
+                rt_glibc_sincos_simd(a, &s2, &c2);
                 if (rt_d2u(s0) != rt_d2u(s1)) { bad++; report("sin", a, 0, s1, s0); }
                 if (rt_d2u(c0) != rt_d2u(c1)) { bad++; report("cos", a, 0, c1, c0); }
+                if (rt_d2u(s0) != rt_d2u(s2)) { bad++; report("sin_simd", a, 0, s2, s0); }
+                if (rt_d2u(c0) != rt_d2u(c2)) { bad++; report("cos_simd", a, 0, c2, c0); }
             }
             g_bad += bad; g_checked += (long)(hi - lo);
         });
