@@ -78,21 +78,43 @@ struct Hit {
 
 __device__ __forceinline__ rv3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
 
-// IntersectTriangle (Raytracer.cpp:348-409) with the ray-invariant part precomputed.
-__device__ __forceinline__ bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b,
-                                         float& g) {
-    rv3 N = ld3(P.nrm);
-    float nd = v3_dot(N, d);
+// (num / den) < 0 exactly as the division would decide it, dividing only when
+// the signs do not already decide it (the quotient can still round to -0).
+__device__ __forceinline__ bool quot_lt0(float num, float den) {
+    if (num != num || den != den || num == 0.0f) return false;  // NaN, or +-0 / den
+    if (signbit(num) == signbit(den)) return false;             // > 0, +0 or +inf
+    return (num / den) < 0.0f;
+}
+
+// IntersectTriangle (Raytracer.cpp:348-409) with the ray-invariant part
+// precomputed. WANT_BARY: also return alpha/beta/gamma (closest hit); the
+// any-hit form only needs the accept/reject decision. Both decide exactly as
+// the reference's divisions would.
+template <bool WANT_BARY>
+__device__ __forceinline__ bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
+    const rv3 N = ld3(P.nrm);
+    const float nd = v3_dot(N, d);
     if (rt_lt_eps(fabsf(nd))) return false;  // NearlyEquals(nd, 0)
-    t = -(v3_dot(N, o) + P.d) / nd;
+    const float num = -(v3_dot(N, o) + P.d);
+    // t = num / nd <= EPSILON: decided by signs when t <= 0 (|nd| > EPSILON here)
+    if (num == num && (num == 0.0f || signbit(num) != signbit(nd))) return false;
+    t = num / nd;
     if (rt_lt_eps(t)) return false;           // t <= EPSILON
-    rv3 Pp = v3_add(o, v3_scale(d, t));
-    rv3 v0 = ld3(P.p0), v1 = ld3(P.p1), v2 = ld3(P.p2);
+    const rv3 Pp = v3_add(o, v3_scale(d, t));
+    const rv3 v0 = ld3(P.p0), v1 = ld3(P.p1), v2 = ld3(P.p2);
     // CalcTriangleAreaSigned (Raytracer.cpp:937-942): 0.5 * dot(cross(B-A, C-A), N)
-    a = (0.5f * v3_dot(v3_cross(v3_sub(v1, Pp), v3_sub(v2, Pp)), N)) / P.area;
-    b = (0.5f * v3_dot(v3_cross(v3_sub(Pp, v0), v3_sub(v2, v0)), N)) / P.area;
-    g = (0.5f * v3_dot(v3_cross(v3_sub(v1, v0), v3_sub(Pp, v0)), N)) / P.area;
-    return !(a < 0 || b < 0 || g < 0);
+    const float aa = 0.5f * v3_dot(v3_cross(v3_sub(v1, Pp), v3_sub(v2, Pp)), N);
+    if (quot_lt0(aa, P.area)) return false;
+    const float bb = 0.5f * v3_dot(v3_cross(v3_sub(Pp, v0), v3_sub(v2, v0)), N);
+    if (quot_lt0(bb, P.area)) return false;
+    const float gg = 0.5f * v3_dot(v3_cross(v3_sub(v1, v0), v3_sub(Pp, v0)), N);
+    if (quot_lt0(gg, P.area)) return false;
+    if (WANT_BARY) {
+        a = aa / P.area;
+        b = bb / P.area;
+        g = gg / P.area;
+    }
+    return true;
 }
 
 // IntersectSphere (Raytracer.cpp:419-464)
@@ -138,7 +160,7 @@ __device__ bool closest_hit(const DevScene& S, rt_prim* tile, bool resident, boo
             for (int j = 0; j < n; j++) {
                 const rt_prim& P = tile[j];
                 float t, a = 0, b = 0, g = 0;
-                bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+                bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test<true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
                 if (hit && (!found || t < h.t)) {
                     found = true;
                     h.t = t; h.a = a; h.b = b; h.g = g; h.prim = base + j;
@@ -164,7 +186,7 @@ __device__ bool any_hit(const DevScene& S, rt_prim* tile, bool resident, bool ac
             for (int j = 0; j < n; j++) {
                 const rt_prim& P = tile[j];
                 float t, a, b, g;
-                if (P.kind == RT_PRIM_TRIANGLE ? tri_test(P, o, d, t, a, b, g) : sph_test(P, o, d, t)) {
+                if (P.kind == RT_PRIM_TRIANGLE ? tri_test<false>(P, o, d, t, a, b, g) : sph_test(P, o, d, t)) {
                     hit = true;
                     break;
                 }
@@ -574,6 +596,9 @@ __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWor
 // + RandomUnitVector (:269-281): one lane per (call, sample).
 __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork W) {
     __shared__ rt_prim tile[TILE];
+    __shared__ double sct[440];  // glibc __sincostab, staged once per workgroup
+    for (int i = threadIdx.x; i < 440; i += TB) sct[i] = rt_dev::rt_sincostab[i];
+    __syncthreads();
     const uint32_t N = (uint32_t)F.ao_samples;
     const uint64_t items = W.totals[0] * (uint64_t)N;
     const bool pow2 = (N & (N - 1)) == 0;
@@ -591,16 +616,32 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
         }
         rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
         if (active) {
-            const NodeRec& nd = W.nodes[W.call_node[c]];
-            const rv3 hp = ld3(nd.hp), n = ld3(nd.n);
+            // With N a multiple of 64 a wave serves one call: keep its data scalar.
+            uint32_t cc = (uint32_t)c;
+            if (wave_per_call) cc = __builtin_amdgcn_readfirstlane(cc);
+            uint32_t node = W.call_node[cc];
+            if (wave_per_call) node = __builtin_amdgcn_readfirstlane(node);
+            const NodeRec& nd = W.nodes[node];
+            rv3 hp = ld3(nd.hp), n = ld3(nd.n);
+            uint64_t rbase = W.call_rng[cc];
+            if (wave_per_call) {
+                hp = v3(__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.x))),
+                        __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.y))),
+                        __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.z))));
+                n = v3(__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.x))),
+                       __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.y))),
+                       __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.z))));
+                rbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rbase >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)rbase);
+            }
             float u0, u1;
             if (F.rng_engine == RT_RNG_MINSTD_RAND0) {
-                uint32_t st = mersenne31_mul((uint32_t)W.call_rng[c], c_minstd_j1[s]);
+                uint32_t st = mersenne31_mul((uint32_t)rbase, c_minstd_j1[s]);
                 u0 = canon_minstd(st);
                 st = mersenne31_mul(st, 16807u);
                 u1 = canon_minstd(st);
             } else {
-                const uint64_t k = W.call_rng[c] * 2ull * (uint64_t)N + 2ull * s;
+                const uint64_t k = rbase * 2ull * (uint64_t)N + 2ull * s;
                 u0 = canon_mt(W.mt_stream[k]);
                 u1 = canon_mt(W.mt_stream[k + 1]);
             }
@@ -609,7 +650,7 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
             const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
             const float r = sqrtf(1 - z * z);
             double sa, ca;
-            rt_glibc_sincos_simd((double)ang, &sa, &ca);
+            rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
             rv3 v = v3_normalize(v3((float)((double)r * ca), (float)((double)r * sa), z));
             if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
             o = v3_add(hp, v3_scale(v, 0.2f));

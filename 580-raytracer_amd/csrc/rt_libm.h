@@ -194,7 +194,9 @@ RT_HD double rt_sc_taylor_sin(double xx, double a, double da) {
     return a + t;
 }
 
-RT_HD double rt_sc_do_cos(double x, double dx) {
+// do_cos / do_sin read the 440-entry __sincostab through `tab` (constant memory
+// by default; the AO kernel passes a copy staged in LDS).
+RT_HD double rt_sc_do_cos_t(const double* tab, double x, double dx) {
     if (x < 0) dx = -dx;
     double ax = fabs(x);
     double ux = RT_SC_BIG + ax;
@@ -204,13 +206,13 @@ RT_HD double rt_sc_do_cos(double x, double dx) {
     double s = x + x * xx * (RT_SC_SN3 + xx * RT_SC_SN5);
     double c = xx * (RT_SC_CS2 + xx * (RT_SC_CS4 + xx * RT_SC_CS6));
     int k = (int)(lo << 2);
-    double sn = RT_T(rt_sincostab)[k], ssn = RT_T(rt_sincostab)[k + 1];
-    double cs = RT_T(rt_sincostab)[k + 2], ccs = RT_T(rt_sincostab)[k + 3];
+    double sn = tab[k], ssn = tab[k + 1];
+    double cs = tab[k + 2], ccs = tab[k + 3];
     double cor = (ccs - s * ssn - cs * c) - sn * s;
     return cs + cor;
 }
 
-RT_HD double rt_sc_do_sin(double x, double dx) {
+RT_HD double rt_sc_do_sin_t(const double* tab, double x, double dx) {
     double xold = x;
     if (fabs(x) < RT_SC_TAYLOR_CUT) return rt_sc_taylor_sin(x * x, x, dx);
     if (x <= 0) dx = -dx;
@@ -222,11 +224,14 @@ RT_HD double rt_sc_do_sin(double x, double dx) {
     double s = x + (dx + x * xx * (RT_SC_SN3 + xx * RT_SC_SN5));
     double c = x * dx + xx * (RT_SC_CS2 + xx * (RT_SC_CS4 + xx * RT_SC_CS6));
     int k = (int)(lo << 2);
-    double sn = RT_T(rt_sincostab)[k], ssn = RT_T(rt_sincostab)[k + 1];
-    double cs = RT_T(rt_sincostab)[k + 2], ccs = RT_T(rt_sincostab)[k + 3];
+    double sn = tab[k], ssn = tab[k + 1];
+    double cs = tab[k + 2], ccs = tab[k + 3];
     double cor = (ssn + s * ccs - sn * c) + cs * s;
     return copysign(sn + cor, xold);
 }
+
+RT_HD double rt_sc_do_cos(double x, double dx) { return rt_sc_do_cos_t(RT_T(rt_sincostab), x, dx); }
+RT_HD double rt_sc_do_sin(double x, double dx) { return rt_sc_do_sin_t(RT_T(rt_sincostab), x, dx); }
 
 RT_HD int rt_sc_reduce(double x, double* a, double* da) {
     double t = (x * RT_SC_HPINV + RT_SC_TOINT);
@@ -251,7 +256,7 @@ RT_HD int rt_sc_reduce(double x, double* a, double* da) {
 // ONE do_sin and ONE do_cos keeps a wavefront of random angles on a single path
 // (the divergent form runs up to three). Same operations on the same operands,
 // so the same bits (checked exhaustively against glibc, tests/native/libm_check.cpp).
-RT_HD void rt_glibc_sincos_simd(double x, double* sinx, double* cosx) {
+RT_HD void rt_glibc_sincos_simd_t(const double* tab, double x, double* sinx, double* cosx) {
     const uint32_t k = (uint32_t)(rt_d2u(x) >> 32) & 0x7fffffffu;
     double a = x, da = 0.0;
     int mode;  // 0: small, 1: 0.855..2.426, 2: reduced
@@ -268,8 +273,8 @@ RT_HD void rt_glibc_sincos_simd(double x, double* sinx, double* cosx) {
         n = rt_sc_reduce(x, &a, &da) & 3;
         if (n == 1 || n == 2) { a = -a; da = -da; }
     }
-    const double S = rt_sc_do_sin(a, da);
-    const double C = rt_sc_do_cos(a, da);
+    const double S = rt_sc_do_sin_t(tab, a, da);
+    const double C = rt_sc_do_cos_t(tab, a, da);
     double sv, cv;
     if (mode == 0) { sv = S; cv = C; }
     else if (mode == 1) { sv = copysign(C, x); cv = S; }
@@ -281,6 +286,10 @@ RT_HD void rt_glibc_sincos_simd(double x, double* sinx, double* cosx) {
     if (k >= 0x419921fbu) { sv = cv = (x - x) / (x - x); }  // outside the path's domain
     *sinx = sv;
     *cosx = cv;
+}
+
+RT_HD void rt_glibc_sincos_simd(double x, double* sinx, double* cosx) {
+    rt_glibc_sincos_simd_t(RT_T(rt_sincostab), x, sinx, cosx);
 }
 
 // Valid for |x| < 105414350 (the reference only passes angles in [0, 2*pi)).
