@@ -27,6 +27,7 @@
 // in rt_libm.h; double precision only where the reference uses double.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/rt580.h"
 #include "rt_kernels.h"
@@ -90,31 +91,35 @@ __device__ __forceinline__ bool quot_lt0(float num, float den) {
 // precomputed. WANT_BARY: also return alpha/beta/gamma (closest hit); the
 // any-hit form only needs the accept/reject decision. Both decide exactly as
 // the reference's divisions would.
-template <bool WANT_BARY>
+template <bool WANT_BARY, bool SIGN = true>
 __device__ __forceinline__ bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
     const rv3 N = ld3(P.nrm);
     const float nd = v3_dot(N, d);
     if (rt_lt_eps(fabsf(nd))) return false;  // NearlyEquals(nd, 0)
     const float num = -(v3_dot(N, o) + P.d);
     // t = num / nd <= EPSILON: decided by signs when t <= 0 (|nd| > EPSILON here)
-    if (num == num && (num == 0.0f || signbit(num) != signbit(nd))) return false;
+    if (SIGN && num == num && (num == 0.0f || signbit(num) != signbit(nd))) return false;
     t = num / nd;
     if (rt_lt_eps(t)) return false;           // t <= EPSILON
     const rv3 Pp = v3_add(o, v3_scale(d, t));
     const rv3 v0 = ld3(P.p0), v1 = ld3(P.p1), v2 = ld3(P.p2);
     // CalcTriangleAreaSigned (Raytracer.cpp:937-942): 0.5 * dot(cross(B-A, C-A), N)
     const float aa = 0.5f * v3_dot(v3_cross(v3_sub(v1, Pp), v3_sub(v2, Pp)), N);
-    if (quot_lt0(aa, P.area)) return false;
     const float bb = 0.5f * v3_dot(v3_cross(v3_sub(Pp, v0), v3_sub(v2, v0)), N);
-    if (quot_lt0(bb, P.area)) return false;
     const float gg = 0.5f * v3_dot(v3_cross(v3_sub(v1, v0), v3_sub(Pp, v0)), N);
-    if (quot_lt0(gg, P.area)) return false;
-    if (WANT_BARY) {
-        a = aa / P.area;
-        b = bb / P.area;
-        g = gg / P.area;
+    if (SIGN) {
+        if (quot_lt0(aa, P.area) || quot_lt0(bb, P.area) || quot_lt0(gg, P.area)) return false;
+        if (WANT_BARY) {
+            a = aa / P.area;
+            b = bb / P.area;
+            g = gg / P.area;
+        }
+        return true;
     }
-    return true;
+    a = aa / P.area;
+    b = bb / P.area;
+    g = gg / P.area;
+    return !(a < 0 || b < 0 || g < 0);
 }
 
 // IntersectSphere (Raytracer.cpp:419-464)
@@ -173,6 +178,7 @@ __device__ bool closest_hit(const DevScene& S, rt_prim* tile, bool resident, boo
 
 // IntersectScene where only the boolean is read (directional shadows, AO rays):
 // any hit, with a workgroup-wide early exit once every active lane has hit.
+template <bool SIGN = true>
 __device__ bool any_hit(const DevScene& S, rt_prim* tile, bool resident, bool active, rv3 o, rv3 d) {
     bool hit = false;
     for (int base = 0; base < S.n_prims; base += TILE) {
@@ -186,7 +192,7 @@ __device__ bool any_hit(const DevScene& S, rt_prim* tile, bool resident, bool ac
             for (int j = 0; j < n; j++) {
                 const rt_prim& P = tile[j];
                 float t, a, b, g;
-                if (P.kind == RT_PRIM_TRIANGLE ? tri_test<false>(P, o, d, t, a, b, g) : sph_test(P, o, d, t)) {
+                if (P.kind == RT_PRIM_TRIANGLE ? tri_test<false, SIGN>(P, o, d, t, a, b, g) : sph_test(P, o, d, t)) {
                     hit = true;
                     break;
                 }
@@ -594,16 +600,23 @@ __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWor
 // ---------------------------------------------------------------- AO
 // CalculateAmbientOcclusion (Raytracer.cpp:315-330) + RandomInHemisphere (:283-292)
 // + RandomUnitVector (:269-281): one lane per (call, sample).
+// VARIANT bits (A/B switches, results identical): 1 = sincos table in LDS,
+// 2 = scalar per-call data (readfirstlane), 4 = sign-decided triangle rejects.
+template <int VARIANT>
 __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork W) {
     __shared__ rt_prim tile[TILE];
-    __shared__ double sct[440];  // glibc __sincostab, staged once per workgroup
-    for (int i = threadIdx.x; i < 440; i += TB) sct[i] = rt_dev::rt_sincostab[i];
-    __syncthreads();
+    __shared__ double sct_lds[440];  // glibc __sincostab, staged once per workgroup
+    const double* sct = rt_dev::rt_sincostab;
+    if (VARIANT & 1) {
+        for (int i = threadIdx.x; i < 440; i += TB) sct_lds[i] = rt_dev::rt_sincostab[i];
+        __syncthreads();
+        sct = sct_lds;
+    }
     const uint32_t N = (uint32_t)F.ao_samples;
     const uint64_t items = W.totals[0] * (uint64_t)N;
     const bool pow2 = (N & (N - 1)) == 0;
     const int log2n = 31 - __clz((int)N);
-    const bool wave_per_call = (N & 63u) == 0;
+    const bool wave_per_call = (VARIANT & 2) && (N & 63u) == 0;
     const bool resident = stage_resident(S, tile);
     for (uint64_t b0 = (uint64_t)blockIdx.x * TB; b0 < items; b0 += (uint64_t)gridDim.x * TB) {
         const uint64_t item = b0 + threadIdx.x;
@@ -656,8 +669,8 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
             o = v3_add(hp, v3_scale(v, 0.2f));
             d = v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
         }
-        const bool hit = any_hit(S, tile, resident, active, o, d);
-        if (wave_per_call) {
+        const bool hit = any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
+        if ((N & 63u) == 0) {
             const uint64_t m = __ballot(active && hit);
             if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.occ[c], (uint32_t)__popcll(m));
         } else if (active && hit) {
@@ -805,9 +818,23 @@ hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, c
     return hipGetLastError();
 }
 
+static int ao_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_VARIANT");
+        v = e ? (atoi(e) & 7) : 0;
+    }
+    return v;
+}
+
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     if (!F.ao_enabled || S.n_ambient == 0 || F.n_rows == 0) return hipSuccess;
-    hipLaunchKernelGGL(ao_kernel, dim3(8192), dim3(TB), 0, s, S, F, W);
+    switch (ao_variant()) {
+#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
+        RT_AO_CASE(0) RT_AO_CASE(1) RT_AO_CASE(2) RT_AO_CASE(3)
+        RT_AO_CASE(4) RT_AO_CASE(5) RT_AO_CASE(6) RT_AO_CASE(7)
+#undef RT_AO_CASE
+    }
     return hipGetLastError();
 }
 
