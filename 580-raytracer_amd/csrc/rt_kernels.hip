@@ -91,7 +91,7 @@ __device__ __forceinline__ bool quot_lt0(float num, float den) {
 // precomputed. WANT_BARY: also return alpha/beta/gamma (closest hit); the
 // any-hit form only needs the accept/reject decision. Both decide exactly as
 // the reference's divisions would.
-template <bool WANT_BARY, bool SIGN = true>
+template <bool WANT_BARY, bool SIGN = false>
 __device__ __forceinline__ bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
     const rv3 N = ld3(P.nrm);
     const float nd = v3_dot(N, d);
@@ -178,7 +178,7 @@ __device__ bool closest_hit(const DevScene& S, rt_prim* tile, bool resident, boo
 
 // IntersectScene where only the boolean is read (directional shadows, AO rays):
 // any hit, with a workgroup-wide early exit once every active lane has hit.
-template <bool SIGN = true>
+template <bool SIGN = false>
 __device__ bool any_hit(const DevScene& S, rt_prim* tile, bool resident, bool active, rv3 o, rv3 d) {
     bool hit = false;
     for (int base = 0; base < S.n_prims; base += TILE) {
@@ -201,6 +201,46 @@ __device__ bool any_hit(const DevScene& S, rt_prim* tile, bool resident, bool ac
         if (base + TILE < S.n_prims && __syncthreads_and(!active || hit)) break;
     }
     return hit;
+}
+
+// Scene records read through the constant address space: with a wave-uniform
+// index the compiler emits s_load (primitive fields land in SGPRs and every
+// per-primitive branch is uniform; the scalar cache holds small scenes).
+typedef const uint32_t __attribute__((address_space(4)))* cu32_ptr;
+
+__device__ __forceinline__ rt_prim load_prim_scalar(const rt_prim* prims, int j) {
+    const cu32_ptr src = (cu32_ptr)(prims + j);
+    rt_prim P;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&P);
+#pragma unroll
+    for (int k = 0; k < 16; k++) dst[k] = src[k];
+    return P;
+}
+
+__device__ bool closest_hit_scalar(const DevScene& S, rv3 o, rv3 d, Hit& h) {
+    bool found = false;
+    for (int j = 0; j < S.n_prims; j++) {
+        const rt_prim P = load_prim_scalar(S.prims, j);
+        float t, a = 0, b = 0, g = 0;
+        const bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test<true, false>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+        if (hit && (!found || t < h.t)) {
+            found = true;
+            h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
+        }
+    }
+    return found;
+}
+
+template <bool SIGN = false>
+__device__ bool any_hit_scalar(const DevScene& S, bool active, rv3 o, rv3 d) {
+    bool hit = !active;
+    for (int j = 0; j < S.n_prims; j++) {
+        const rt_prim P = load_prim_scalar(S.prims, j);
+        float t, a, b, g;
+        if (!hit) hit = P.kind == RT_PRIM_TRIANGLE ? tri_test<false, SIGN>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+        if (__builtin_amdgcn_read_exec() == __ballot(hit)) break;  // every lane of the wave done
+    }
+    return active && hit;
 }
 
 // Small scenes (<= TILE primitives) are staged once per workgroup and stay resident.
@@ -617,7 +657,7 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
     const bool pow2 = (N & (N - 1)) == 0;
     const int log2n = 31 - __clz((int)N);
     const bool wave_per_call = (VARIANT & 2) && (N & 63u) == 0;
-    const bool resident = stage_resident(S, tile);
+    const bool resident = (VARIANT & 8) ? true : stage_resident(S, tile);
     for (uint64_t b0 = (uint64_t)blockIdx.x * TB; b0 < items; b0 += (uint64_t)gridDim.x * TB) {
         const uint64_t item = b0 + threadIdx.x;
         const bool active = item < items;
@@ -669,7 +709,8 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
             o = v3_add(hp, v3_scale(v, 0.2f));
             d = v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
         }
-        const bool hit = any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
+        const bool hit = (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
+                                       : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
         if ((N & 63u) == 0) {
             const uint64_t m = __ballot(active && hit);
             if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.occ[c], (uint32_t)__popcll(m));
@@ -822,7 +863,7 @@ static int ao_variant() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_AO_VARIANT");
-        v = e ? (atoi(e) & 7) : 0;
+        v = e ? (atoi(e) & 15) : 1;
     }
     return v;
 }
@@ -833,6 +874,8 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
         RT_AO_CASE(0) RT_AO_CASE(1) RT_AO_CASE(2) RT_AO_CASE(3)
         RT_AO_CASE(4) RT_AO_CASE(5) RT_AO_CASE(6) RT_AO_CASE(7)
+        RT_AO_CASE(8) RT_AO_CASE(9) RT_AO_CASE(10) RT_AO_CASE(11)
+        RT_AO_CASE(12) RT_AO_CASE(13) RT_AO_CASE(14) RT_AO_CASE(15)
 #undef RT_AO_CASE
     }
     return hipGetLastError();
