@@ -643,7 +643,7 @@ __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWor
 // VARIANT bits (A/B switches, results identical): 1 = sincos table in LDS,
 // 2 = scalar per-call data (readfirstlane), 4 = sign-decided triangle rejects.
 template <int VARIANT>
-__global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork W) {
+__device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, const DevWork& W) {
     __shared__ rt_prim tile[TILE];
     __shared__ double sct_lds[440];  // glibc __sincostab, staged once per workgroup
     const double* sct = rt_dev::rt_sincostab;
@@ -718,6 +718,19 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
             atomicAdd(&W.occ[c], 1u);
         }
     }
+}
+
+template <int VARIANT>
+__global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork W) {
+    ao_body<VARIANT>(S, F, W);
+}
+
+// Same kernel with the register budget capped for 8 waves per SIMD (SGPR <= 80
+// admits 8 workgroups per CU instead of 6).
+template <int VARIANT>
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(8, 8)))
+ao_kernel_occ8(DevScene S, DevFrame F, DevWork W) {
+    ao_body<VARIANT>(S, F, W);
 }
 
 // ---------------------------------------------------------------- resolve
@@ -863,14 +876,24 @@ static int ao_variant() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_AO_VARIANT");
-        v = e ? (atoi(e) & 15) : 1;
+        v = e ? (atoi(e) & 31) : 9;
     }
     return v;
 }
 
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     if (!F.ao_enabled || S.n_ambient == 0 || F.n_rows == 0) return hipSuccess;
-    switch (ao_variant()) {
+    const int v = ao_variant();
+    if (v & 16) {
+        switch (v & 15) {
+#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
+            RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8)
+#undef RT_AO_CASE
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    switch (v) {
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
         RT_AO_CASE(0) RT_AO_CASE(1) RT_AO_CASE(2) RT_AO_CASE(3)
         RT_AO_CASE(4) RT_AO_CASE(5) RT_AO_CASE(6) RT_AO_CASE(7)
