@@ -703,13 +703,16 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
             const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
             const float r = sqrtf(1 - z * z);
             double sa, ca;
-            rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
-            rv3 v = v3_normalize(v3((float)((double)r * ca), (float)((double)r * sa), z));
+            if (VARIANT & 64) { sa = ang; ca = z; }  // DIAGNOSTIC ablation only (wrong output)
+            else rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
+            rv3 v = v3((float)((double)r * ca), (float)((double)r * sa), z);
+            if (!(VARIANT & 128)) v = v3_normalize(v);
             if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
             o = v3_add(hp, v3_scale(v, 0.2f));
-            d = v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
+            d = (VARIANT & 128) ? v : v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
         }
-        const bool hit = (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
+        const bool hit = (VARIANT & 32) ? (d.x > 2.0f)  // DIAGNOSTIC ablation only
+                       : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
                                        : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
         if ((N & 63u) == 0) {
             const uint64_t m = __ballot(active && hit);
@@ -876,7 +879,7 @@ static int ao_variant() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_AO_VARIANT");
-        v = e ? (atoi(e) & 31) : 9;
+        v = e ? (atoi(e) & 255) : 25;  // measured best: LDS sincos table + scalar scene + 8 waves/SIMD
     }
     return v;
 }
@@ -888,6 +891,15 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         switch (v & 15) {
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
             RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8)
+#undef RT_AO_CASE
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    if (v >= 32) {  // diagnostic ablations (timing only)
+        switch (v) {
+#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
+            RT_AO_CASE(41) RT_AO_CASE(73) RT_AO_CASE(137) RT_AO_CASE(105) RT_AO_CASE(233)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;
         }

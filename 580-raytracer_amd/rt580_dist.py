@@ -59,8 +59,15 @@ def render_frame(backend, dist, torch, height, width, rank, world, gather=True):
     on rank 0 (None elsewhere, or the local tile when gather=False)."""
     n_max = n_max_rows(height, world)
     counts = backend.count(rank, world)                       # int32[n_max], zero padded
-    gathered = [torch.empty_like(counts) for _ in range(world)]
-    dist.all_gather(gathered, counts)
+    # gloo has no device collectives: stage through the host (tests / fallback
+    # rehearsal of the multi-rank logic on one GPU); nccl (= RCCL) stays on device.
+    stage = dist.get_backend() == "gloo" and counts.is_cuda
+    dev = counts.device
+    c_x = counts.cpu() if stage else counts
+    gathered = [torch.empty_like(c_x) for _ in range(world)]
+    dist.all_gather(gathered, c_x)
+    if stage:
+        gathered = [g.to(dev) for g in gathered]
     # row y lives on rank y % G at local index y // G
     full = torch.stack(gathered, dim=1).reshape(-1)[:height].to(torch.int64)
     base = torch.cumsum(full, 0) - full                       # exclusive scan, raster order
@@ -72,9 +79,13 @@ def render_frame(backend, dist, torch, height, width, rank, world, gather=True):
         return fb
     # int16 has no RCCL/gloo dtype: the tiles travel as their bytes
     fb_bytes = fb.view(torch.uint8)
+    if stage:
+        fb_bytes = fb_bytes.cpu()
     if rank == 0:
         tiles = [torch.empty_like(fb_bytes) for _ in range(world)]
         dist.gather(fb_bytes, gather_list=tiles, dst=0)
+        if stage:
+            tiles = [t.to(dev) for t in tiles]
         frame = torch.stack([t.view(torch.int16).view(n_max, width, 3) for t in tiles], dim=1)
         return frame.reshape(n_max * world, width, 3)[:height]
     dist.gather(fb_bytes, dst=0)

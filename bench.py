@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--check", action="store_true", help="verify the frame against the golden sha256")
     args = ap.parse_args()
 
     import torch
@@ -53,12 +55,17 @@ def main():
     import helpers
 
     rank, world = env_int("RANK", 0), env_int("WORLD_SIZE", 1)
-    local_rank = env_int("LOCAL_RANK", 0)
+    # one GPU per rank; on a box with fewer GPUs than ranks (rehearsal of the
+    # multi-rank path with --backend gloo) ranks share devices round-robin
+    local_rank = env_int("LOCAL_RANK", 0) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group(args.backend, rank=rank, world_size=world)
 
     rt580 = helpers.rt580()
     lib = rt580.load()
@@ -85,16 +92,29 @@ def main():
     def step():
         if world == 1:
             rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(fbp)), "rt_gpu_render_device")
-        else:
-            dist_mod.render_frame(backend, dist, torch, HEIGHT, WIDTH, rank, world)
+            return None
+        return dist_mod.render_frame(backend, dist, torch, HEIGHT, WIDTH, rank, world)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
+    frame = None
+    for _ in range(max(args.warmup, 1 if args.check else 0)):
+        frame = step()
     torch.cuda.synchronize()
+    check_ok = None
+    if args.check and rank == 0:
+        # the frame of the (last warm-up) step vs the reference's config-2 hash
+        if world == 1:
+            import numpy as np
+            host = np.zeros(WIDTH * HEIGHT * 3, dtype=np.int16)
+            rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
+            frame_np = host.reshape(HEIGHT, WIDTH, 3)
+        else:
+            frame_np = frame.cpu().numpy()
+        want = next(e for e in helpers.golden_entries(False) if e["name"] == "config2_1080p_d4_ao64")["sha256"]
+        check_ok = helpers.sha256(rt580.ppm_bytes(frame_np)) == want
     # rays of one frame (this rank's rows), from the count pass of the last frame
     st = rt580.RenderStats()
     rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "rt_gpu_last_stats")
@@ -173,6 +193,8 @@ def main():
                         "is VALU-bound (the %d-primitive scene is re-read from LDS, not HBM)" % len(prims),
             },
         }
+        if check_ok is not None:
+            out["frame_matches_reference"] = check_ok
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(lib, rt580, helpers, params)
         print(json.dumps(out), flush=True)

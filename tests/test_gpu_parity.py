@@ -79,3 +79,41 @@ def test_against_oracle(scene, w, h, depth, ao):
     assert np.array_equal(fb, ref), "%d pixels differ" % int((fb != ref).any(axis=2).sum())
     for k in ("rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"):
         assert st[k] == cnt[k], k
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_multi_rank_split_on_one_gpu(world):
+    """The C-ABI split used across GPUs (rt_gpu_count_rows -> all-gather/scan ->
+    rt_gpu_shade_rows) driven rank by rank on one device; the de-interleaved
+    frame must equal the single-call render."""
+    import torch
+    rt580 = helpers.rt580()
+    d = helpers.rt580_dist()
+    scene, w, h, depth, ao = "simpleSphereScene.json", 97, 61, 4, 64
+    full, _ = render_gpu(scene, w, h, depth, ao, True)
+    rt = rt580.Raytracer(w, h, helpers.ASSETS_ROOT)
+    assert rt.LoadSceneJSON(scene) == 0
+    rt.set_depth(depth)
+    rt.set_ao(ao, True)
+    assert rt.InitializeRenderer() == 0
+    params = rt.render_params()
+    lib = rt580.load()
+    s = rt.scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    dev = torch.device("cuda", 0)
+    rt580.check(lib.rt_gpu_set_stream(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "stream")
+    backend = d.GpuRows(rt580, params, torch, dev)
+    n_max = d.n_max_rows(h, world)
+    counts = [backend.count(r, world).clone() for r in range(world)]
+    full_counts = torch.stack(counts, dim=1).reshape(-1)[:h].to(torch.int64)
+    base = torch.cumsum(full_counts, 0) - full_counts
+    tiles = []
+    for r in range(world):
+        backend.count(r, world)                     # phase 1 again (phase 2 reuses its per-pixel data)
+        lb = torch.zeros(n_max, dtype=torch.int64, device=dev)
+        mine = base[r::world]
+        lb[:mine.numel()] = mine
+        tiles.append(backend.shade(r, world, lb).view(n_max, w, 3).clone())
+    frame = torch.stack(tiles, dim=1).reshape(n_max * world, w, 3)[:h].cpu().numpy()
+    rt580.check(lib.rt_gpu_set_stream(None), "stream")
+    assert np.array_equal(frame, full)
