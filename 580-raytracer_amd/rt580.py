@@ -86,6 +86,21 @@ SIGNATURES = [
 _lib = None
 
 
+def _preload_torch_hip_runtime():
+    """PyTorch-ROCm wheels bundle their own libamdhip64.so. A process must hold
+    ONE HIP runtime (device pointers, streams and events are runtime objects),
+    so when torch is installed its copy is loaded first, by path: lib580rt.so's
+    libamdhip64.so.7 then binds to it (same SONAME) and a later `import torch`
+    reuses the same file. Without torch, /opt/rocm's runtime is used."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    hip = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+
+
 def load(path=LIB_PATH):
     """Load lib580rt.so (built by `make -C 580-raytracer_amd`); raise if absent."""
     global _lib
@@ -93,6 +108,7 @@ def load(path=LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise RuntimeError("lib580rt.so not built (%s); run __graft_entry__.build()" % path)
+    _preload_torch_hip_runtime()
     lib = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
         f = getattr(lib, name)

@@ -116,4 +116,8 @@ def test_multi_rank_split_on_one_gpu(world):
         tiles.append(backend.shade(r, world, lb).view(n_max, w, 3).clone())
     frame = torch.stack(tiles, dim=1).reshape(n_max * world, w, 3)[:h].cpu().numpy()
     rt580.check(lib.rt_gpu_set_stream(None), "stream")
+    for r in range(world):
+        rows = list(range(r, h, world))
+        bad = [y for y in rows if not np.array_equal(frame[y], full[y])]
+        assert not bad, "rank %d/%d: rows %s differ" % (r, world, bad[:10])
     assert np.array_equal(frame, full)
