@@ -306,9 +306,11 @@ int rt_gpu_init(int device) {
 int rt_gpu_set_stream(void* s) {
     if (!g.inited) return fail("rt_gpu_init not called");
     HIP_TRY(hipStreamSynchronize(g.stream));
-    g.stream = s ? (hipStream_t)s : g.own_stream;
+    g.stream = (hipStream_t)s;  // NULL: the HIP null stream (e.g. PyTorch's default stream)
     return RT_SUCCESS;
 }
+
+void* rt_gpu_own_stream(void) { return g.inited ? (void*)g.own_stream : nullptr; }
 
 int rt_gpu_upload_scene(const rt_scene_soa* s) {
     if (!g.inited && rt_gpu_init(-1) != RT_SUCCESS) return RT_FAILURE;

@@ -147,8 +147,11 @@ typedef struct rt_render_stats {
 int rt_gpu_init(int device);
 /* Upload (replace) the flattened scene; buffers stay resident in HBM. */
 int rt_gpu_upload_scene(const rt_scene_soa* scene);
-/* Use this HIP stream (hipStream_t) for all work; NULL: the shim's own stream. */
+/* Queue all further work on this HIP stream (hipStream_t); NULL is the HIP null
+ * stream (PyTorch's default stream). Initially: the shim's own non-blocking
+ * stream, whose handle rt_gpu_own_stream() returns. */
 int rt_gpu_set_stream(void* hip_stream);
+void* rt_gpu_own_stream(void);
 /* Render the rows selected by params into fb_out (host, Pixel layout: int16
  * r,g,b interleaved; the selected rows packed in order, each `width` pixels).
  * Single-rank: the RNG offsets are scanned on the device. Blocking. */

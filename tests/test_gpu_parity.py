@@ -115,7 +115,7 @@ def test_multi_rank_split_on_one_gpu(world):
         lb[:mine.numel()] = mine
         tiles.append(backend.shade(r, world, lb).view(n_max, w, 3).clone())
     frame = torch.stack(tiles, dim=1).reshape(n_max * world, w, 3)[:h].cpu().numpy()
-    rt580.check(lib.rt_gpu_set_stream(None), "stream")
+    rt580.check(lib.rt_gpu_set_stream(lib.rt_gpu_own_stream()), "stream")
     for r in range(world):
         rows = list(range(r, h, world))
         bad = [y for y in rows if not np.array_equal(frame[y], full[y])]
