@@ -206,7 +206,7 @@ def main():
 def measured_traffic():
     """HBM bytes per render_kernel launch from the committed rocprofv3 --pmc
     summary (profiles/), corrected per MI355X_MICROARCH.md §HBM; None if absent."""
-    path = os.path.join(REPO, "profiles", "pmc_render_kernel.json")
+    path = os.path.join(REPO, "profiles", "pmc_ao_kernel.json")
     if os.path.exists(path):
         try:
             return json.load(open(path)).get("hbm_bytes_per_launch")
