@@ -9,7 +9,12 @@ N > 1 the all-gather of per-row AO counts and the RCCL gather of the row tiles
 to rank 0). The scene is resident in HBM; the framebuffer stays in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+                    [--workload config2|cornell10k|field100k_1080p|field100k|field1m]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+--workload selects another BASELINE configuration (synthetic scenes from
+tools/gen_scenes.py, generated on first use under tests/_scenes); config2 is
+the headline. Synthetic workloads default to 2 steps after 1 warm-up.
 
 Rank 0 prints ONE JSON line (metric, value = whole-job Mrays/s, ms_per_step,
 roofline of the shading kernel, cpu_baseline = the reference itself timed on
@@ -26,11 +31,24 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-SCENE, WIDTH, HEIGHT, DEPTH, AO = "simpleSphereScene.json", 1920, 1080, 4, 64
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# CPU baseline sample: the same scene/depth/AO at 1/16 of the pixels (480x270),
-# rendered by the reference binary (oracle/_ref) on one core.
-CPU_SAMPLE = (480, 270)
+
+# name -> (scene, synthetic?, width, height, depth, AO samples, CPU-baseline sample (w, h, depth, ao), label)
+# The CPU sample is a downscaled frame of the same scene rendered by the reference
+# binary on one core (~10-30 s); the reference is O(primitives) per ray, so the
+# triangle scenes get tiny samples (and, for 1M triangles, fewer AO samples).
+WORKLOADS = {
+    "config2": ("simpleSphereScene.json", False, 1920, 1080, 4, 64, (480, 270, 4, 64),
+                "BASELINE config 2: simpleSphereScene.json 1920x1080 depth=4 AO=64"),
+    "cornell10k": ("cornell10k.json", True, 1920, 1080, 4, 64, (6, 4, 4, 64),
+                   "BASELINE config 3: 10k-triangle Cornell box 1920x1080 depth=4 AO=64"),
+    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64, (4, 3, 4, 64),
+                        "north_star target: 100k-triangle field 1920x1080 depth=4 AO=64"),
+    "field100k": ("field100k.json", True, 3840, 2160, 6, 256, (4, 3, 6, 64),
+                  "BASELINE config 4: 100k-triangle field 3840x2160 depth=6 AO=256"),
+    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, (2, 1, 8, 4),
+                "BASELINE config 5: 1M-triangle field 7680x4320 depth=8 AO=256"),
+}
 
 
 def env_int(k, d):
@@ -43,12 +61,19 @@ def env_int(k, d):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="default 20 (config2), 2 (synthetic)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 3 (config2), 1 (synthetic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
-    ap.add_argument("--check", action="store_true", help="verify the frame against the golden sha256")
+    ap.add_argument("--check", action="store_true", help="verify the frame against the golden sha256 (config2)")
+    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     args = ap.parse_args()
+    global SCENE, WIDTH, HEIGHT, DEPTH, AO, CPU_SAMPLE, LABEL, SYNTH
+    SCENE, SYNTH, WIDTH, HEIGHT, DEPTH, AO, CPU_SAMPLE, LABEL = WORKLOADS[args.workload]
+    if args.steps is None:
+        args.steps = 2 if SYNTH else 20
+    if args.warmup is None:
+        args.warmup = 1 if SYNTH else 3
 
     import torch
     import torch.distributed as dist
@@ -73,7 +98,8 @@ def main():
     stream = torch.cuda.current_stream(device)
     rt580.check(lib.rt_gpu_set_stream(ctypes.c_void_p(stream.cuda_stream)), "rt_gpu_set_stream")
 
-    rt = rt580.Raytracer(WIDTH, HEIGHT, helpers.ASSETS_ROOT)
+    root = helpers.synthetic_root(SCENE[:-5]) if SYNTH else helpers.ASSETS_ROOT
+    rt = rt580.Raytracer(WIDTH, HEIGHT, root)
     assert rt.LoadSceneJSON(SCENE) == 0, "LoadSceneJSON failed"
     rt.set_depth(DEPTH)
     rt.set_ao(AO, True)
@@ -100,8 +126,11 @@ def main():
             dist.barrier()
 
     frame = None
-    for _ in range(max(args.warmup, 1 if args.check else 0)):
+    for i in range(max(args.warmup, 1 if args.check else 0)):
         frame = step()
+        if SYNTH:
+            torch.cuda.synchronize()
+            log("warmup step %d done" % i)
     torch.cuda.synchronize()
     check_ok = None
     if args.check and rank == 0:
@@ -124,8 +153,12 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         step()
+        if SYNTH:  # long frames: keep a progress line per step (sync costs microseconds)
+            torch.cuda.synchronize()
+            if rank == 0:
+                log("step %d done" % i)
     barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -149,11 +182,17 @@ def main():
     if rank == 0:
         value = rays_frame * args.steps / dt / 1e6
         bytes_per_ray = 56 * n_tri + 16 * n_sph  # SoA primitive records, no reuse
-        ao_ms = per_frame[2]
         # dominant kernel: ao_kernel (one launch = this rank's AO rays of a frame)
-        achieved = int(local["rays_ao"]) * bytes_per_ray / (ao_ms * 1e-3) / 1e9 if ao_ms > 0 else 0.0
+        # or, when it takes longer, trace_kernel (camera, reflection/refraction and
+        # shadow rays of all levels; per-level launches summed)
+        if per_frame[0] > per_frame[2]:
+            kname, kms = "trace_kernel", per_frame[0]
+            krays = int(local["rays_primary"]) + int(local["rays_secondary"]) + int(local["rays_shadow"])
+        else:
+            kname, kms, krays = "ao_kernel", per_frame[2], int(local["rays_ao"])
+        achieved = krays * bytes_per_ray / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
         out = {
-            "metric": "Mrays/sec (+ ms/frame) at 1920x1080, depth=4, 64 AO samples",
+            "metric": "Mrays/sec (+ ms/frame) at %dx%d, depth=%d, %d AO samples" % (WIDTH, HEIGHT, DEPTH, AO),
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -164,9 +203,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "reference scene file Assets/simpleSphereScene.json (no dataset needed)",
+            "data": ("synthetic scene (tools/gen_scenes.py, seed 580, %d triangles)" % n_tri) if SYNTH else
+                    "reference scene file Assets/%s (no dataset needed)" % SCENE,
             "config": {
-                "workload": "BASELINE config 2: simpleSphereScene.json 1920x1080 depth=4 AO=64",
+                "workload": LABEL,
                 "scene": SCENE, "width": WIDTH, "height": HEIGHT, "depth": DEPTH, "ao_samples": AO,
                 "rng": "minstd_rand0 (libstdc++ default_random_engine)",
                 "rays_per_frame": rays_frame,
@@ -179,34 +219,41 @@ def main():
                 "resolve": round(per_frame[3], 4),
             },
             "roofline": {
-                "kernel": "ao_kernel",
+                "kernel": kname,
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": measured_traffic(),
+                "traffic": measured_traffic(args.workload, kname),
                 "bytes_per_ray": bytes_per_ray,
-                "rays_per_launch": int(local["rays_ao"]),
-                "note": "algorithmic scene-stream bytes (56*T + 16*S per ray, SURVEY §8d) x AO rays of one "
-                        "ao_kernel launch / its mean duration (HIP events on its stream); the kernel itself "
-                        "is VALU-bound (the %d-primitive scene is re-read from LDS, not HBM)" % len(prims),
+                "rays_per_launch": krays,
+                "note": "algorithmic scene-stream bytes (56*T + 16*S per ray, SURVEY §8d) x rays of one "
+                        "%s launch / its mean duration (HIP events on its stream); the kernel itself "
+                        "is VALU-bound (the %d-primitive scene is re-read from LDS/scalar cache, not HBM)"
+                        % (kname, len(prims)),
             },
         }
         if check_ok is not None:
             out["frame_matches_reference"] = check_ok
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(lib, rt580, helpers, params)
+            out["cpu_baseline"] = cpu_baseline(lib, rt580, helpers, root)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def measured_traffic():
-    """HBM bytes per render_kernel launch from the committed rocprofv3 --pmc
+def log(msg):
+    print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
+
+
+def measured_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
     summary (profiles/), corrected per MI355X_MICROARCH.md §HBM; None if absent."""
-    path = os.path.join(REPO, "profiles", "pmc_ao_kernel.json")
+    name = "pmc_ao_kernel.json" if workload == "config2" and kernel == "ao_kernel" else \
+        "pmc_%s_%s.json" % (workload, kernel)
+    path = os.path.join(REPO, "profiles", name)
     if os.path.exists(path):
         try:
             return json.load(open(path)).get("hbm_bytes_per_launch")
@@ -215,17 +262,17 @@ def measured_traffic():
     return None
 
 
-def cpu_baseline(lib, rt580, helpers, params):
+def cpu_baseline(lib, rt580, helpers, root):
     """The reference binary (oracle/_ref, built from /root/reference's own
     sources) on one core, on a bounded sample of the same workload."""
-    w, h = CPU_SAMPLE
+    w, h, depth, ao = CPU_SAMPLE
     exe = os.path.join(REPO, "oracle", "_ref", "rt_ref_param")
-    root = os.path.join(REPO, "oracle", "_ref", "root")
+    ref_root = root if SYNTH else os.path.join(REPO, "oracle", "_ref", "root")
     # rays of the sample frame: the GPU count pass of the same configuration
-    rt = rt580.Raytracer(w, h, helpers.ASSETS_ROOT)
+    rt = rt580.Raytracer(w, h, root)
     assert rt.LoadSceneJSON(SCENE) == 0
-    rt.set_depth(DEPTH)
-    rt.set_ao(AO, True)
+    rt.set_depth(depth)
+    rt.set_ao(ao, True)
     assert rt.InitializeRenderer() == 0
     p = rt.render_params()
     fb = (ctypes.c_int16 * (w * h * 3))()
@@ -236,8 +283,8 @@ def cpu_baseline(lib, rt580, helpers, params):
     kind = "reference"
     if os.path.exists(exe):
         t0 = time.perf_counter()
-        pr = subprocess.run(["taskset", "-c", "0", exe, root, SCENE, str(w), str(h), str(DEPTH), "/dev/null",
-                             str(AO), "0"], capture_output=True, text=True)
+        pr = subprocess.run(["taskset", "-c", "0", exe, ref_root, SCENE, str(w), str(h), str(depth), "/dev/null",
+                             str(ao), "0"], capture_output=True, text=True)
         wall = time.perf_counter() - t0
         secs = wall
         for line in pr.stderr.splitlines():
@@ -248,7 +295,7 @@ def cpu_baseline(lib, rt580, helpers, params):
     else:
         kind = "port"
         t0 = time.perf_counter()
-        _, cnt = helpers.oracle_render(SCENE, w, h, DEPTH, AO, True, threads=1)
+        _, cnt = helpers.oracle_render(SCENE, w, h, depth, ao, True, threads=1, root=root)
         secs = time.perf_counter() - t0
         rays = cnt["rays_total"]
     cpu = ""
@@ -260,16 +307,16 @@ def cpu_baseline(lib, rt580, helpers, params):
     except OSError:
         pass
     return {
-        "value": round(rays / secs / 1e6, 4),
+        "value": float("%.4g" % (rays / secs / 1e6)),
         "unit": "Mrays/s",
         "cores": 1,
         "kind": kind,
         "seconds": round(secs, 3),
         "rays": rays,
         "cpu": cpu,
-        "sample": "%s %dx%d depth=%d AO=%d (1/16 of config 2's pixels), single thread, "
-                  "oracle/_ref/rt_ref_param = reference Raytracer.cpp with the AO count as a parameter"
-                  % (SCENE, w, h, DEPTH, AO),
+        "sample": "%s %dx%d depth=%d AO=%d (a downscaled frame of the workload, %.4g%% of its pixels), "
+                  "single thread, oracle/_ref/rt_ref_param = reference Raytracer.cpp with the AO count as a "
+                  "parameter" % (SCENE, w, h, depth, ao, 100.0 * w * h / (WIDTH * HEIGHT)),
     }
 
 

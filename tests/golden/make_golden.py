@@ -45,6 +45,18 @@ SMALL += [
     ("sss_tall_d1_aooff", "simpleSphereScene.json", 7, 53, 1, 128, 0, "minstd"),
     ("sss_1x1_d4_ao16", "simpleSphereScene.json", 1, 1, 4, 16, 1, "minstd"),
 ]
+# Synthetic scenes for BASELINE configs 3-5 (tools/gen_scenes.py, seed 580). The
+# reference is O(prims) per ray (~0.33 us per ray-triangle test as written), so
+# these stay tiny; "assets" names the generated set, whose file hashes are pinned.
+SYNTH = [
+    ("cornell10k_d4_ao4", "cornell10k.json", 32, 18, 4, 4, 1, "minstd"),
+    ("cornell10k_d2_ao16_mt", "cornell10k.json", 20, 12, 2, 16, 1, "mt19937"),
+    ("cornell10k_d6_aooff", "cornell10k.json", 24, 16, 6, 128, 0, "minstd"),
+    ("field100k_d4_ao4", "field100k.json", 16, 9, 4, 4, 1, "minstd"),
+    ("field1m_d2_ao2", "field1m.json", 8, 5, 2, 2, 1, "minstd"),
+]
+SYNTH_ROOT = os.path.join(REF, "synth")
+
 BIG = [
     # BASELINE config 1 and 2, the reference's committed output.ppm configuration,
     # and the reference main() as shipped (500x500, Render(): depth 4, AO 128)
@@ -62,11 +74,24 @@ def binary(ao_n, ao_on, engine):
     return os.path.join(REF, name)
 
 
-def run(entry, keep_ppm):
+sys.path.insert(0, os.path.join(REPO, "tools"))
+from gen_scenes import scene_files  # noqa: E402
+
+
+def synth_assets(scene):
+    """Generate the synthetic scene and return {file: sha256} of everything it reads."""
+    stem = scene[:-5]
+    subprocess.run([sys.executable, os.path.join(REPO, "tools", "gen_scenes.py"), SYNTH_ROOT, stem], check=True)
+    assets = os.path.join(SYNTH_ROOT, "Assets")
+    files = sorted(scene_files(stem))
+    return {f: hashlib.sha256(open(os.path.join(assets, f), "rb").read()).hexdigest() for f in files}
+
+
+def run(entry, keep_ppm, root=ROOT, extra=None):
     name, scene, w, h, depth, ao_n, ao_on, engine = entry
     exe = binary(ao_n, ao_on, engine)
     out = os.path.join("/tmp", "golden_%s.ppm" % name)
-    cmd = [exe, ROOT, scene, str(w), str(h), str(depth), out, str(ao_n), str(int(not ao_on))]
+    cmd = [exe, root, scene, str(w), str(h), str(depth), out, str(ao_n), str(int(not ao_on))]
     t0 = time.time()
     p = subprocess.run(cmd, capture_output=True, text=True)
     if p.returncode != 0:
@@ -80,6 +105,7 @@ def run(entry, keep_ppm):
         "reference_binary": os.path.basename(exe),
         "reference_seconds": round(time.time() - t0, 3),
     }
+    rec.update(extra or {})
     if keep_ppm:
         dst = os.path.join(HERE, "ppm", name + ".ppm")
         shutil.copyfile(out, dst)
@@ -95,11 +121,16 @@ def main():
     man_path = os.path.join(HERE, "manifest.json")
     man = json.load(open(man_path)) if os.path.exists(man_path) else {"entries": []}
     have = {e["name"]: e for e in man["entries"]}
-    todo = [(e, True) for e in SMALL] + ([(e, False) for e in BIG] if big else [])
-    for e, keep in todo:
+    todo = [(e, True, False) for e in SMALL] + [(e, True, True) for e in SYNTH] + \
+        ([(e, False, False) for e in BIG] if big else [])
+    for e, keep, synth in todo:
         if e[0] in have and (not keep or os.path.exists(os.path.join(HERE, have[e[0]].get("ppm", "-")))):
             continue
-        have[e[0]] = run(e, keep)
+        if synth:
+            files = synth_assets(e[1])
+            have[e[0]] = run(e, keep, SYNTH_ROOT, {"assets": "synthetic", "asset_sha256": files})
+        else:
+            have[e[0]] = run(e, keep)
         man["entries"] = sorted(have.values(), key=lambda r: r["name"])
         json.dump(man, open(man_path, "w"), indent=1)
     # The reference's own committed render (mt19937, depth 0, AO 128, 500x500;

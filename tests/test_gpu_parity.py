@@ -13,9 +13,9 @@ import helpers
 pytestmark = pytest.mark.gpu
 
 
-def render_gpu(scene, w, h, depth, ao_samples, ao_enabled, rng=0, rows=None):
+def render_gpu(scene, w, h, depth, ao_samples, ao_enabled, rng=0, rows=None, root=helpers.ASSETS_ROOT):
     rt580 = helpers.rt580()
-    rt = rt580.Raytracer(w, h, helpers.ASSETS_ROOT)
+    rt = rt580.Raytracer(w, h, root)
     assert rt.LoadSceneJSON(scene) == 0
     rt.set_depth(depth)
     rt.set_ao(ao_samples, ao_enabled)
@@ -33,7 +33,7 @@ def render_gpu(scene, w, h, depth, ao_samples, ao_enabled, rng=0, rows=None):
 def test_golden_small(entry):
     rng = 1 if entry["rng"] == "mt19937" else 0
     fb, _ = render_gpu(entry["scene"], entry["width"], entry["height"], entry["depth"],
-                       entry["ao_samples"], entry["ao_enabled"], rng)
+                       entry["ao_samples"], entry["ao_enabled"], rng, root=helpers.entry_root(entry))
     got = helpers.rt580().ppm_bytes(fb)
     want = helpers.golden_ppm(entry)
     assert got == want, helpers.diff_summary(got, want)
@@ -72,10 +72,14 @@ def test_row_subset_matches_full_frame(rows):
     ("simpleSphereScene.json", 160, 120, 6, 32),
     ("scene.json", 96, 72, 3, 8),
     ("simpleSphereSceneAO.json", 128, 96, 8, 16),
+    ("cornell10k.json", 96, 54, 4, 8),
+    ("cornell10k.json", 40, 30, 8, 2),
+    ("field100k.json", 32, 18, 4, 4),
 ])
 def test_against_oracle(scene, w, h, depth, ao):
-    fb, st = render_gpu(scene, w, h, depth, ao, True)
-    ref, cnt = helpers.oracle_render(scene, w, h, depth, ao, True)
+    root = helpers.synthetic_root(scene[:-5]) if scene.startswith(("cornell", "field")) else helpers.ASSETS_ROOT
+    fb, st = render_gpu(scene, w, h, depth, ao, True, root=root)
+    ref, cnt = helpers.oracle_render(scene, w, h, depth, ao, True, root=root)
     assert np.array_equal(fb, ref), "%d pixels differ" % int((fb != ref).any(axis=2).sum())
     for k in ("rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"):
         assert st[k] == cnt[k], k

@@ -15,7 +15,7 @@ import helpers
 def test_oracle_matches_reference_golden(entry):
     rng = 1 if entry["rng"] == "mt19937" else 0
     fb, _ = helpers.oracle_render(entry["scene"], entry["width"], entry["height"], entry["depth"],
-                                  entry["ao_samples"], entry["ao_enabled"], rng)
+                                  entry["ao_samples"], entry["ao_enabled"], rng, root=helpers.entry_root(entry))
     got = helpers.rt580().ppm_bytes(fb)
     assert got == helpers.golden_ppm(entry), helpers.diff_summary(got, helpers.golden_ppm(entry))
 
