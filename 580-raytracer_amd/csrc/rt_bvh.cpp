@@ -1,0 +1,366 @@
+// rt_bvh.cpp — builders for the exact-semantics triangle structures (see
+// rt_bvh.h for the error analysis that makes culling exact). Host C++, run
+// once per scene upload.
+#include "rt_bvh.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+namespace rt580 {
+namespace {
+
+constexpr int kBins = 16;
+constexpr int kLeafMax = 4;   // triangles per spatial leaf
+constexpr int kFarLeaf = 8;   // planes per far-tree leaf
+constexpr int kSahDepth = 40; // below this depth: median splits (bounded stack)
+constexpr double kU = 5.9604644775390625e-08;  // 2^-24
+
+struct Box {
+    float lo[3] = {INFINITY, INFINITY, INFINITY};
+    float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const Box& b) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    void grow(const float p[3]) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], p[k]);
+            hi[k] = std::max(hi[k], p[k]);
+        }
+    }
+    double area() const {
+        double e[3];
+        for (int k = 0; k < 3; k++) e[k] = hi[k] >= lo[k] ? (double)hi[k] - lo[k] : 0.0;
+        return 2.0 * (e[0] * e[1] + e[1] * e[2] + e[2] * e[0]);
+    }
+};
+
+struct Ref {
+    Box box;
+    float c[3];
+    uint32_t id;
+};
+
+float max_abs3(const float* p) { return std::max(std::fabs(p[0]), std::max(std::fabs(p[1]), std::fabs(p[2]))); }
+
+// ---------------------------------------------------------------- analysis
+struct TriBounds {
+    bool ok;
+    double dhi, dlo, delta;
+};
+
+double dist3(const float* a, const float* b) {
+    const double x = (double)a[0] - b[0], y = (double)a[1] - b[1], z = (double)a[2] - b[2];
+    return std::sqrt(x * x + y * y + z * z);
+}
+
+double angle_at(const float* p, const float* q, const float* r) {  // angle at p of triangle (p, q, r)
+    double a[3], b[3];
+    for (int k = 0; k < 3; k++) { a[k] = (double)q[k] - p[k]; b[k] = (double)r[k] - p[k]; }
+    const double la = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    const double lb = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
+    if (!(la > 0) || !(lb > 0)) return 0.0;
+    double c = (a[0] * b[0] + a[1] * b[1] + a[2] * b[2]) / (la * lb);
+    c = std::min(1.0, std::max(-1.0, c));
+    return std::acos(c);
+}
+
+TriBounds analyse(const rt_prim& p, double S, double inflate) {
+    TriBounds r{false, 0, 0, 0};
+    const double e01 = dist3(p.p0, p.p1), e12 = dist3(p.p1, p.p2), e20 = dist3(p.p2, p.p0);
+    const double emin = std::min(e01, std::min(e12, e20)), emax = std::max(e01, std::max(e12, e20));
+    const double a0 = angle_at(p.p0, p.p1, p.p2), a1 = angle_at(p.p1, p.p2, p.p0), a2 = angle_at(p.p2, p.p0, p.p1);
+    const double amin = std::min(a0, std::min(a1, a2));
+    if (!(emin > 0) || !(amin > 1e-4) || !std::isfinite(emax)) return r;
+    const double s = std::sin(0.5 * amin);
+    const double kappa = 16.0 + 4.0 / std::sin(amin);
+    const double ep = emax + std::ldexp(S, -10);  // + off-plane height and rounding slack
+    const double a = kappa * kU, b = emin * s;
+    const double bb = b - 2 * a * ep;
+    const double disc = bb * bb - 4 * a * a * ep * ep;
+    if (!(bb > 0) || !(disc > 0)) return r;
+    r.dhi = (bb + std::sqrt(disc)) / (2 * a);
+    r.dlo = ep * ep / r.dhi;  // product of the roots
+    // near hit points lie within D_lo of the triangle; the rest of the float
+    // error budget is carried by the fat-ray slab test (rt_isect.h)
+    r.delta = std::max(std::max(inflate * emin, std::ldexp(S, -20)), 2.0 * r.dlo);
+    r.ok = std::isfinite(r.dhi) && std::isfinite(r.delta);
+    return r;
+}
+
+// ---------------------------------------------------------------- spatial BVH
+struct Builder {
+    const rt_prim* prims;
+    std::vector<Ref> refs;
+    BvhBuild* out;
+
+    Box bounds(int b, int e) const {
+        Box x;
+        for (int i = b; i < e; i++) x.grow(refs[i].box);
+        return x;
+    }
+
+    int32_t leaf(int b, int e) {
+        const int32_t first = (int32_t)out->prims.size();
+        for (int i = b; i < e; i++) {
+            out->prims.push_back(prims[refs[i].id]);
+            out->ids.push_back(refs[i].id);
+        }
+        out->max_leaf = std::max(out->max_leaf, e - b);
+        return first;
+    }
+
+    int split(int b, int e, int depth) {
+        const int n = e - b;
+        Box cb;
+        for (int i = b; i < e; i++) cb.grow(refs[i].c);
+        int axis = 0;
+        for (int k = 1; k < 3; k++)
+            if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+        auto median = [&](int ax) {
+            const int m = b + n / 2;
+            std::nth_element(refs.begin() + b, refs.begin() + m, refs.begin() + e, [ax](const Ref& x, const Ref& y) {
+                return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.id < y.id);
+            });
+            return m;
+        };
+        if (!(cb.hi[axis] > cb.lo[axis])) return b + n / 2;  // coincident centroids: any split
+        if (depth >= kSahDepth) return median(axis);
+        double best = INFINITY;
+        int best_axis = -1, best_bin = -1;
+        for (int k = 0; k < 3; k++) {
+            const float ext = cb.hi[k] - cb.lo[k];
+            if (!(ext > 0)) continue;
+            Box bb[kBins];
+            int cnt[kBins] = {0};
+            const float scale = kBins / ext;
+            for (int i = b; i < e; i++) {
+                int t = (int)((refs[i].c[k] - cb.lo[k]) * scale);
+                t = std::min(std::max(t, 0), kBins - 1);
+                cnt[t]++;
+                bb[t].grow(refs[i].box);
+            }
+            double right_area[kBins];
+            int right_cnt[kBins];
+            Box acc;
+            int c = 0;
+            for (int t = kBins - 1; t > 0; t--) {
+                acc.grow(bb[t]);
+                c += cnt[t];
+                right_area[t] = acc.area();
+                right_cnt[t] = c;
+            }
+            Box lacc;
+            int lc = 0;
+            for (int t = 0; t < kBins - 1; t++) {
+                lacc.grow(bb[t]);
+                lc += cnt[t];
+                if (lc == 0 || right_cnt[t + 1] == 0) continue;
+                const double cost = lacc.area() * lc + right_area[t + 1] * right_cnt[t + 1];
+                if (cost < best) { best = cost; best_axis = k; best_bin = t; }
+            }
+        }
+        if (best_axis < 0) return median(axis);
+        const int k = best_axis;
+        const float scale = kBins / (cb.hi[k] - cb.lo[k]);
+        const float lo = cb.lo[k];
+        auto it = std::partition(refs.begin() + b, refs.begin() + e, [&](const Ref& r) {
+            int t = (int)((r.c[k] - lo) * scale);
+            t = std::min(std::max(t, 0), kBins - 1);
+            return t <= best_bin;
+        });
+        const int m = (int)(it - refs.begin());
+        return (m > b && m < e) ? m : median(axis);
+    }
+
+    void build_child(int b, int e, int depth, int32_t& c, int32_t& n, Box& box) {
+        box = bounds(b, e);
+        if (e - b <= kLeafMax) {
+            c = leaf(b, e);
+            n = e - b;
+            return;
+        }
+        const int32_t id = (int32_t)out->nodes.size();
+        out->nodes.emplace_back();
+        c = id;
+        n = 0;
+        build_node(id, b, e, depth + 1);
+    }
+
+    void build_node(int32_t id, int b, int e, int depth) {
+        out->depth = std::max(out->depth, depth);
+        const int m = split(b, e, depth);
+        Box lb, rb;
+        int32_t c0, n0, c1, n1;
+        build_child(b, m, depth, c0, n0, lb);
+        build_child(m, e, depth, c1, n1, rb);
+        BvhNode& nd = out->nodes[id];
+        for (int k = 0; k < 3; k++) {
+            nd.lo0[k] = lb.lo[k]; nd.hi0[k] = lb.hi[k];
+            nd.lo1[k] = rb.lo[k]; nd.hi1[k] = rb.hi[k];
+        }
+        nd.c0 = c0; nd.n0 = n0;
+        nd.c1 = c1; nd.n1 = n1;
+    }
+};
+
+// ---------------------------------------------------------------- plane tree
+struct FarBuilder {
+    std::vector<FarTri>& tris;
+    std::vector<FarNode>& nodes;
+    int depth = 0;
+
+    void fill(FarNode& nd, int b, int e) {
+        for (int k = 0; k < 3; k++) { nd.nlo[k] = INFINITY; nd.nhi[k] = -INFINITY; }
+        nd.dlo = INFINITY; nd.dhi = -INFINITY;
+        nd.min_dhi = INFINITY; nd.min_delta = INFINITY;
+        for (int i = b; i < e; i++) {
+            const FarTri& t = tris[i];
+            for (int k = 0; k < 3; k++) {
+                nd.nlo[k] = std::min(nd.nlo[k], t.n[k]);
+                nd.nhi[k] = std::max(nd.nhi[k], t.n[k]);
+            }
+            nd.dlo = std::min(nd.dlo, t.d);
+            nd.dhi = std::max(nd.dhi, t.d);
+            nd.min_dhi = std::min(nd.min_dhi, t.dhi);
+            nd.min_delta = std::min(nd.min_delta, t.delta);
+        }
+    }
+
+    // Node `id` covers [b, e). The far test's interval of N.q + D (q ~ T d away)
+    // has width ~ T_typ * |normal box| + |D range|: median-split the widest of
+    // the four, so leaves are tight in both normal and offset.
+    float t_typ = 1.0f;
+
+    void build(int32_t id, int b, int e, int d) {
+        depth = std::max(depth, d);
+        fill(nodes[id], b, e);
+        if (e - b <= kFarLeaf) {
+            nodes[id].first = b;
+            nodes[id].count = e - b;
+            return;
+        }
+        int axis = 3;
+        float w = nodes[id].dhi - nodes[id].dlo;
+        for (int k = 0; k < 3; k++) {
+            const float x = t_typ * (nodes[id].nhi[k] - nodes[id].nlo[k]);
+            if (x > w) { w = x; axis = k; }
+        }
+        const int m = b + (e - b) / 2;
+        std::nth_element(tris.begin() + b, tris.begin() + m, tris.begin() + e, [axis](const FarTri& x, const FarTri& y) {
+            const float kx = axis < 3 ? x.n[axis] : x.d, ky = axis < 3 ? y.n[axis] : y.d;
+            return kx < ky || (kx == ky && x.id < y.id);
+        });
+        const int32_t c = (int32_t)nodes.size();
+        nodes.emplace_back();
+        nodes.emplace_back();
+        nodes[id].first = c;
+        nodes[id].count = 0;
+        build(c, b, m, d + 1);
+        build(c + 1, m, e, d + 1);
+    }
+};
+
+}  // namespace
+
+bool build_bvh(const rt_prim* prims, int n, BvhBuild& out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    out = BvhBuild();
+    const char* env = std::getenv("RT580_BVH_INFLATE");
+    out.inflate = env ? std::atof(env) : 0.0;
+    if (!(out.inflate >= 0)) out.inflate = 0.0;
+    float S = 0.0f;
+    for (int i = 0; i < n; i++) {
+        const rt_prim& p = prims[i];
+        if (p.kind == RT_PRIM_TRIANGLE) {
+            out.n_tri++;
+            S = std::max(S, std::max(max_abs3(p.p0), std::max(max_abs3(p.p1), max_abs3(p.p2))));
+        } else {
+            S = std::max(S, max_abs3(p.p0) + std::sqrt(std::max(p.d, 0.0f)));
+        }
+    }
+    if (out.n_tri == 0 || !(S > 0.0f) || !std::isfinite(S)) return false;
+    out.scale = S;
+    Builder B;
+    B.prims = prims;
+    B.out = &out;
+    for (int i = 0; i < n; i++) {
+        const rt_prim& p = prims[i];
+        TriBounds tb{false, 0, 0, 0};
+        if (p.kind == RT_PRIM_TRIANGLE) tb = analyse(p, S, out.inflate);
+        if (!tb.ok) {
+            out.brute.push_back((uint32_t)i);
+            continue;
+        }
+        const float delta = (float)tb.delta;
+        Ref r;
+        r.box.grow(p.p0);
+        r.box.grow(p.p1);
+        r.box.grow(p.p2);
+        for (int k = 0; k < 3; k++) {
+            // rounded outward: the float box contains the exact [lo - delta, hi + delta]
+            r.box.lo[k] = std::nextafter(r.box.lo[k] - delta, -INFINITY);
+            r.box.hi[k] = std::nextafter(r.box.hi[k] + delta, INFINITY);
+            r.c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
+        }
+        r.id = (uint32_t)i;
+        B.refs.push_back(r);
+        FarTri ft;
+        std::memcpy(ft.n, p.nrm, sizeof ft.n);
+        ft.d = p.d;
+        ft.dhi = (float)tb.dhi;  // rounded: the device subtracts margins (see rt_kernels.hip)
+        ft.delta = delta;
+        ft.id = (uint32_t)i;
+        ft.pad = 0;
+        out.far_tris.push_back(ft);
+    }
+    const int nt = (int)B.refs.size();
+    if (nt > 0) {
+        out.nodes.reserve(nt);
+        out.prims.reserve(nt);
+        out.ids.reserve(nt);
+        out.nodes.emplace_back();  // root
+        if (nt <= kLeafMax) {
+            Box b = B.bounds(0, nt);
+            BvhNode& r = out.nodes[0];
+            std::memset(&r, 0, sizeof r);
+            for (int k = 0; k < 3; k++) {
+                r.lo0[k] = b.lo[k]; r.hi0[k] = b.hi[k];
+                r.lo1[k] = INFINITY; r.hi1[k] = -INFINITY;
+            }
+            r.c0 = B.leaf(0, nt);
+            r.n0 = nt;
+            r.c1 = 0;
+            r.n1 = -1;
+        } else {
+            B.build_node(0, 0, nt, 0);
+        }
+        out.far_nodes.reserve(nt / 4 + 2);
+        out.far_nodes.emplace_back();
+        FarBuilder F{out.far_tris, out.far_nodes};
+        {   // typical far threshold: median over triangles of min(0.45 delta / 8u, D_hi)
+            std::vector<float> ts;
+            ts.reserve(out.far_tris.size());
+            for (const FarTri& t : out.far_tris) ts.push_back(t.dhi);
+            std::nth_element(ts.begin(), ts.begin() + ts.size() / 2, ts.end());
+            F.t_typ = std::max(ts[ts.size() / 2], 1.0f);
+        }
+        F.build(0, 0, nt, 0);
+        out.far_depth = F.depth;
+    }
+    out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return out.depth + 2 <= RT_BVH_STACK && out.far_depth + 2 <= RT_BVH_STACK;
+}
+
+bool bvh_usable(const BvhBuild& b, const float cam_from[3]) {
+    if (!(b.scale > 0.0f) || b.n_tri == 0) return false;
+    // the bounds hold for any origin; keep the float ranges sane
+    return max_abs3(cam_from) <= 1e6f * b.scale;
+}
+
+}  // namespace rt580

@@ -1,0 +1,99 @@
+// rt_bvh.h — exact-semantics acceleration structures over the scene's
+// triangles, built on the host at upload time.
+//
+// The reference brute-forces every primitive for every ray
+// (IntersectScene, Raytracer.cpp:473-526). Here the structures only decide
+// which primitives are *tested*; every test is the unchanged per-primitive
+// arithmetic on the same rt_prim record, and the combination rule is the
+// reference's: closest hit = lexicographic minimum of (t, primitive index)
+// (what "first hit taken, later ones only if strictly closer" yields for
+// finite t, :491-516); any-hit = the boolean over all primitives.
+//
+// The catch is that the reference's float triangle test also ACCEPTS some
+// hit points far outside the triangle: for rays nearly parallel to the plane,
+// t = num/nd is huge and the signed sub-areas of (Pp, v_i, v_j) are then
+// dominated by rounding (measured: ~2.5e-4 of AO rays on a 100k-triangle
+// scene get such a "far hit" at t ~ 1e6-1e7). A culling structure must keep
+// those. Per triangle j (edges e_min..e_max, smallest angle a_min,
+// s = sin(a_min/2)), with u = 2^-24 and kappa = 16 + 4/sin(a_min):
+//   |computed sub-area - exact| <= kappa*u*|a||b|  (a, b = v - Pp, |.| <= D + e')
+//   exact negative sub-area of a point at in-plane distance D outside
+//     >= e_min * s * D / 2
+// so an accepted hit point is either within D_lo of the triangle ("near") or
+// at distance >= D_hi ("far"), the roots of kappa*u*(D + e')^2 = e_min*s*D.
+//   near hits: found by a spatial BVH whose triangle boxes are inflated by
+//     delta_j >= 2 D_lo and tested with a "fat ray" (box grown by alpha + beta t
+//     covering the float error of the hit point and of the slab arithmetic,
+//     rt_isect.h), conservative at every t;
+//   far hits (t >= T_j = D_hi(j) - |o| - sqrt3*S): found by a second tree over
+//     the triangles' planes (normal boxes + D ranges) that enumerates every
+//     plane the ray crosses beyond T_j, with exact interval padding; those
+//     candidates get the full reference test.
+// Triangles for which the analysis does not give a usable split (slivers,
+// degenerate) and all spheres are tested brute force for every ray.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/rt580.h"
+
+namespace rt580 {
+
+// Spatial BVH node: both children's boxes live in the parent, so one 64-byte
+// fetch culls both. Child link: n == 0 -> internal node `c`; n > 0 -> leaf of
+// the n triangles at slots [c, c + n) of the reordered arrays; n < 0 -> empty.
+struct alignas(16) BvhNode {
+    float lo0[3], hi0[3];
+    float lo1[3], hi1[3];
+    int32_t c0, c1, n0, n1;
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode is one 64-byte line");
+
+// Plane-tree node (own bounds): normals in [nlo, nhi], plane offsets D in
+// [dlo, dhi], and the subtree minima of D_hi and delta (for its T bound).
+// count > 0: leaf of far_tris [first, first + count); else children first, first + 1.
+struct alignas(16) FarNode {
+    float nlo[3], nhi[3];
+    float dlo, dhi;
+    float min_dhi, min_delta;
+    int32_t first, count;
+};
+static_assert(sizeof(FarNode) == 48, "FarNode layout");
+
+// A triangle's plane as the far search reads it (same floats as rt_prim).
+struct alignas(16) FarTri {
+    float n[3];
+    float d;
+    float dhi;      // D_hi(j)
+    float delta;    // delta_j (box inflation)
+    uint32_t id;    // scene primitive index
+    uint32_t pad;
+};
+static_assert(sizeof(FarTri) == 32, "FarTri layout");
+
+#define RT_BVH_STACK 64  // device traversal stack; deeper trees are rejected
+
+struct BvhBuild {
+    std::vector<BvhNode> nodes;     // node 0 is the root
+    std::vector<rt_prim> prims;     // near-set triangles in leaf order (copies of the scene records)
+    std::vector<uint32_t> ids;      // scene index of each slot (tie-break + shading lookups)
+    std::vector<FarNode> far_nodes; // node 0 is the root (empty when no far-set triangle)
+    std::vector<FarTri> far_tris;
+    std::vector<uint32_t> brute;    // spheres + unanalysable triangles, ascending scene index
+    float scale = 0.0f;             // S: largest |coordinate| of the primitives
+    int depth = 0, far_depth = 0;   // deepest levels (stack bounds)
+    int max_leaf = 0;
+    int n_tri = 0;
+    double inflate = 0.0;           // delta_j / e_min(j)
+    double build_ms = 0.0;
+};
+
+// Build over prims[0..n). Returns false if there are no triangles or a tree
+// would exceed the device stack (the caller then keeps brute force).
+bool build_bvh(const rt_prim* prims, int n, BvhBuild& out);
+
+// Render-time guard for the camera (float ranges only; the bounds hold for any origin).
+bool bvh_usable(const BvhBuild& b, const float cam_from[3]);
+
+}  // namespace rt580

@@ -1,0 +1,395 @@
+// rt_isect.h — per-primitive tests and the exact-semantics BVH queries,
+// compiled for the device (rt_kernels.hip) and the host (tests/native BVH
+// checker). Requires -ffp-contract=off like everything else.
+//
+//   tri_test      IntersectTriangle (Raytracer.cpp:348-409), ray-invariant part
+//                 precomputed on the host (rt_scene.cpp)
+//   sph_test      IntersectSphere (Raytracer.cpp:419-464)
+//   bvh_closest   IntersectScene closest hit (Raytracer.cpp:473-526)
+//   bvh_any       IntersectScene where only the boolean is read
+// See rt_bvh.h for why the culling below never changes a result.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/rt580.h"
+#include "rt_bvh.h"
+#include "rt_math.h"
+
+namespace rt580 {
+
+struct Hit {
+    float t, a, b, g;
+    int prim;
+};
+
+RTM_HD rv3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
+
+// (num / den) < 0 exactly as the division would decide it, dividing only when
+// the signs do not already decide it (the quotient can still round to -0).
+RTM_HD bool quot_lt0(float num, float den) {
+    if (num != num || den != den || num == 0.0f) return false;  // NaN, or +-0 / den
+    if (signbit(num) == signbit(den)) return false;             // > 0, +0 or +inf
+    return (num / den) < 0.0f;
+}
+
+// IntersectTriangle. WANT_BARY: also return alpha/beta/gamma (closest hit); the
+// any-hit form only needs the accept/reject decision. Both decide exactly as
+// the reference's divisions would.
+template <bool WANT_BARY, bool SIGN = false>
+RTM_HD bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
+    const rv3 N = ld3(P.nrm);
+    const float nd = v3_dot(N, d);
+    if (rt_lt_eps(fabsf(nd))) return false;  // NearlyEquals(nd, 0)
+    const float num = -(v3_dot(N, o) + P.d);
+    // t = num / nd <= EPSILON: decided by signs when t <= 0 (|nd| > EPSILON here)
+    if (SIGN && num == num && (num == 0.0f || signbit(num) != signbit(nd))) return false;
+    t = num / nd;
+    if (rt_lt_eps(t)) return false;           // t <= EPSILON
+    const rv3 Pp = v3_add(o, v3_scale(d, t));
+    const rv3 v0 = ld3(P.p0), v1 = ld3(P.p1), v2 = ld3(P.p2);
+    // CalcTriangleAreaSigned (Raytracer.cpp:937-942): 0.5 * dot(cross(B-A, C-A), N)
+    const float aa = 0.5f * v3_dot(v3_cross(v3_sub(v1, Pp), v3_sub(v2, Pp)), N);
+    const float bb = 0.5f * v3_dot(v3_cross(v3_sub(Pp, v0), v3_sub(v2, v0)), N);
+    const float gg = 0.5f * v3_dot(v3_cross(v3_sub(v1, v0), v3_sub(Pp, v0)), N);
+    if (SIGN) {
+        if (quot_lt0(aa, P.area) || quot_lt0(bb, P.area) || quot_lt0(gg, P.area)) return false;
+        if (WANT_BARY) {
+            a = aa / P.area;
+            b = bb / P.area;
+            g = gg / P.area;
+        }
+        return true;
+    }
+    a = aa / P.area;
+    b = bb / P.area;
+    g = gg / P.area;
+    return !(a < 0 || b < 0 || g < 0);
+}
+
+RTM_HD bool sph_test(const rt_prim& P, rv3 o, rv3 d, float& t) {
+    rv3 oc = v3_sub(o, ld3(P.p0));
+    float b = 2.0f * v3_dot(d, oc);
+    float c = v3_dot(oc, oc) - P.d;
+    float disc = (b * b) - (4.0f * c);
+    if (rt_lt_eps(disc)) return false;
+    float sq = sqrtf(disc);
+    float t0 = (-b + sq) / 2.0f;
+    float t1 = (-b - sq) / 2.0f;
+    bool g0 = rt_gt_eps(t0), g1 = rt_gt_eps(t1);
+    if (!g0 && !g1) return false;
+    if (!g0) t = t1;
+    else if (!g1) t = t0;
+    else t = fminf(t0, t1);
+    return true;
+}
+
+RTM_HD bool prim_test_closest(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
+    a = b = g = 0.0f;
+    return P.kind == RT_PRIM_TRIANGLE ? tri_test<true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+}
+
+RTM_HD bool prim_test_any(const rt_prim& P, rv3 o, rv3 d) {
+    float t, a, b, g;
+    return P.kind == RT_PRIM_TRIANGLE ? tri_test<false>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+}
+
+// ---------------------------------------------------------------- BVH queries
+struct BvhView {
+    const rt_prim* all;         // scene primitives by index
+    const BvhNode* nodes;
+    const rt_prim* prims;       // spatial leaf order
+    const uint32_t* ids;
+    const FarNode* far_nodes;
+    const FarTri* far_tris;
+    const uint32_t* brute;      // spheres + unanalysable triangles, ascending
+    int n_brute;
+    int has_tree, has_far;
+    float scale;                // S
+};
+
+#define RT_U 5.9604644775390625e-08f  // 2^-24
+
+// Host-only traversal counters (tests/native/bvh_check.cpp -DRT_BVH_COUNT).
+#if defined(RT_BVH_COUNT) && !defined(__HIP_DEVICE_COMPILE__)
+struct BvhCounters {
+    long nodes, leaf_tris, far_nodes, far_cands, far_tests, brute_tests;
+};
+inline thread_local BvhCounters g_bvh_cnt;
+#define RT_CNT(f, n) (g_bvh_cnt.f += (n))
+#else
+#define RT_CNT(f, n) ((void)0)
+#endif
+
+// A zero direction (CalculateRefraction's total internal reflection result,
+// Raytracer.cpp:197-199, is still traced) makes nd = dot(N, d) = 0 for every
+// triangle, which tri_test rejects (NearlyEquals): only spheres can be hit.
+RTM_HD bool dir_zero(rv3 d) { return d.x == 0.0f && d.y == 0.0f && d.z == 0.0f; }
+
+// Closest hit keeps the lexicographic minimum of (t, primitive index).
+RTM_HD bool lex_better(float t, int id, bool found, const Hit& h) {
+    return !found || t < h.t || (t == h.t && id < h.prim);
+}
+
+// "Fat ray" slab test. An accepted near hit at t has its float hit point Pp
+// within D_lo + h of the triangle (rt_bvh.h), and the exact ray point o + d t
+// within u (2t + |o|) of Pp per component. So the exact ray meets the triangle's
+// box (inflated by delta_j >= D_lo) grown by alpha + beta t with
+// alpha = 32u (|o| + S) >= u |o| + h + rounding, beta = 16u >= 2u + slack for
+// the rounding of the slab arithmetic itself. Per axis:
+//   (d + beta) t >= lo - alpha - o   and   (d - beta) t <= hi + alpha - o
+// with the three sign cases of d +- beta; the culling is then conservative for
+// every t, with no bound on the ray length.
+struct SlabRay {
+    rv3 o;
+    float ip[3], im[3];  // 1/(d + beta), -1/(beta - d)
+    int mode[3];         // 1: d > beta, -1: d < -beta, 0: |d| <= beta
+    float alpha;
+};
+
+RTM_HD SlabRay slab_ray(const BvhView& V, rv3 o, rv3 d) {
+    SlabRay r;
+    r.o = o;
+    const float beta = 16.0f * RT_U;
+    const float dv[3] = {d.x, d.y, d.z};
+    for (int k = 0; k < 3; k++) {
+        r.ip[k] = 1.0f / (dv[k] + beta);
+        r.im[k] = -1.0f / (beta - dv[k]);
+        r.mode[k] = dv[k] > beta ? 1 : (dv[k] < -beta ? -1 : 0);
+    }
+    const float oi = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    r.alpha = 32.0f * RT_U * (oi + V.scale);
+    return r;
+}
+
+// NaN-ignoring min/max: a NaN bound comes from 0 * inf, i.e. a constraint that
+// holds for every t.
+RTM_HD bool slab(const float* lo, const float* hi, const SlabRay& r, float& tn) {
+    const float ov[3] = {r.o.x, r.o.y, r.o.z};
+    float tmin = -INFINITY, tmax = INFINITY;
+    for (int k = 0; k < 3; k++) {
+        const float t1 = ((lo[k] - r.alpha) - ov[k]) * r.ip[k];
+        const float t2 = ((hi[k] + r.alpha) - ov[k]) * r.im[k];
+        const float l = r.mode[k] > 0 ? t1 : (r.mode[k] < 0 ? t2 : fmaxf(t1, t2));
+        const float h = r.mode[k] > 0 ? t2 : (r.mode[k] < 0 ? t1 : INFINITY);
+        tmin = fmaxf(tmin, l);
+        tmax = fminf(tmax, h);
+    }
+    tn = tmin;
+    return tmin <= tmax && tmax >= 0.0f;
+}
+
+// Far-search threshold for a ray: a hit with t < T_j = (D_hi(j) - R)(1 - 1e-4),
+// R = |o|_2 + sqrt(3) S, has its hit point within D_lo of the triangle, so the
+// spatial BVH finds it. Monotone in D_hi, so a node's bound from its minimum
+// is <= every member's.
+struct FarRay {
+    float R;
+};
+RTM_HD FarRay far_ray(const BvhView& V, rv3 o) {
+    FarRay f;
+    f.R = sqrtf(o.x * o.x + o.y * o.y + o.z * o.z) * 1.0001f + 1.7321f * V.scale;
+    return f;
+}
+RTM_HD float far_T(const FarRay& r, float dhi) { return (dhi - r.R) * 0.9999f; }
+
+// Could any plane of this node be crossed beyond T_node (and so need the far
+// test)? Interval arithmetic with padding that covers every rounding of both
+// this bound and the reference's num / nd (see rt_bvh.h).
+RTM_HD bool far_node_may(const FarNode& n, const FarRay& r, rv3 o, rv3 d, float& T) {
+    T = far_T(r, n.min_dhi);
+    if (!(T > 0.0f)) return true;
+    const float T2 = T * (1.0f - 0x1p-20f);
+    const rv3 q = v3_add(o, v3_scale(d, T2));
+    float gl = 0, gh = 0, fl = n.dlo, fh = n.dhi;
+    const float dv[3] = {d.x, d.y, d.z}, qv[3] = {q.x, q.y, q.z};
+    for (int k = 0; k < 3; k++) {
+        const float a0 = n.nlo[k] * dv[k], a1 = n.nhi[k] * dv[k];
+        gl += fminf(a0, a1);
+        gh += fmaxf(a0, a1);
+        const float b0 = n.nlo[k] * qv[k], b1 = n.nhi[k] * qv[k];
+        fl += fminf(b0, b1);
+        fh += fmaxf(b0, b1);
+    }
+    const float oi = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    const float P = 32.0f * RT_U * (3.0f * oi + 3.0f * T2 + fmaxf(fabsf(n.dlo), fabsf(n.dhi))) + 1e-30f;
+    const float Pg = 16.0f * RT_U;
+    const bool prune = (fl > P && gl > Pg) || (fh < -P && gh < -Pg);
+    return !prune;
+}
+
+// Is this plane crossed at t >= T_j (computed exactly as tri_test computes t)?
+RTM_HD bool far_candidate(const FarTri& ft, const FarRay& r, rv3 o, rv3 d) {
+    const rv3 N = ld3(ft.n);
+    const float nd = v3_dot(N, d);
+    if (rt_lt_eps(fabsf(nd))) return false;
+    const float num = -(v3_dot(N, o) + ft.d);
+    const float t = num / nd;
+    return t >= far_T(r, ft.dhi);
+}
+
+// with_far = false: brute list + spatial BVH only; the caller then runs the far
+// search itself unless found && h.t < far_T_root (see trace_kernel's phases).
+RTM_HD bool bvh_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool with_far = true) {
+    bool found = false;
+    h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
+    RT_CNT(brute_tests, V.n_brute);
+    for (int k = 0; k < V.n_brute; k++) {
+        const int j = (int)V.brute[k];
+        float t, a, b, g;
+        if (prim_test_closest(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
+            found = true;
+            h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
+        }
+    }
+    if (!V.has_tree || dir_zero(d)) return found;
+    const SlabRay sr = slab_ray(V, o, d);
+    uint32_t stk[RT_BVH_STACK];
+    float tstk[RT_BVH_STACK];
+    int sp = 0;
+    int32_t c = 0, n = 0;  // root (internal)
+    for (;;) {
+        if (n == 0) {
+            RT_CNT(nodes, 1);
+            const BvhNode& nd = V.nodes[c];
+            float t0, t1;
+            bool h0 = nd.n0 >= 0 && slab(nd.lo0, nd.hi0, sr, t0) && (!found || t0 <= h.t);
+            bool h1 = nd.n1 >= 0 && slab(nd.lo1, nd.hi1, sr, t1) && (!found || t1 <= h.t);
+            if (h0 && h1) {
+                const bool first0 = t0 <= t1;
+                const int32_t fc = first0 ? nd.c1 : nd.c0, fn = first0 ? nd.n1 : nd.n0;
+                stk[sp] = ((uint32_t)fn << 27) | (uint32_t)fc;
+                tstk[sp] = first0 ? t1 : t0;
+                sp++;
+                c = first0 ? nd.c0 : nd.c1;
+                n = first0 ? nd.n0 : nd.n1;
+                continue;
+            }
+            if (h0 || h1) {
+                c = h0 ? nd.c0 : nd.c1;
+                n = h0 ? nd.n0 : nd.n1;
+                continue;
+            }
+        } else {
+            RT_CNT(leaf_tris, n);
+            for (int k = c; k < c + n; k++) {
+                float t, a, b, g;
+                if (tri_test<true>(V.prims[k], o, d, t, a, b, g)) {
+                    const int id = (int)V.ids[k];
+                    if (lex_better(t, id, found, h)) {
+                        found = true;
+                        h.t = t; h.a = a; h.b = b; h.g = g; h.prim = id;
+                    }
+                }
+            }
+        }
+        bool popped = false;
+        while (sp > 0) {
+            sp--;
+            if (found && tstk[sp] > h.t) continue;
+            c = (int32_t)(stk[sp] & 0x7ffffffu);
+            n = (int32_t)(stk[sp] >> 27);
+            popped = true;
+            break;
+        }
+        if (!popped) break;
+    }
+    if (!V.has_far || !with_far) return found;
+    const FarRay fr = far_ray(V, o);
+    int32_t fstk[RT_BVH_STACK];
+    int fsp = 0;
+    fstk[fsp++] = 0;
+    while (fsp > 0) {
+        const FarNode& fnode = V.far_nodes[fstk[--fsp]];
+        RT_CNT(far_nodes, 1);
+        float T;
+        if (!far_node_may(fnode, fr, o, d, T)) continue;
+        if (found && h.t < T) continue;  // every far hit below has t >= T
+        if (fnode.count == 0) {
+            fstk[fsp++] = fnode.first + 1;
+            fstk[fsp++] = fnode.first;
+            continue;
+        }
+        RT_CNT(far_cands, fnode.count);
+        for (int k = fnode.first; k < fnode.first + fnode.count; k++) {
+            const FarTri& ft = V.far_tris[k];
+            if (!far_candidate(ft, fr, o, d)) continue;
+            RT_CNT(far_tests, 1);
+            const int j = (int)ft.id;
+            float t, a, b, g;
+            if (tri_test<true>(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
+                found = true;
+                h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
+            }
+        }
+    }
+    return found;
+}
+
+// with_far = false: brute list + spatial BVH only (the caller runs the far
+// search itself, e.g. the sorted wave-cooperative pass of rt_kernels.hip).
+RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true) {
+    RT_CNT(brute_tests, V.n_brute);
+    for (int k = 0; k < V.n_brute; k++)
+        if (prim_test_any(V.all[V.brute[k]], o, d)) return true;
+    if (!V.has_tree || dir_zero(d)) return false;
+    const SlabRay sr = slab_ray(V, o, d);
+    uint32_t stk[RT_BVH_STACK];
+    int sp = 0;
+    int32_t c = 0, n = 0;
+    for (;;) {
+        if (n == 0) {
+            RT_CNT(nodes, 1);
+            const BvhNode& nd = V.nodes[c];
+            float t0, t1;
+            const bool h0 = nd.n0 >= 0 && slab(nd.lo0, nd.hi0, sr, t0);
+            const bool h1 = nd.n1 >= 0 && slab(nd.lo1, nd.hi1, sr, t1);
+            if (h0 && h1) {
+                const bool first0 = t0 <= t1;
+                stk[sp++] = first0 ? (((uint32_t)nd.n1 << 27) | (uint32_t)nd.c1)
+                                   : (((uint32_t)nd.n0 << 27) | (uint32_t)nd.c0);
+                c = first0 ? nd.c0 : nd.c1;
+                n = first0 ? nd.n0 : nd.n1;
+                continue;
+            }
+            if (h0 || h1) {
+                c = h0 ? nd.c0 : nd.c1;
+                n = h0 ? nd.n0 : nd.n1;
+                continue;
+            }
+        } else {
+            RT_CNT(leaf_tris, n);
+            for (int k = c; k < c + n; k++) {
+                float t, a, b, g;
+                if (tri_test<false>(V.prims[k], o, d, t, a, b, g)) return true;
+            }
+        }
+        if (sp == 0) break;
+        sp--;
+        c = (int32_t)(stk[sp] & 0x7ffffffu);
+        n = (int32_t)(stk[sp] >> 27);
+    }
+    if (!V.has_far || !with_far) return false;
+    const FarRay fr = far_ray(V, o);
+    int32_t fstk[RT_BVH_STACK];
+    int fsp = 0;
+    fstk[fsp++] = 0;
+    while (fsp > 0) {
+        const FarNode& fnode = V.far_nodes[fstk[--fsp]];
+        RT_CNT(far_nodes, 1);
+        float T;
+        if (!far_node_may(fnode, fr, o, d, T)) continue;
+        if (fnode.count == 0) {
+            fstk[fsp++] = fnode.first + 1;
+            fstk[fsp++] = fnode.first;
+            continue;
+        }
+        RT_CNT(far_cands, fnode.count);
+        for (int k = fnode.first; k < fnode.first + fnode.count; k++) {
+            const FarTri& ft = V.far_tris[k];
+            if (far_candidate(ft, fr, o, d) && prim_test_any(V.all[ft.id], o, d)) return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace rt580

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/rt580.h"
+#include "rt_isect.h"
 
 // Deepest recursion supported (reference default 4; BASELINE config 5 uses 8).
 #define RT_MAX_DEPTH 16
@@ -19,6 +20,8 @@ struct DevScene {
     int n_prims;
     int n_lights;
     int n_ambient;
+    int use_bvh;   // triangle scenes: exact BVH queries (rt_isect.h) instead of brute force
+    BvhView bv;
 };
 
 struct DevFrame {
@@ -75,6 +78,23 @@ struct DevWork {
     const uint32_t* mt_stream;  // mt19937 draws (absolute index), else null
     uint32_t node_cap;
     uint32_t call_cap;
+    // BVH scenes: AO rays that miss every near triangle, queued for the sorted
+    // far-hit pass (rt_bvh.h): (o.xyz, call) and (d.xyz, -) per ray, its
+    // direction key, and the radix sort's double buffers + temporary storage.
+    float4* far_rays;      // [2 * far_cap]
+    uint32_t* far_keys;    // [far_cap] x2 (keys, sorted keys)
+    uint32_t* far_keys_alt;
+    uint32_t* far_vals;    // [far_cap] x2 (ray index, sorted)
+    uint32_t* far_vals_alt;
+    uint32_t* far_count;   // [1]
+    uint32_t* far_count_host;  // pinned
+    void* sort_tmp;
+    size_t sort_tmp_bytes;
+    uint32_t far_cap;
+    // provisional closest hits of the tree rays (node id) between the near and
+    // far phases of a BVH trace level: (t, alpha, beta, gamma), prim (-1: none)
+    float4* hit4;          // [node_cap]
+    int32_t* hit_prim;     // [node_cap]
 };
 
 void upload_minstd_table(hipStream_t s);
@@ -86,6 +106,8 @@ hipError_t launch_row_counts(const DevScene& S, const DevFrame& F, const DevWork
 hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, const uint64_t* row_base_global,
                        hipStream_t s);
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s);
+// Temporary storage of the far-queue radix sort for `cap` rays.
+size_t far_sort_tmp_bytes(uint32_t cap);
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s);
 hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows,
                             int16_t* dst, hipStream_t s);

@@ -29,8 +29,11 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include "../../include/rt580.h"
 #include "rt_kernels.h"
+#include "rt_isect.h"
 #include "rt_libm.h"
 #include "rt_math.h"
 
@@ -72,73 +75,8 @@ __device__ __forceinline__ float canon_mt(uint32_t x) {      // r = 2^32
 }
 
 // ---------------------------------------------------------------- scene queries
-struct Hit {
-    float t, a, b, g;
-    int prim;
-};
-
-__device__ __forceinline__ rv3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
-
-// (num / den) < 0 exactly as the division would decide it, dividing only when
-// the signs do not already decide it (the quotient can still round to -0).
-__device__ __forceinline__ bool quot_lt0(float num, float den) {
-    if (num != num || den != den || num == 0.0f) return false;  // NaN, or +-0 / den
-    if (signbit(num) == signbit(den)) return false;             // > 0, +0 or +inf
-    return (num / den) < 0.0f;
-}
-
-// IntersectTriangle (Raytracer.cpp:348-409) with the ray-invariant part
-// precomputed. WANT_BARY: also return alpha/beta/gamma (closest hit); the
-// any-hit form only needs the accept/reject decision. Both decide exactly as
-// the reference's divisions would.
-template <bool WANT_BARY, bool SIGN = false>
-__device__ __forceinline__ bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
-    const rv3 N = ld3(P.nrm);
-    const float nd = v3_dot(N, d);
-    if (rt_lt_eps(fabsf(nd))) return false;  // NearlyEquals(nd, 0)
-    const float num = -(v3_dot(N, o) + P.d);
-    // t = num / nd <= EPSILON: decided by signs when t <= 0 (|nd| > EPSILON here)
-    if (SIGN && num == num && (num == 0.0f || signbit(num) != signbit(nd))) return false;
-    t = num / nd;
-    if (rt_lt_eps(t)) return false;           // t <= EPSILON
-    const rv3 Pp = v3_add(o, v3_scale(d, t));
-    const rv3 v0 = ld3(P.p0), v1 = ld3(P.p1), v2 = ld3(P.p2);
-    // CalcTriangleAreaSigned (Raytracer.cpp:937-942): 0.5 * dot(cross(B-A, C-A), N)
-    const float aa = 0.5f * v3_dot(v3_cross(v3_sub(v1, Pp), v3_sub(v2, Pp)), N);
-    const float bb = 0.5f * v3_dot(v3_cross(v3_sub(Pp, v0), v3_sub(v2, v0)), N);
-    const float gg = 0.5f * v3_dot(v3_cross(v3_sub(v1, v0), v3_sub(Pp, v0)), N);
-    if (SIGN) {
-        if (quot_lt0(aa, P.area) || quot_lt0(bb, P.area) || quot_lt0(gg, P.area)) return false;
-        if (WANT_BARY) {
-            a = aa / P.area;
-            b = bb / P.area;
-            g = gg / P.area;
-        }
-        return true;
-    }
-    a = aa / P.area;
-    b = bb / P.area;
-    g = gg / P.area;
-    return !(a < 0 || b < 0 || g < 0);
-}
-
-// IntersectSphere (Raytracer.cpp:419-464)
-__device__ __forceinline__ bool sph_test(const rt_prim& P, rv3 o, rv3 d, float& t) {
-    rv3 oc = v3_sub(o, ld3(P.p0));
-    float b = 2.0f * v3_dot(d, oc);
-    float c = v3_dot(oc, oc) - P.d;
-    float disc = (b * b) - (4.0f * c);
-    if (rt_lt_eps(disc)) return false;
-    float sq = sqrtf(disc);
-    float t0 = (-b + sq) / 2.0f;
-    float t1 = (-b - sq) / 2.0f;
-    bool g0 = rt_gt_eps(t0), g1 = rt_gt_eps(t1);
-    if (!g0 && !g1) return false;
-    if (!g0) t = t1;
-    else if (!g1) t = t0;
-    else t = fminf(t0, t1);
-    return true;
-}
+// Hit, tri_test, sph_test and the BVH queries (bvh_closest / bvh_any) live in
+// rt_isect.h, shared with the host-side BVH checker.
 
 // Stage primitives [base, base+n) in LDS (every thread of the workgroup calls it).
 __device__ __forceinline__ void load_tile(const rt_prim* __restrict__ prims, int base, int n, rt_prim* tile) {
@@ -385,20 +323,66 @@ __device__ __forceinline__ void wave_alloc2(uint32_t* counter, bool fa, bool fb,
     sb = base + na + (uint32_t)__popcll(mb & lt);
 }
 
+// Octahedral direction key (10 + 10 bits): groups AO rays of similar direction
+// for the far-hit pass (grouping only; never affects a result).
+__device__ __forceinline__ uint32_t dir_key(rv3 d) {
+    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float x = d.x / s, y = d.y / s;
+    if (d.z < 0.0f) {
+        const float ax = fabsf(x), ay = fabsf(y);
+        x = (1.0f - ay) * (x < 0.0f ? -1.0f : 1.0f);
+        y = (1.0f - ax) * (y < 0.0f ? -1.0f : 1.0f);
+    }
+    const uint32_t u = (uint32_t)fminf(fmaxf((x * 0.5f + 0.5f) * 1023.0f, 0.0f), 1023.0f);
+    const uint32_t v = (uint32_t)fminf(fmaxf((y * 0.5f + 0.5f) * 1023.0f, 0.0f), 1023.0f);
+    return (u << 10) | v;
+}
+
+// Wave-uniform loads of the plane tree (the node index is uniform: every lane
+// of the wave walks the same node sequence).
+__device__ __forceinline__ FarNode load_far_node(const FarNode* nodes, int j) {
+    const cu32_ptr src = (cu32_ptr)(nodes + j);
+    FarNode n;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&n);
+#pragma unroll
+    for (int k = 0; k < 12; k++) dst[k] = src[k];
+    return n;
+}
+__device__ __forceinline__ FarTri load_far_tri(const FarTri* tris, int j) {
+    const cu32_ptr src = (cu32_ptr)(tris + j);
+    FarTri t;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&t);
+#pragma unroll
+    for (int k = 0; k < 8; k++) dst[k] = src[k];
+    return t;
+}
+
 // ---------------------------------------------------------------- trace (one tree level)
 __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { return F.row_begin + lr * F.row_step; }
 
-__global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level) {
+// PHASE 0: the whole level in one pass (brute force, or BVH without sorted far
+// pass). BVH scenes with a plane tree split it: PHASE 1 = near closest hit,
+// provisional hit stored per node and rays that may still have a far hit
+// queued (sorted far_closest_kernel in between); PHASE 2 = shading from the
+// stored hit. Items [i0, i1) of the level.
+template <bool BVH, int PHASE>
+__global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
+                                                   uint32_t i1) {
     __shared__ rt_prim tile[TILE];
     const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
-    const uint32_t count = level == 0 ? npix : W.lvl[level];
     const uint32_t base_id = level == 0 ? 0u : W.lvl[LVL_BASE + level];
-    const uint32_t next_base = base_id + count;
+    // Children beyond the node capacity were not stored (the frame is re-rendered
+    // with a larger capacity, rt_shim.cpp check_capacity): never touch their ids.
+    const uint32_t room = W.node_cap > base_id ? W.node_cap - base_id : 0u;
+    const uint32_t count_req = level == 0 ? npix : W.lvl[level];
+    const uint32_t count_all = count_req < room ? count_req : room;
+    const uint32_t count = i1 < count_all ? i1 : count_all;
+    const uint32_t next_base = base_id + count_all;
     if (blockIdx.x == 0 && threadIdx.x == 0) W.lvl[LVL_BASE + level + 1] = next_base;
     const int bounces = F.depth - level;
-    const bool resident = stage_resident(S, tile);
+    const bool resident = BVH ? false : stage_resident(S, tile);
 
-    for (uint32_t b0 = blockIdx.x * TB; b0 < count; b0 += gridDim.x * TB) {
+    for (uint32_t b0 = i0 + blockIdx.x * TB; b0 < count; b0 += gridDim.x * TB) {
         const uint32_t item = b0 + threadIdx.x;
         const bool active = item < count;
         const uint32_t node = base_id + item;
@@ -417,7 +401,44 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             }
         }
         Hit h;
-        const bool hit = closest_hit(S, tile, resident, active, o, d, h);
+        h.t = 0; h.prim = 0;
+        if (PHASE == 1) {
+            const bool nh = active && bvh_closest(S.bv, o, d, h, /*with_far=*/false);
+            bool q = false;
+            if (active) {
+                W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
+                W.hit_prim[node] = nh ? h.prim : -1;
+                const FarNode root = load_far_node(S.bv.far_nodes, 0);
+                q = !dir_zero(d) && !(nh && h.t < far_T(far_ray(S.bv, o), root.min_dhi));
+            }
+            const uint64_t qm = __ballot(q);
+            if (qm) {
+                const int leader = __ffsll((unsigned long long)qm) - 1;
+                uint32_t qb = 0;
+                if ((threadIdx.x & 63) == leader) qb = atomicAdd(W.far_count, (uint32_t)__popcll(qm));
+                qb = __shfl(qb, leader);
+                if (q) {
+                    const uint32_t slot = qb + (uint32_t)__popcll(qm & lanemask_lt());
+                    W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float(node));
+                    W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+                    W.far_keys[slot] = dir_key(d);
+                    W.far_vals[slot] = slot;
+                }
+            }
+            continue;
+        }
+        bool hit;
+        if (PHASE == 2) {
+            hit = false;
+            if (active) {
+                const int32_t hp = W.hit_prim[node];
+                const float4 hv = W.hit4[node];
+                hit = hp >= 0;
+                h.t = hv.x; h.a = hv.y; h.b = hv.z; h.g = hv.w; h.prim = hp;
+            }
+        } else {
+            hit = BVH ? (active && bvh_closest(S.bv, o, d, h)) : closest_hit(S, tile, resident, active, o, d, h);
+        }
 
         HitInfo hi;
         rt_material m;
@@ -454,10 +475,12 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             }
             bool occluded;
             if (l.kind == RT_LIGHT_DIRECTIONAL) {
-                occluded = any_hit(S, tile, resident, hit, so, L2);
+                occluded = BVH ? (hit && bvh_any(S.bv, so, L2)) : any_hit(S, tile, resident, hit, so, L2);
             } else {
                 Hit sh;
-                const bool shit = closest_hit(S, tile, resident, hit, so, L2, sh);
+                sh.t = 0;
+                const bool shit = BVH ? (hit && bvh_closest(S.bv, so, L2, sh))
+                                      : closest_hit(S, tile, resident, hit, so, L2, sh);
                 occluded = shit && !(sh.t > dist);
             }
             if (hit && !occluded) local = px_add(local, local_color(S, F, hi, l, m, L));
@@ -641,9 +664,13 @@ __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWor
 // CalculateAmbientOcclusion (Raytracer.cpp:315-330) + RandomInHemisphere (:283-292)
 // + RandomUnitVector (:269-281): one lane per (call, sample).
 // VARIANT bits (A/B switches, results identical): 1 = sincos table in LDS,
-// 2 = scalar per-call data (readfirstlane), 4 = sign-decided triangle rejects.
+// 2 = scalar per-call data (readfirstlane), 4 = sign-decided triangle rejects,
+// 8 = scalar (wave-uniform) scene loop, 16 = 8-waves/SIMD register cap,
+// 512 = exact BVH queries (triangle scenes; rt_isect.h).
+// AO items [item_begin, item_end) (item = call * N + sample).
 template <int VARIANT>
-__device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, const DevWork& W) {
+__device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, const DevWork& W,
+                                        uint64_t item_begin = 0, uint64_t item_end = ~0ull) {
     __shared__ rt_prim tile[TILE];
     __shared__ double sct_lds[440];  // glibc __sincostab, staged once per workgroup
     const double* sct = rt_dev::rt_sincostab;
@@ -653,12 +680,13 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
         sct = sct_lds;
     }
     const uint32_t N = (uint32_t)F.ao_samples;
-    const uint64_t items = W.totals[0] * (uint64_t)N;
+    const uint64_t items_all = W.totals[0] * (uint64_t)N;
+    const uint64_t items = item_end < items_all ? item_end : items_all;
     const bool pow2 = (N & (N - 1)) == 0;
     const int log2n = 31 - __clz((int)N);
     const bool wave_per_call = (VARIANT & 2) && (N & 63u) == 0;
-    const bool resident = (VARIANT & 8) ? true : stage_resident(S, tile);
-    for (uint64_t b0 = (uint64_t)blockIdx.x * TB; b0 < items; b0 += (uint64_t)gridDim.x * TB) {
+    const bool resident = (VARIANT & (8 | 512)) ? true : stage_resident(S, tile);
+    for (uint64_t b0 = item_begin + (uint64_t)blockIdx.x * TB; b0 < items; b0 += (uint64_t)gridDim.x * TB) {
         const uint64_t item = b0 + threadIdx.x;
         const bool active = item < items;
         uint64_t c = 0;
@@ -712,8 +740,27 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
             d = (VARIANT & 128) ? v : v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
         }
         const bool hit = (VARIANT & 32) ? (d.x > 2.0f)  // DIAGNOSTIC ablation only
+                       : (VARIANT & 512) ? (active && bvh_any(S.bv, o, d, /*with_far=*/false))
                        : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
                                        : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
+        if (VARIANT & 512) {
+            // rays that miss every near triangle go to the sorted far-hit pass
+            const bool q = active && !hit && S.bv.has_far;
+            const uint64_t qm = __ballot(q);
+            if (qm) {
+                const int leader = __ffsll((unsigned long long)qm) - 1;
+                uint32_t base = 0;
+                if ((threadIdx.x & 63) == leader) base = atomicAdd(W.far_count, (uint32_t)__popcll(qm));
+                base = __shfl(base, leader);
+                if (q) {
+                    const uint32_t slot = base + (uint32_t)__popcll(qm & lanemask_lt());
+                    W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
+                    W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+                    W.far_keys[slot] = dir_key(d);
+                    W.far_vals[slot] = slot;
+                }
+            }
+        }
         if ((N & 63u) == 0) {
             const uint64_t m = __ballot(active && hit);
             if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.occ[c], (uint32_t)__popcll(m));
@@ -726,6 +773,124 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
 template <int VARIANT>
 __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork W) {
     ao_body<VARIANT>(S, F, W);
+}
+
+// BVH scenes: near any-hit of AO items [b, e); misses are queued (far pass below).
+__global__ void __launch_bounds__(TB) ao_near_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
+    ao_body<513>(S, F, W, b, e);
+}
+
+// ---------------------------------------------------------------- far-hit pass
+// The queued AO rays, sorted by direction key, 64 per wave: the wave walks the
+// plane tree once for all its lanes (a node is entered if any live lane may
+// have a far hit below it), each lane evaluating the exact tests of rt_isect.h
+// for its own ray. Same candidates, same full tests as bvh_any's far search.
+__global__ void __launch_bounds__(TB) far_any_kernel(DevScene S, DevWork W, uint32_t n) {
+    __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * TB;
+    for (uint32_t base = (blockIdx.x * (TB / 64) + wave) * 64u; base < n; base += stride) {
+        const uint32_t i = base + lane;
+        bool live = i < n;
+        rv3 o = v3(0, 0, 0), d = v3(1, 0, 0);
+        uint32_t call = 0;
+        if (live) {
+            const uint32_t r = W.far_vals_alt[i];
+            const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
+            o = v3(a.x, a.y, a.z);
+            call = __float_as_uint(a.w);
+            d = v3(b.x, b.y, b.z);
+        }
+        const FarRay fr = far_ray(S.bv, o);
+        bool hit = false;
+        int sp = 0;
+        stk[wave][sp++] = 0;  // every lane writes the same value: no cross-lane ordering needed
+        while (sp > 0) {
+            if (__ballot(live) == 0) break;
+            const int node = __builtin_amdgcn_readfirstlane(stk[wave][--sp]);
+            const FarNode fn = load_far_node(S.bv.far_nodes, node);
+            float T;
+            const bool may = live && far_node_may(fn, fr, o, d, T);
+            if (__ballot(may) == 0) continue;
+            if (fn.count == 0) {
+                stk[wave][sp++] = fn.first + 1;
+                stk[wave][sp++] = fn.first;
+                continue;
+            }
+            for (int k = fn.first; k < fn.first + fn.count; k++) {
+                const FarTri ft = load_far_tri(S.bv.far_tris, k);
+                bool cand = may && live && far_candidate(ft, fr, o, d);
+                if (__ballot(cand) == 0) continue;
+                const rt_prim P = load_prim_scalar(S.prims, (int)ft.id);
+                if (cand && prim_test_any(P, o, d)) {
+                    hit = true;
+                    live = false;
+                }
+            }
+        }
+        if (hit) atomicAdd(&W.occ[call], 1u);
+    }
+}
+
+// Queued tree rays of a BVH trace level (sorted by direction key): the far part
+// of bvh_closest, merged into the provisional hit with the same lexicographic
+// rule; wave-cooperative like far_any_kernel.
+__global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, uint32_t n) {
+    __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * TB;
+    for (uint32_t base = (blockIdx.x * (TB / 64) + wave) * 64u; base < n; base += stride) {
+        const uint32_t i = base + lane;
+        const bool live = i < n;
+        rv3 o = v3(0, 0, 0), d = v3(1, 0, 0);
+        uint32_t node = 0;
+        Hit h;
+        h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
+        bool found = false;
+        if (live) {
+            const uint32_t r = W.far_vals_alt[i];
+            const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
+            o = v3(a.x, a.y, a.z);
+            node = __float_as_uint(a.w);
+            d = v3(b.x, b.y, b.z);
+            const float4 hv = W.hit4[node];
+            h.prim = W.hit_prim[node];
+            found = h.prim >= 0;
+            h.t = hv.x; h.a = hv.y; h.b = hv.z; h.g = hv.w;
+        }
+        const FarRay fr = far_ray(S.bv, o);
+        bool changed = false;
+        int sp = 0;
+        stk[wave][sp++] = 0;
+        while (sp > 0) {
+            const int fnode = __builtin_amdgcn_readfirstlane(stk[wave][--sp]);
+            const FarNode fn = load_far_node(S.bv.far_nodes, fnode);
+            float T;
+            const bool may = live && far_node_may(fn, fr, o, d, T) && !(found && h.t < T);
+            if (__ballot(may) == 0) continue;
+            if (fn.count == 0) {
+                stk[wave][sp++] = fn.first + 1;
+                stk[wave][sp++] = fn.first;
+                continue;
+            }
+            for (int k = fn.first; k < fn.first + fn.count; k++) {
+                const FarTri ft = load_far_tri(S.bv.far_tris, k);
+                const bool cand = may && far_candidate(ft, fr, o, d);
+                if (__ballot(cand) == 0) continue;
+                const rt_prim P = load_prim_scalar(S.prims, (int)ft.id);
+                float t, a, b, g;
+                if (cand && prim_test_closest(P, o, d, t, a, b, g) && lex_better(t, (int)ft.id, found, h)) {
+                    found = true;
+                    changed = true;
+                    h.t = t; h.a = a; h.b = b; h.g = g; h.prim = (int)ft.id;
+                }
+            }
+        }
+        if (changed) {
+            W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
+            W.hit_prim[node] = h.prim;
+        }
+    }
 }
 
 // Same kernel with the register budget capped for 8 waves per SIMD (SGPR <= 80
@@ -847,14 +1012,59 @@ void upload_minstd_table(hipStream_t s) {
     (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
 }
 
+// Sort the far queue (W.far_count entries) by direction key; returns its length.
+static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq) {
+    hipError_t e = hipMemcpyAsync(W.far_count_host, W.far_count, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    nq = *W.far_count_host;
+    if (nq == 0) return hipSuccess;
+    size_t tmp = W.sort_tmp_bytes;
+    return hipcub::DeviceRadixSort::SortPairs(W.sort_tmp, tmp, W.far_keys, W.far_keys_alt, W.far_vals,
+                                              W.far_vals_alt, (int)nq, 0, 20, s);
+}
+
 hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     const uint64_t npix = (uint64_t)F.n_rows * F.width;
     hipError_t e = hipMemsetAsync(W.lvl, 0, sizeof(uint32_t) * 2 * LVL_BASE, s);
     if (e != hipSuccess) return e;
+    const bool split = S.use_bvh && S.bv.has_far && W.hit4 && W.far_cap;
     for (int level = 0; level <= F.depth; level++) {
+        if (split) {
+            // near phase, sorted far pass, shading; in chunks of the far queue's capacity
+            uint32_t count = (uint32_t)npix;
+            if (level > 0) {
+                if ((e = hipMemcpyAsync(W.far_count_host, W.lvl + level, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                    (e = hipStreamSynchronize(s)) != hipSuccess)
+                    return e;
+                count = *W.far_count_host;
+            }
+            if (count == 0) {  // still publish the next level's base
+                hipLaunchKernelGGL((trace_kernel<true, 2>), dim3(1), dim3(TB), 0, s, S, F, W, level, 0u, 0u);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                continue;
+            }
+            for (uint32_t c0 = 0; c0 < count; c0 += W.far_cap) {
+                const uint32_t c1 = count - c0 > W.far_cap ? c0 + W.far_cap : count;
+                const int grid = grid_for(c1 - c0, 1 << 20);
+                if ((e = hipMemsetAsync(W.far_count, 0, 4, s)) != hipSuccess) return e;
+                hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                uint32_t nq = 0;
+                if ((e = sort_far_queue(W, s, nq)) != hipSuccess) return e;
+                if (nq) {
+                    hipLaunchKernelGGL(far_closest_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                }
+                hipLaunchKernelGGL((trace_kernel<true, 2>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
+            continue;
+        }
         // level 0 has exactly npix rays; deeper levels read their count on the device
         const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, 4096);
-        hipLaunchKernelGGL(trace_kernel, dim3(grid), dim3(TB), 0, s, S, F, W, level);
+        if (S.use_bvh) hipLaunchKernelGGL((trace_kernel<true, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
+        else hipLaunchKernelGGL((trace_kernel<false, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -875,6 +1085,13 @@ hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, c
     return hipGetLastError();
 }
 
+size_t far_sort_tmp_bytes(uint32_t cap) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, 0, 20);
+    return bytes;
+}
+
 static int ao_variant() {
     static int v = -1;
     if (v < 0) {
@@ -886,6 +1103,29 @@ static int ao_variant() {
 
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     if (!F.ao_enabled || S.n_ambient == 0 || F.n_rows == 0) return hipSuccess;
+    if (S.use_bvh) {
+        // chunks of the AO items: near pass + queue, sort the misses by
+        // direction, wave-cooperative far pass
+        uint64_t calls = 0;
+        hipError_t e = hipMemcpyAsync(&calls, W.totals, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        const uint64_t items = calls * (uint64_t)F.ao_samples;
+        const uint64_t chunk = S.bv.has_far ? (uint64_t)W.far_cap : items;
+        for (uint64_t b = 0; b < items; b += chunk) {
+            const uint64_t e1 = b + chunk < items ? b + chunk : items;
+            if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 4, s)) != hipSuccess) return e;
+            hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if (!S.bv.has_far) continue;
+            uint32_t nq = 0;
+            if ((e = sort_far_queue(W, s, nq)) != hipSuccess) return e;
+            if (nq == 0) continue;
+            hipLaunchKernelGGL(far_any_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     const int v = ao_variant();
     if (v & 16) {
         switch (v & 15) {

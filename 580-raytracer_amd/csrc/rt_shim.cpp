@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/rt580.h"
+#include "rt_bvh.h"
 #include "rt_kernels.h"
 
 using namespace rt580;
@@ -39,10 +40,19 @@ struct State {
     DevBuf prims, shade, mats, lights;
     int n_prims = 0, n_lights = 0, n_ambient = 0, n_nonambient = 0;
     bool have_scene = false;
+    // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
+    DevBuf bvh_nodes, bvh_prims, bvh_ids, far_nodes, far_tris, brute;
+    BvhBuild bvh;
+    bool bvh_ok = false;
+    int accel = RT_ACCEL_AUTO;
+    bool last_accel = false;
     uint64_t scene_gen = 0;
     // workspace
     DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
         row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream;
+    DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim;
+    uint32_t* far_count_host = nullptr;  // pinned
+    uint32_t far_cap = 0;
     uint32_t node_cap = 0, call_cap = 0;
     double node_factor = 4.0;         // node capacity per pixel (grown on overflow)
     uint32_t* needed_host = nullptr;  // pinned
@@ -110,8 +120,9 @@ int check_params(const rt_render_params* p) {
     return RT_SUCCESS;
 }
 
-DevScene dev_scene() {
+DevScene dev_scene(const rt_render_params* p) {
     DevScene s;
+    std::memset(&s, 0, sizeof s);
     s.prims = (const rt_prim*)g.prims.p;
     s.shade = (const rt_prim_shade*)g.shade.p;
     s.mats = (const rt_material*)g.mats.p;
@@ -119,7 +130,35 @@ DevScene dev_scene() {
     s.n_prims = g.n_prims;
     s.n_lights = g.n_lights;
     s.n_ambient = g.n_ambient;
+    s.use_bvh = g.accel == RT_ACCEL_AUTO && g.bvh_ok && bvh_usable(g.bvh, p->cam_from);
+    BvhView& v = s.bv;
+    v.all = s.prims;
+    v.nodes = (const BvhNode*)g.bvh_nodes.p;
+    v.prims = (const rt_prim*)g.bvh_prims.p;
+    v.ids = (const uint32_t*)g.bvh_ids.p;
+    v.far_nodes = (const FarNode*)g.far_nodes.p;
+    v.far_tris = (const FarTri*)g.far_tris.p;
+    v.brute = (const uint32_t*)g.brute.p;
+    v.n_brute = (int)g.bvh.brute.size();
+    v.has_tree = !g.bvh.nodes.empty();
+    v.has_far = !g.bvh.far_nodes.empty();
+    {   // DIAGNOSTIC (timing ablation only, wrong results): RT580_BVH_DIAG=1 skips the far search
+        static int diag = -1;
+        if (diag < 0) {
+            const char* e = std::getenv("RT580_BVH_DIAG");
+            diag = e ? std::atoi(e) : 0;
+        }
+        if (diag & 1) v.has_far = 0;
+    }
+    v.scale = g.bvh.scale;
     return s;
+}
+
+template <typename T>
+int upload_vec(DevBuf& b, const std::vector<T>& v) {
+    if (ensure(b, sizeof(T) * v.size() + 64)) return RT_FAILURE;
+    if (!v.empty()) HIP_TRY(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, g.stream));
+    return RT_SUCCESS;
 }
 
 DevFrame dev_frame(const rt_render_params* p, int row_begin, int row_step, int n_rows) {
@@ -164,6 +203,19 @@ DevWork dev_work() {
     w.mt_stream = (const uint32_t*)g.mt_stream.p;
     w.node_cap = g.node_cap;
     w.call_cap = g.call_cap;
+    w.far_rays = (float4*)g.far_rays.p;
+    w.far_keys = (uint32_t*)g.far_keys.p;
+    w.far_keys_alt = (uint32_t*)g.far_keys_alt.p;
+    w.far_vals = (uint32_t*)g.far_vals.p;
+    w.far_vals_alt = (uint32_t*)g.far_vals_alt.p;
+    w.far_count = (uint32_t*)g.far_count.p;
+    w.far_count_host = g.far_count_host;
+    w.sort_tmp = g.sort_tmp.p;
+    w.sort_tmp_bytes = g.sort_tmp.bytes;
+    w.far_cap = g.far_cap;
+    const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
+    w.hit4 = split ? (float4*)g.hit4.p : nullptr;
+    w.hit_prim = split ? (int32_t*)g.hit_prim.p : nullptr;
     return w;
 }
 
@@ -202,6 +254,19 @@ int ensure_work(const rt_render_params* p, int n_rows) {
         return RT_FAILURE;
     g.node_cap = (uint32_t)cap;
     g.call_cap = (uint32_t)ccap;
+    // far-hit queue of the BVH AO pass (chunks of at most far_cap AO rays)
+    if (g.bvh_ok && !g.bvh.far_nodes.empty() && g.far_cap == 0) {
+        const uint32_t fc = 1u << 24;
+        if (ensure(g.far_rays, (size_t)fc * 32) || ensure(g.far_keys, (size_t)fc * 4) ||
+            ensure(g.far_keys_alt, (size_t)fc * 4) || ensure(g.far_vals, (size_t)fc * 4) ||
+            ensure(g.far_vals_alt, (size_t)fc * 4) || ensure(g.far_count, 64) ||
+            ensure(g.sort_tmp, far_sort_tmp_bytes(fc) + 256))
+            return RT_FAILURE;
+        g.far_cap = fc;
+    }
+    if (g.bvh_ok && !g.bvh.far_nodes.empty() &&
+        (ensure(g.hit4, (size_t)cap * 16) || ensure(g.hit_prim, (size_t)cap * 4)))
+        return RT_FAILURE;
     return RT_SUCCESS;
 }
 
@@ -210,8 +275,10 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     if (ensure_work(p, n_rows)) return RT_FAILURE;
     HIP_TRY(hipMemsetAsync(g.needed.p, 0, 4, g.stream));
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
-    HIP_TRY(launch_trace(dev_scene(), f, dev_work(), g.stream));
-    HIP_TRY(launch_row_counts(dev_scene(), f, dev_work(), g.stream));
+    const DevScene sc = dev_scene(p);
+    g.last_accel = sc.use_bvh != 0;
+    HIP_TRY(launch_trace(sc, f, dev_work(), g.stream));
+    HIP_TRY(launch_row_counts(sc, f, dev_work(), g.stream));
     HIP_TRY(hipEventRecord(g.ev[EV_TRACE], g.stream));
     g.last_rows = n_rows;
     g.last_width = p->width;
@@ -242,13 +309,14 @@ int prepare_mt_stream(const rt_render_params* p) {
 int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_rows, const uint64_t* row_base_global,
                int16_t* fb_out) {
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
-    HIP_TRY(launch_rank(dev_scene(), f, dev_work(), row_base_global, g.stream));
+    const DevScene sc = dev_scene(p);
+    HIP_TRY(launch_rank(sc, f, dev_work(), row_base_global, g.stream));
     HIP_TRY(hipEventRecord(g.ev[EV_RANK], g.stream));
     if (prepare_mt_stream(p)) return RT_FAILURE;
     DevWork w = dev_work();
-    HIP_TRY(launch_ao(dev_scene(), f, w, g.stream));
+    HIP_TRY(launch_ao(sc, f, w, g.stream));
     HIP_TRY(hipEventRecord(g.ev[EV_AO], g.stream));
-    HIP_TRY(launch_resolve(dev_scene(), f, w, fb_out, g.stream));
+    HIP_TRY(launch_resolve(sc, f, w, fb_out, g.stream));
     HIP_TRY(hipEventRecord(g.ev[EV_RESOLVE], g.stream));
     return RT_SUCCESS;
 }
@@ -296,6 +364,7 @@ int rt_gpu_init(int device) {
     for (auto& ev : g.ev_default) HIP_TRY(hipEventCreate(&ev));
     g.ev = g.ev_default.data();
     HIP_TRY(hipHostMalloc((void**)&g.needed_host, 64, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&g.far_count_host, 64, hipHostMallocDefault));
     upload_minstd_table(g.stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(g.stream));
@@ -339,6 +408,20 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         HIP_TRY(hipMemcpyAsync(g.mats.p, s->materials, sizeof(rt_material) * s->n_materials, hipMemcpyHostToDevice, g.stream));
     if (s->n_lights)
         HIP_TRY(hipMemcpyAsync(g.lights.p, s->lights, sizeof(rt_light) * s->n_lights, hipMemcpyHostToDevice, g.stream));
+    // exact BVH for triangle scenes that do not fit one LDS tile (rt_bvh.h)
+    g.bvh = BvhBuild();
+    g.bvh_ok = false;
+    if (s->n_prims > 64) {
+        g.bvh_ok = build_bvh(s->prims, s->n_prims, g.bvh);
+        if (g.bvh_ok && (upload_vec(g.bvh_nodes, g.bvh.nodes) || upload_vec(g.bvh_prims, g.bvh.prims) ||
+                         upload_vec(g.bvh_ids, g.bvh.ids) || upload_vec(g.far_nodes, g.bvh.far_nodes) ||
+                         upload_vec(g.far_tris, g.bvh.far_tris) || upload_vec(g.brute, g.bvh.brute)))
+            return RT_FAILURE;
+        // the device needs only the arrays; keep the host copy small
+        g.bvh.prims = std::vector<rt_prim>();
+        g.bvh.ids = std::vector<uint32_t>();
+        g.bvh.far_tris = std::vector<FarTri>();
+    }
     HIP_TRY(hipStreamSynchronize(g.stream));
     g.n_prims = s->n_prims;
     g.n_lights = s->n_lights;
@@ -433,6 +516,15 @@ int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device
     return shade_rows(p, p->row_begin, p->row_step, n_selected_rows(p), row_base_device, fb_device);
 }
 
+int rt_gpu_set_accel(int mode) {
+    if (mode != RT_ACCEL_BRUTE && mode != RT_ACCEL_AUTO) return fail("bad accel mode %d", mode);
+    g.accel = mode;
+    g.verified_valid = false;  // node capacity is re-verified under the new mode
+    return RT_SUCCESS;
+}
+
+int rt_gpu_accel_active(void) { return g.last_accel ? 1 : 0; }
+
 int rt_gpu_last_stats(rt_render_stats* st) {
     if (!st) return RT_INVALID_ARG;
     std::memset(st, 0, sizeof *st);
@@ -495,6 +587,10 @@ void rt_gpu_shutdown(void) {
     if (!g.inited) return;
     (void)hipSetDevice(g.device);
     (void)hipStreamSynchronize(g.stream);
+    for (DevBuf* b : {&g.bvh_nodes, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
+                      &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
+                      &g.hit4, &g.hit_prim})
+        release(*b);
     for (DevBuf* b : {&g.prims, &g.shade, &g.mats, &g.lights, &g.nodes, &g.rays, &g.lvl, &g.needed, &g.pix_hits,
                       &g.pix_nodes, &g.pix_prefix, &g.row_calls, &g.row_hits, &g.row_nodes, &g.row_base_local,
                       &g.totals, &g.call_node, &g.call_rng, &g.occ, &g.fb, &g.fb_full, &g.mt_stream})
@@ -504,6 +600,7 @@ void rt_gpu_shutdown(void) {
     for (auto& q : g.prof_pool)
         for (auto& ev : q) (void)hipEventDestroy(ev);
     if (g.needed_host) (void)hipHostFree(g.needed_host);
+    if (g.far_count_host) (void)hipHostFree(g.far_count_host);
     if (g.own_stream) (void)hipStreamDestroy(g.own_stream);
     g = State();
 }

@@ -144,11 +144,6 @@ def main():
             frame_np = frame.cpu().numpy()
         want = next(e for e in helpers.golden_entries(False) if e["name"] == "config2_1080p_d4_ao64")["sha256"]
         check_ok = helpers.sha256(rt580.ppm_bytes(frame_np)) == want
-    # rays of one frame (this rank's rows), from the count pass of the last frame
-    st = rt580.RenderStats()
-    rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "rt_gpu_last_stats")
-    local = st.as_dict()
-
     rt580.check(lib.rt_gpu_profile(1), "rt_gpu_profile")
     barrier()
     torch.cuda.synchronize()
@@ -167,6 +162,10 @@ def main():
     rt580.check(lib.rt_gpu_profile_read(*[ctypes.byref(m) for m in ms], ctypes.byref(frames)), "rt_gpu_profile_read")
     per_frame = [m.value / max(frames.value, 1) for m in ms]  # trace, rank, ao, resolve
     rt580.check(lib.rt_gpu_profile(0), "rt_gpu_profile")
+    # rays of one frame (this rank's rows), from the count pass of the last frame
+    st = rt580.RenderStats()
+    rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "rt_gpu_last_stats")
+    local = st.as_dict()
 
     rays_local = int(local["rays_total"])
     if world > 1:
@@ -211,6 +210,8 @@ def main():
                 "rng": "minstd_rand0 (libstdc++ default_random_engine)",
                 "rays_per_frame": rays_frame,
                 "parallelism": "interleaved rows x%d + RCCL all_gather/gather" % world if world > 1 else "1 GPU",
+                "scene_query": "exact BVH + plane tree (rt_bvh.h)" if lib.rt_gpu_accel_active() else
+                               "brute force (every primitive per ray, as the reference)",
             },
             "kernel_ms_per_frame": {
                 "trace": round(per_frame[0], 4),

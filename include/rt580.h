@@ -171,6 +171,15 @@ int rt_gpu_render_device(const rt_render_params* params, int16_t** fb_device);
 int rt_gpu_count_rows(const rt_render_params* params, uint32_t* row_calls_device);
 int rt_gpu_shade_rows(const rt_render_params* params, const uint64_t* row_base_device,
                       int16_t* fb_device);
+/* Scene-query acceleration. RT_ACCEL_BRUTE tests every primitive per ray, as
+ * the reference's IntersectScene does (Raytracer.cpp:473-526); RT_ACCEL_AUTO
+ * (default) uses the exact-semantics BVH for triangle scenes larger than one
+ * LDS tile (identical results; see 580-raytracer_amd/csrc/rt_bvh.h). Applies
+ * to the following renders. rt_gpu_accel_active: 1 if the last frame used it. */
+#define RT_ACCEL_BRUTE 0
+#define RT_ACCEL_AUTO 1
+int rt_gpu_set_accel(int mode);
+int rt_gpu_accel_active(void);
 /* Counters and HIP-event timings of the last render. */
 int rt_gpu_last_stats(rt_render_stats* stats);
 /* Bench profiling: with enable=1 every following frame records its own HIP

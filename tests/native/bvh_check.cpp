@@ -1,0 +1,185 @@
+// BVH exactness check (CPU): for random rays of every kind the path casts
+// (camera, AO-style hemisphere rays from surface points, reflection-style rays,
+// and grazing rays nearly parallel to a triangle's plane that provoke the
+// reference's far "hits"), the BVH queries of rt_isect.h must return exactly
+// what the reference's brute-force IntersectScene loop returns
+// (Raytracer.cpp:473-526: every primitive in order, first hit taken, later hits
+// only if strictly closer): the same primitive, t and barycentrics bit for bit,
+// and the same any-hit boolean.
+//
+// usage: bvh_check <assets root> <scene.json> <rays> [seed]
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../580-raytracer_amd/csrc/rt_isect.h"
+#include "../../580-raytracer_amd/csrc/rt_scene.h"
+
+using namespace rt580;
+
+static bool brute_closest(const std::vector<rt_prim>& P, rv3 o, rv3 d, Hit& h) {
+    bool found = false;
+    for (int j = 0; j < (int)P.size(); j++) {
+        float t, a, b, g;
+        if (prim_test_closest(P[j], o, d, t, a, b, g) && (!found || t < h.t)) {
+            found = true;
+            h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
+        }
+    }
+    return found;
+}
+
+static bool brute_any(const std::vector<rt_prim>& P, rv3 o, rv3 d) {
+    for (const rt_prim& p : P)
+        if (prim_test_any(p, o, d)) return true;
+    return false;
+}
+
+static uint32_t fbits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 4) {
+        std::fprintf(stderr, "usage: %s <root> <scene> <rays> [seed]\n", argv[0]);
+        return 2;
+    }
+    Scene s;
+    std::string err;
+    if (load_scene_json(argv[1], argv[2], s, err) != RT_SUCCESS) {
+        std::fprintf(stderr, "load failed: %s\n", err.c_str());
+        return 1;
+    }
+    PackedScene ps;
+    pack_scene(s, ps);
+    const std::vector<rt_prim>& P = ps.prims;
+    BvhBuild B;
+    const bool ok = build_bvh(P.data(), (int)P.size(), B);
+    std::printf("prims=%zu tris=%d bvh_ok=%d nodes=%zu depth=%d far_nodes=%zu far_depth=%d brute=%zu S=%g "
+                "build_ms=%.1f\n", P.size(), B.n_tri, ok, B.nodes.size(), B.depth, B.far_nodes.size(), B.far_depth,
+                B.brute.size(), B.scale, B.build_ms);
+    if (!ok) {
+        std::printf("mismatches=0 (no BVH for this scene)\n");
+        return 0;
+    }
+    BvhView V;
+    V.all = P.data();
+    V.nodes = B.nodes.data();
+    V.prims = B.prims.data();
+    V.ids = B.ids.data();
+    V.far_nodes = B.far_nodes.empty() ? nullptr : B.far_nodes.data();
+    V.far_tris = B.far_tris.empty() ? nullptr : B.far_tris.data();
+    V.brute = B.brute.data();
+    V.n_brute = (int)B.brute.size();
+    V.has_tree = !B.nodes.empty();
+    V.has_far = !B.far_nodes.empty();
+    V.scale = B.scale;
+
+    const long nrays = std::atol(argv[3]);
+    const unsigned seed = argc > 4 ? (unsigned)std::atoi(argv[4]) : 580u;
+    const rv3 cam = s.camera.from;
+    std::vector<int> tris;
+    for (int j = 0; j < (int)P.size(); j++)
+        if (P[j].kind == RT_PRIM_TRIANGLE) tris.push_back(j);
+    BvhView Vnear = V;  // control: without the far search some results must differ
+    Vnear.has_far = 0;
+    std::atomic<long> bad{0}, hits{0}, anyhits{0}, far_closest{0}, near_only_bad{0};
+#ifdef RT_BVH_COUNT
+    std::atomic<long> cnt[2][6] = {};  // [closest, any][counter]
+#endif
+    const int NT = 8;
+    std::vector<std::thread> th;
+    for (int tid = 0; tid < NT; tid++)
+        th.emplace_back([&, tid] {
+            std::mt19937 rng(seed * 7919u + tid);
+            std::uniform_real_distribution<float> U(0.0f, 1.0f);
+            for (long r = tid; r < nrays; r += NT) {
+                const int kind = (int)(r % 4);
+                rv3 o, d;
+                const rt_prim& T = P[tris[rng() % tris.size()]];
+                float u = U(rng), v = U(rng);
+                if (u + v > 1) { u = 1 - u; v = 1 - v; }
+                const rv3 p0 = ld3(T.p0), p1 = ld3(T.p1), p2 = ld3(T.p2), N = ld3(T.nrm);
+                const rv3 sp = v3_add(p0, v3_add(v3_scale(v3_sub(p1, p0), u), v3_scale(v3_sub(p2, p0), v)));
+                if (kind == 0) {  // camera ray towards a surface point (jittered)
+                    o = cam;
+                    d = v3_normalize(v3_sub(v3_add(sp, v3((U(rng) - 0.5f), (U(rng) - 0.5f), (U(rng) - 0.5f))), cam));
+                } else if (kind == 1 || kind == 2) {  // AO / reflection style: hemisphere from a surface point
+                    const float z = U(rng) * 2 - 1, a = U(rng) * 6.2831853f, rr = std::sqrt(1 - z * z);
+                    d = v3_normalize(v3(rr * std::cos(a), rr * std::sin(a), z));
+                    if (!(v3_dot(d, N) > 0.0f)) d = v3_neg(d);
+                    o = v3_add(sp, v3_scale(d, 0.2f));
+                    d = v3_normalize(d);
+                } else {  // grazing: nearly parallel to some triangle's plane (provokes far hits)
+                    const rt_prim& G = P[tris[rng() % tris.size()]];
+                    const rv3 n = ld3(G.nrm);
+                    rv3 w = v3_normalize(v3_cross(n, v3(U(rng) - 0.5f, U(rng) - 0.5f, U(rng) - 0.5f)));
+                    const float eps = std::ldexp(1.0f, -(int)(rng() % 22)) * (U(rng) - 0.5f);
+                    d = v3_normalize(v3_add(w, v3_scale(n, eps)));
+                    o = v3_add(sp, v3_scale(ld3(T.nrm), 0.2f));
+                }
+                Hit hb, hv;
+                const bool cb = brute_closest(P, o, d, hb);
+#ifdef RT_BVH_COUNT
+                g_bvh_cnt = BvhCounters{};
+#endif
+                const bool cv = bvh_closest(V, o, d, hv);
+#ifdef RT_BVH_COUNT
+                {
+                    const long* c = &g_bvh_cnt.nodes;
+                    for (int q = 0; q < 6; q++) cnt[0][q] += c[q];
+                    g_bvh_cnt = BvhCounters{};
+                }
+#endif
+                const bool ab = brute_any(P, o, d);
+                const bool av = bvh_any(V, o, d);
+#ifdef RT_BVH_COUNT
+                if (kind == 1 || kind == 2) {
+                    const long* c = &g_bvh_cnt.nodes;
+                    for (int q = 0; q < 6; q++) cnt[1][q] += c[q];
+                }
+#endif
+                bool same = cb == cv && ab == av;
+                if (same && cb)
+                    same = hb.prim == hv.prim && fbits(hb.t) == fbits(hv.t) && fbits(hb.a) == fbits(hv.a) &&
+                           fbits(hb.b) == fbits(hv.b) && fbits(hb.g) == fbits(hv.g);
+                {
+                    Hit hn;
+                    const bool cn = bvh_closest(Vnear, o, d, hn);
+                    const bool an = bvh_any(Vnear, o, d);
+                    if (cn != cb || an != ab || (cb && (hn.prim != hb.prim || fbits(hn.t) != fbits(hb.t))))
+                        near_only_bad++;
+                }
+                if (cb) hits++;
+                if (ab) anyhits++;
+                if (cb && hb.t > 1e5f) far_closest++;
+                if (!same) {
+                    if (bad.fetch_add(1) < 10)
+                        std::printf("MISMATCH ray %ld kind %d: brute (%d, prim %d, t %.9g) bvh (%d, prim %d, t %.9g) "
+                                    "any %d/%d\n", r, kind, cb, cb ? hb.prim : -1, cb ? hb.t : 0.0f, cv,
+                                    cv ? hv.prim : -1, cv ? hv.t : 0.0f, ab, av);
+                }
+            }
+        });
+    for (auto& t : th) t.join();
+#ifdef RT_BVH_COUNT
+    const char* names[6] = {"nodes", "leaf_tris", "far_nodes", "far_cands", "far_tests", "brute_tests"};
+    for (int w = 0; w < 2; w++) {
+        std::printf("%s per ray:", w ? "any-hit (AO-style rays)" : "closest (all rays)");
+        const double div = w ? nrays / 2.0 : (double)nrays;
+        for (int q = 0; q < 6; q++) std::printf(" %s=%.1f", names[q], cnt[w][q] / div);
+        std::printf("\n");
+    }
+#endif
+    std::printf("rays=%ld closest_hits=%ld any_hits=%ld far_closest_hits=%ld differ_without_far_search=%ld "
+                "mismatches=%ld\n", nrays, (long)hits, (long)anyhits, (long)far_closest, (long)near_only_bad, (long)bad);
+    return bad ? 1 : 0;
+}

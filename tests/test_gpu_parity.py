@@ -125,3 +125,25 @@ def test_multi_rank_split_on_one_gpu(world):
         bad = [y for y in rows if not np.array_equal(frame[y], full[y])]
         assert not bad, "rank %d/%d: rows %s differ" % (r, world, bad[:10])
     assert np.array_equal(frame, full)
+
+
+@pytest.mark.parametrize("scene,w,h,depth,ao", [
+    ("cornell10k.json", 160, 90, 4, 16),
+    ("field100k.json", 96, 54, 4, 8),
+    ("field100k.json", 64, 36, 6, 4),
+])
+def test_bvh_equals_brute_force(scene, w, h, depth, ao):
+    """The exact-semantics BVH path (default for triangle scenes) and the
+    reference's brute-force scene loop give identical frames and ray counts."""
+    lib = helpers.rt580().load()
+    root = helpers.synthetic_root(scene[:-5])
+    try:
+        assert lib.rt_gpu_set_accel(0) == 0
+        fb_b, st_b = render_gpu(scene, w, h, depth, ao, True, root=root)
+        assert lib.rt_gpu_accel_active() == 0
+    finally:
+        assert lib.rt_gpu_set_accel(1) == 0
+    fb_v, st_v = render_gpu(scene, w, h, depth, ao, True, root=root)
+    assert lib.rt_gpu_accel_active() == 1
+    assert np.array_equal(fb_b, fb_v), "%d pixels differ" % int((fb_b != fb_v).any(axis=2).sum())
+    assert st_b["rays_total"] == st_v["rays_total"]

@@ -14,11 +14,11 @@ BUILD = os.path.join(NATIVE, "_build")
 FLAGS = ["-O2", "-std=c++17", "-ffp-contract=off", "-pthread"]
 
 
-def _build(name):
+def _build(name, extra=()):
     os.makedirs(BUILD, exist_ok=True)
     exe = os.path.join(BUILD, name)
     src = os.path.join(NATIVE, name + ".cpp")
-    subprocess.run(["g++"] + FLAGS + ["-o", exe, src], check=True)
+    subprocess.run(["g++"] + FLAGS + ["-o", exe, src] + list(extra), check=True)
     return exe
 
 
@@ -47,3 +47,20 @@ def test_powf_random_pairs():
 
 def test_eps_compares_and_float_to_short_all_floats():
     _run(_build("eps_check"))
+
+
+CSRC = os.path.join(helpers.PKG, "csrc")
+
+
+@pytest.mark.parametrize("scene,rays", [("cornell10k", 60000), ("field100k", 4000)])
+def test_bvh_queries_equal_brute_force(scene, rays):
+    """The exact-semantics BVH (rt_bvh.h / rt_isect.h) against the reference's
+    brute-force IntersectScene loop on camera, AO, reflection and grazing rays:
+    same primitive, bit-identical t and barycentrics, same any-hit boolean. The
+    grazing rays provoke the reference's far "hits" (rt_bvh.h), which only the
+    plane-tree search finds: the control count without it must be non-zero."""
+    root = helpers.synthetic_root(scene)
+    exe = _build("bvh_check", [os.path.join(CSRC, "rt_scene.cpp"), os.path.join(CSRC, "rt_bvh.cpp")])
+    out = _run(exe, root, scene + ".json", str(rays))
+    if scene == "cornell10k":
+        assert "differ_without_far_search=0 " not in out, out
