@@ -85,6 +85,7 @@ struct BvhBuild {
     int depth = 0, far_depth = 0;   // deepest levels (stack bounds)
     int max_leaf = 0;
     int n_tri = 0;
+    int n_far = 0;                  // far_tris.size() (kept after the host copy is dropped)
     double inflate = 0.0;           // delta_j / e_min(j)
     double build_ms = 0.0;
 };

@@ -103,6 +103,8 @@ struct BvhView {
     const FarTri* far_tris;
     const uint32_t* brute;      // spheres + unanalysable triangles, ascending
     int n_brute;
+    int n_far;                  // far_tris entries
+    float far_root_min_dhi;     // smallest D_hi of the plane tree (root bound)
     int has_tree, has_far;
     float scale;                // S
 };
@@ -218,13 +220,51 @@ RTM_HD bool far_node_may(const FarNode& n, const FarRay& r, rv3 o, rv3 d, float&
 }
 
 // Is this plane crossed at t >= T_j (computed exactly as tri_test computes t)?
+// The division is only done when |num| >= 0.999 T |nd| with matching signs
+// (num / nd >= T needs that, with room for the roundings).
 RTM_HD bool far_candidate(const FarTri& ft, const FarRay& r, rv3 o, rv3 d) {
     const rv3 N = ld3(ft.n);
     const float nd = v3_dot(N, d);
     if (rt_lt_eps(fabsf(nd))) return false;
     const float num = -(v3_dot(N, o) + ft.d);
+    const float T = far_T(r, ft.dhi);
+    if (T > 0.0f && !(num * nd > 0.0f && fabsf(num) >= 0.999f * T * fabsf(nd))) return false;
     const float t = num / nd;
-    return t >= far_T(r, ft.dhi);
+    return t >= T;
+}
+
+// The far search of bvh_closest on its own (per ray): merges into h.
+RTM_HD bool far_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool found) {
+    if (dir_zero(d)) return found;
+    const FarRay fr = far_ray(V, o);
+    int32_t fstk[RT_BVH_STACK];
+    int fsp = 0;
+    fstk[fsp++] = 0;
+    while (fsp > 0) {
+        const FarNode& fnode = V.far_nodes[fstk[--fsp]];
+        RT_CNT(far_nodes, 1);
+        float T;
+        if (!far_node_may(fnode, fr, o, d, T)) continue;
+        if (found && h.t < T) continue;  // every far hit below has t >= T
+        if (fnode.count == 0) {
+            fstk[fsp++] = fnode.first + 1;
+            fstk[fsp++] = fnode.first;
+            continue;
+        }
+        RT_CNT(far_cands, fnode.count);
+        for (int k = fnode.first; k < fnode.first + fnode.count; k++) {
+            const FarTri& ft = V.far_tris[k];
+            if (!far_candidate(ft, fr, o, d)) continue;
+            RT_CNT(far_tests, 1);
+            const int j = (int)ft.id;
+            float t, a, b, g;
+            if (tri_test<true>(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
+                found = true;
+                h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
+            }
+        }
+    }
+    return found;
 }
 
 // with_far = false: brute list + spatial BVH only; the caller then runs the far
@@ -294,6 +334,12 @@ RTM_HD bool bvh_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool with_far = 
         if (!popped) break;
     }
     if (!V.has_far || !with_far) return found;
+    return far_closest(V, o, d, h, found);
+}
+
+// The far search of bvh_any on its own (per ray).
+RTM_HD bool far_any(const BvhView& V, rv3 o, rv3 d) {
+    if (dir_zero(d)) return false;
     const FarRay fr = far_ray(V, o);
     int32_t fstk[RT_BVH_STACK];
     int fsp = 0;
@@ -303,7 +349,6 @@ RTM_HD bool bvh_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool with_far = 
         RT_CNT(far_nodes, 1);
         float T;
         if (!far_node_may(fnode, fr, o, d, T)) continue;
-        if (found && h.t < T) continue;  // every far hit below has t >= T
         if (fnode.count == 0) {
             fstk[fsp++] = fnode.first + 1;
             fstk[fsp++] = fnode.first;
@@ -312,17 +357,10 @@ RTM_HD bool bvh_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool with_far = 
         RT_CNT(far_cands, fnode.count);
         for (int k = fnode.first; k < fnode.first + fnode.count; k++) {
             const FarTri& ft = V.far_tris[k];
-            if (!far_candidate(ft, fr, o, d)) continue;
-            RT_CNT(far_tests, 1);
-            const int j = (int)ft.id;
-            float t, a, b, g;
-            if (tri_test<true>(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
-                found = true;
-                h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
-            }
+            if (far_candidate(ft, fr, o, d) && prim_test_any(V.all[ft.id], o, d)) return true;
         }
     }
-    return found;
+    return false;
 }
 
 // with_far = false: brute list + spatial BVH only (the caller runs the far
@@ -369,27 +407,7 @@ RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true) {
         n = (int32_t)(stk[sp] >> 27);
     }
     if (!V.has_far || !with_far) return false;
-    const FarRay fr = far_ray(V, o);
-    int32_t fstk[RT_BVH_STACK];
-    int fsp = 0;
-    fstk[fsp++] = 0;
-    while (fsp > 0) {
-        const FarNode& fnode = V.far_nodes[fstk[--fsp]];
-        RT_CNT(far_nodes, 1);
-        float T;
-        if (!far_node_may(fnode, fr, o, d, T)) continue;
-        if (fnode.count == 0) {
-            fstk[fsp++] = fnode.first + 1;
-            fstk[fsp++] = fnode.first;
-            continue;
-        }
-        RT_CNT(far_cands, fnode.count);
-        for (int k = fnode.first; k < fnode.first + fnode.count; k++) {
-            const FarTri& ft = V.far_tris[k];
-            if (far_candidate(ft, fr, o, d) && prim_test_any(V.all[ft.id], o, d)) return true;
-        }
-    }
-    return false;
+    return far_any(V, o, d);
 }
 
 }  // namespace rt580

@@ -30,6 +30,8 @@
 #include <stdlib.h>
 
 #include <hipcub/hipcub.hpp>
+#include <cstdio>
+#include <vector>
 
 #include "../../include/rt580.h"
 #include "rt_kernels.h"
@@ -323,8 +325,19 @@ __device__ __forceinline__ void wave_alloc2(uint32_t* counter, bool fa, bool fb,
     sb = base + na + (uint32_t)__popcll(mb & lt);
 }
 
-// Octahedral direction key (10 + 10 bits): groups AO rays of similar direction
-// for the far-hit pass (grouping only; never affects a result).
+// Octahedral direction key (12 + 12 bits): groups rays of similar direction
+// for the far-hit passes (grouping only; never affects a result).
+#define RT_DIR_KEY_BITS 25
+#define RT_KEY_BRUTE (1u << 24)  // far-origin rays: brute-force scan, sorted after every direction key
+
+// Rays whose origin is so far out (a child of one of the reference's far hits)
+// that no triangle can be culled (T_root <= 0) or the fat-ray margin covers the
+// scene: the reference's own loop over every primitive (far_scan_kernel) is
+// cheaper than any traversal for them. Routing only; the results are the same.
+__device__ __forceinline__ bool far_origin(const DevScene& S, rv3 o, float root_min_dhi) {
+    const float oi = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    return oi > 64.0f * S.bv.scale || !(far_T(far_ray(S.bv, o), root_min_dhi) > 0.0f);
+}
 __device__ __forceinline__ uint32_t dir_key(rv3 d) {
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
     float x = d.x / s, y = d.y / s;
@@ -333,9 +346,9 @@ __device__ __forceinline__ uint32_t dir_key(rv3 d) {
         x = (1.0f - ay) * (x < 0.0f ? -1.0f : 1.0f);
         y = (1.0f - ax) * (y < 0.0f ? -1.0f : 1.0f);
     }
-    const uint32_t u = (uint32_t)fminf(fmaxf((x * 0.5f + 0.5f) * 1023.0f, 0.0f), 1023.0f);
-    const uint32_t v = (uint32_t)fminf(fmaxf((y * 0.5f + 0.5f) * 1023.0f, 0.0f), 1023.0f);
-    return (u << 10) | v;
+    const uint32_t u = (uint32_t)fminf(fmaxf((x * 0.5f + 0.5f) * 4095.0f, 0.0f), 4095.0f);
+    const uint32_t v = (uint32_t)fminf(fmaxf((y * 0.5f + 0.5f) * 4095.0f, 0.0f), 4095.0f);
+    return (u << 12) | v;
 }
 
 // Wave-uniform loads of the plane tree (the node index is uniform: every lane
@@ -403,14 +416,17 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
         Hit h;
         h.t = 0; h.prim = 0;
         if (PHASE == 1) {
-            const bool nh = active && bvh_closest(S.bv, o, d, h, /*with_far=*/false);
+            const FarNode root = load_far_node(S.bv.far_nodes, 0);
+            const bool brute = active && far_origin(S, o, root.min_dhi);
+            const bool nh = active && !brute && bvh_closest(S.bv, o, d, h, /*with_far=*/false);
             bool q = false;
             if (active) {
                 W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
                 W.hit_prim[node] = nh ? h.prim : -1;
-                const FarNode root = load_far_node(S.bv.far_nodes, 0);
-                q = !dir_zero(d) && !(nh && h.t < far_T(far_ray(S.bv, o), root.min_dhi));
+                q = brute || (!dir_zero(d) && !(nh && h.t < far_T(far_ray(S.bv, o), root.min_dhi)));
             }
+            const uint64_t bm = __ballot(brute);
+            if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
             const uint64_t qm = __ballot(q);
             if (qm) {
                 const int leader = __ffsll((unsigned long long)qm) - 1;
@@ -421,7 +437,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                     const uint32_t slot = qb + (uint32_t)__popcll(qm & lanemask_lt());
                     W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float(node));
                     W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
-                    W.far_keys[slot] = dir_key(d);
+                    W.far_keys[slot] = brute ? RT_KEY_BRUTE : dir_key(d);
                     W.far_vals[slot] = slot;
                 }
             }
@@ -696,6 +712,7 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
             else { c = item / N; s = (uint32_t)(item - c * N); }
         }
         rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+        bool ao_brute = false;
         if (active) {
             // With N a multiple of 64 a wave serves one call: keep its data scalar.
             uint32_t cc = (uint32_t)c;
@@ -738,15 +755,18 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
             if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
             o = v3_add(hp, v3_scale(v, 0.2f));
             d = (VARIANT & 128) ? v : v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
+            if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o, S.bv.far_root_min_dhi);
         }
         const bool hit = (VARIANT & 32) ? (d.x > 2.0f)  // DIAGNOSTIC ablation only
-                       : (VARIANT & 512) ? (active && bvh_any(S.bv, o, d, /*with_far=*/false))
+                       : (VARIANT & 512) ? (active && !ao_brute && bvh_any(S.bv, o, d, /*with_far=*/false))
                        : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
                                        : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
         if (VARIANT & 512) {
             // rays that miss every near triangle go to the sorted far-hit pass
             const bool q = active && !hit && S.bv.has_far;
             const uint64_t qm = __ballot(q);
+            const uint64_t bm = __ballot(ao_brute);
+            if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
             if (qm) {
                 const int leader = __ffsll((unsigned long long)qm) - 1;
                 uint32_t base = 0;
@@ -756,7 +776,7 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                     const uint32_t slot = base + (uint32_t)__popcll(qm & lanemask_lt());
                     W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
                     W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
-                    W.far_keys[slot] = dir_key(d);
+                    W.far_keys[slot] = ao_brute ? RT_KEY_BRUTE : dir_key(d);
                     W.far_vals[slot] = slot;
                 }
             }
@@ -830,6 +850,121 @@ __global__ void __launch_bounds__(TB) far_any_kernel(DevScene S, DevWork W, uint
         }
         if (hit) atomicAdd(&W.occ[call], 1u);
     }
+}
+
+// Per-lane variants (each lane walks its own path): better than the wave union
+// when the queue is too sparse for sorted waves to share a direction.
+__global__ void __launch_bounds__(TB) far_any_lane_kernel(DevScene S, DevWork W, uint32_t n) {
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
+        const uint32_t r = W.far_vals_alt[i];
+        const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
+        if (far_any(S.bv, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z))) atomicAdd(&W.occ[__float_as_uint(a.w)], 1u);
+    }
+}
+
+__global__ void __launch_bounds__(TB) far_closest_lane_kernel(DevScene S, DevWork W, uint32_t n) {
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
+        const uint32_t r = W.far_vals_alt[i];
+        const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
+        const uint32_t node = __float_as_uint(a.w);
+        const float4 hv = W.hit4[node];
+        Hit h;
+        h.prim = W.hit_prim[node];
+        h.t = hv.x; h.a = hv.y; h.b = hv.z; h.g = hv.w;
+        const bool found = h.prim >= 0;
+        const int prev = h.prim;
+        const float prev_t = h.t;
+        if (far_closest(S.bv, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), h, found) &&
+            (h.prim != prev || __float_as_uint(h.t) != __float_as_uint(prev_t))) {
+            W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
+            W.hit_prim[node] = h.prim;
+        }
+    }
+}
+
+// One wave per ray: the lanes stride over every plane with the exact candidate
+// test (a superset of what the tree visits: its pruning is only conservative),
+// full tests on the candidates, lexicographic wave reduction. Latency-friendly
+// for sparse queues, where sorted waves no longer share directions.
+// brute != 0: every primitive in scene order with the plain tests (the
+// reference's IntersectScene loop), for the far-origin rays.
+__global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uint32_t first, uint32_t n, int closest,
+                                                      int n_far, int brute) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n_scan = brute ? S.n_prims : n_far;
+    for (uint32_t i = first + blockIdx.x * (TB / 64) + wave; i < n; i += gridDim.x * (TB / 64)) {
+        const uint32_t r = W.far_vals_alt[i];
+        const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
+        const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+        const uint32_t tag = __float_as_uint(a.w);  // AO call (any) or tree node (closest)
+        if (!brute && dir_zero(d)) continue;
+        const FarRay fr = far_ray(S.bv, o);
+        if (!closest) {
+            bool hit = false;
+            for (int k0 = 0; k0 < n_scan; k0 += 64) {
+                const int k = k0 + lane;
+                if (k < n_scan) {
+                    if (brute) {
+                        if (prim_test_any(S.prims[k], o, d)) hit = true;
+                    } else {
+                        const FarTri ft = S.bv.far_tris[k];
+                        if (far_candidate(ft, fr, o, d) && prim_test_any(S.prims[ft.id], o, d)) hit = true;
+                    }
+                }
+                if (__ballot(hit)) break;
+            }
+            if (__ballot(hit) && lane == 0) atomicAdd(&W.occ[tag], 1u);
+            continue;
+        }
+        Hit h;
+        h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
+        bool found = false;
+        for (int k = lane; k < n_scan; k += 64) {
+            int id = k;
+            if (!brute) {
+                const FarTri ft = S.bv.far_tris[k];
+                if (!far_candidate(ft, fr, o, d)) continue;
+                id = (int)ft.id;
+            }
+            float t, aa, bb, gg;
+            if (prim_test_closest(S.prims[id], o, d, t, aa, bb, gg) && lex_better(t, id, found, h)) {
+                found = true;
+                h.t = t; h.a = aa; h.b = bb; h.g = gg; h.prim = id;
+            }
+        }
+        // lexicographic (t, prim) minimum over the wave; t > EPSILON > 0, so the
+        // float bits order like the values
+        uint64_t key = found ? (((uint64_t)__float_as_uint(h.t) << 32) | (uint32_t)h.prim) : ~0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t other = __shfl_xor(key, off);
+            key = other < key ? other : key;
+        }
+        if (key == ~0ull) continue;
+        const bool mine = found && key == ((((uint64_t)__float_as_uint(h.t)) << 32) | (uint32_t)h.prim);
+        const uint64_t owner = __ballot(mine);
+        if (lane == __ffsll((unsigned long long)owner) - 1) {
+            const float4 hv = W.hit4[tag];
+            const int32_t hp = W.hit_prim[tag];
+            Hit cur;
+            cur.t = hv.x; cur.prim = hp;
+            if (lex_better(h.t, h.prim, hp >= 0, cur)) {
+                W.hit4[tag] = make_float4(h.t, h.a, h.b, h.g);
+                W.hit_prim[tag] = h.prim;
+            }
+        }
+    }
+}
+
+// Far-pass flavour for a queue of nq rays: 1 = wave union (sorted, dense
+// queues), 2 = per lane, 3 = scan. RT580_FAR_MODE overrides the size rule (A/B only).
+static int far_mode(uint32_t nq) {
+    static int forced = -1;
+    if (forced < 0) {
+        const char* e = getenv("RT580_FAR_MODE");
+        forced = e ? atoi(e) : 0;
+    }
+    if (forced >= 1 && forced <= 3) return forced;
+    return 1;
 }
 
 // Queued tree rays of a BVH trace level (sorted by direction key): the far part
@@ -1013,15 +1148,16 @@ void upload_minstd_table(hipStream_t s) {
 }
 
 // Sort the far queue (W.far_count entries) by direction key; returns its length.
-static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq) {
-    hipError_t e = hipMemcpyAsync(W.far_count_host, W.far_count, 4, hipMemcpyDeviceToHost, s);
+static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
+    hipError_t e = hipMemcpyAsync(W.far_count_host, W.far_count, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
-    nq = *W.far_count_host;
+    nq = W.far_count_host[0];
+    nb = W.far_count_host[1];  // far-origin rays: keyed to sort last
     if (nq == 0) return hipSuccess;
     size_t tmp = W.sort_tmp_bytes;
     return hipcub::DeviceRadixSort::SortPairs(W.sort_tmp, tmp, W.far_keys, W.far_keys_alt, W.far_vals,
-                                              W.far_vals_alt, (int)nq, 0, 20, s);
+                                              W.far_vals_alt, (int)nq, 0, RT_DIR_KEY_BITS, s);
 }
 
 hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
@@ -1047,13 +1183,37 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
             for (uint32_t c0 = 0; c0 < count; c0 += W.far_cap) {
                 const uint32_t c1 = count - c0 > W.far_cap ? c0 + W.far_cap : count;
                 const int grid = grid_for(c1 - c0, 1 << 20);
-                if ((e = hipMemsetAsync(W.far_count, 0, 4, s)) != hipSuccess) return e;
+                if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
                 hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
-                uint32_t nq = 0;
-                if ((e = sort_far_queue(W, s, nq)) != hipSuccess) return e;
+                uint32_t nq = 0, nb = 0;
+                if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
+                if (nb) {
+                    hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W,
+                                       nq - nb, nq, 1, (int)S.bv.n_far, 1);
+                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                    nq -= nb;
+                }
+                if (const char* dump = getenv("RT580_DUMP_FAR")) {  // DIAGNOSTIC: queued rays per level
+                    std::vector<float4> host((size_t)nq * 2);
+                    if (nq) (void)hipMemcpy(host.data(), W.far_rays, (size_t)nq * 32, hipMemcpyDeviceToHost);
+                    if (FILE* f = fopen(dump, "ab")) {
+                        const uint32_t m = nq < 100000u ? nq : 100000u;  // a sample per level
+                        const int hdr[2] = {level, (int)m};
+                        fwrite(hdr, sizeof hdr, 1, f);
+                        fwrite(host.data(), 32, m, f);
+                        fclose(f);
+                    }
+                }
                 if (nq) {
-                    hipLaunchKernelGGL(far_closest_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                    const int fm = far_mode(nq);
+                    if (fm == 1)
+                        hipLaunchKernelGGL(far_closest_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                    else if (fm == 2)
+                        hipLaunchKernelGGL(far_closest_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                    else
+                        hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nq * 64, 16384)), dim3(TB), 0, s, S,
+                                           W, 0u, nq, 1, (int)S.bv.n_far, 0);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                 }
                 hipLaunchKernelGGL((trace_kernel<true, 2>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
@@ -1088,7 +1248,7 @@ hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, c
 size_t far_sort_tmp_bytes(uint32_t cap) {
     size_t bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                             (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, 0, 20);
+                                             (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, 0, RT_DIR_KEY_BITS);
     return bytes;
 }
 
@@ -1114,14 +1274,27 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         const uint64_t chunk = S.bv.has_far ? (uint64_t)W.far_cap : items;
         for (uint64_t b = 0; b < items; b += chunk) {
             const uint64_t e1 = b + chunk < items ? b + chunk : items;
-            if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 4, s)) != hipSuccess) return e;
+            if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
             hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if (!S.bv.has_far) continue;
-            uint32_t nq = 0;
-            if ((e = sort_far_queue(W, s, nq)) != hipSuccess) return e;
+            uint32_t nq = 0, nb = 0;
+            if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
+            if (nb) {
+                hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W,
+                                   nq - nb, nq, 0, (int)S.bv.n_far, 1);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                nq -= nb;
+            }
             if (nq == 0) continue;
-            hipLaunchKernelGGL(far_any_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+            const int fm = far_mode(nq);
+            if (fm == 1)
+                hipLaunchKernelGGL(far_any_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+            else if (fm == 2)
+                hipLaunchKernelGGL(far_any_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+            else
+                hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nq * 64, 16384)), dim3(TB), 0, s, S, W,
+                                   0u, nq, 0, (int)S.bv.n_far, 0);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         return hipSuccess;

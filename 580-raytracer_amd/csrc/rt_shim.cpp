@@ -140,6 +140,8 @@ DevScene dev_scene(const rt_render_params* p) {
     v.far_tris = (const FarTri*)g.far_tris.p;
     v.brute = (const uint32_t*)g.brute.p;
     v.n_brute = (int)g.bvh.brute.size();
+    v.n_far = g.bvh.n_far;
+    v.far_root_min_dhi = g.bvh.far_nodes.empty() ? 0.0f : g.bvh.far_nodes[0].min_dhi;
     v.has_tree = !g.bvh.nodes.empty();
     v.has_far = !g.bvh.far_nodes.empty();
     {   // DIAGNOSTIC (timing ablation only, wrong results): RT580_BVH_DIAG=1 skips the far search
@@ -256,7 +258,7 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     g.call_cap = (uint32_t)ccap;
     // far-hit queue of the BVH AO pass (chunks of at most far_cap AO rays)
     if (g.bvh_ok && !g.bvh.far_nodes.empty() && g.far_cap == 0) {
-        const uint32_t fc = 1u << 24;
+        const uint32_t fc = 1u << 26;  // rays per sorted chunk: more rays, more coherent waves
         if (ensure(g.far_rays, (size_t)fc * 32) || ensure(g.far_keys, (size_t)fc * 4) ||
             ensure(g.far_keys_alt, (size_t)fc * 4) || ensure(g.far_vals, (size_t)fc * 4) ||
             ensure(g.far_vals_alt, (size_t)fc * 4) || ensure(g.far_count, 64) ||
@@ -420,6 +422,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         // the device needs only the arrays; keep the host copy small
         g.bvh.prims = std::vector<rt_prim>();
         g.bvh.ids = std::vector<uint32_t>();
+        g.bvh.n_far = (int)g.bvh.far_tris.size();
         g.bvh.far_tris = std::vector<FarTri>();
     }
     HIP_TRY(hipStreamSynchronize(g.stream));

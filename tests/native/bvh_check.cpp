@@ -79,6 +79,7 @@ int main(int argc, char** argv) {
     V.far_tris = B.far_tris.empty() ? nullptr : B.far_tris.data();
     V.brute = B.brute.data();
     V.n_brute = (int)B.brute.size();
+    V.n_far = (int)B.far_tris.size();
     V.has_tree = !B.nodes.empty();
     V.has_far = !B.far_nodes.empty();
     V.scale = B.scale;
