@@ -75,12 +75,21 @@ TriBounds analyse(const rt_prim& p, double S, double inflate) {
     const double e01 = dist3(p.p0, p.p1), e12 = dist3(p.p1, p.p2), e20 = dist3(p.p2, p.p0);
     const double emin = std::min(e01, std::min(e12, e20)), emax = std::max(e01, std::max(e12, e20));
     const double a0 = angle_at(p.p0, p.p1, p.p2), a1 = angle_at(p.p1, p.p2, p.p0), a2 = angle_at(p.p2, p.p0, p.p1);
-    const double amin = std::min(a0, std::min(a1, a2));
-    if (!(emin > 0) || !(amin > 1e-4) || !std::isfinite(emax)) return r;
-    const double s = std::sin(0.5 * amin);
-    const double kappa = 16.0 + 4.0 / std::sin(amin);
+    if (!(emin > 0) || !(std::min(a0, std::min(a1, a2)) > 1e-6) || !std::isfinite(emax) || !(a0 > 1e-6)) return r;
+    // Signal: a point at in-plane distance D outside the triangle whose closest
+    // triangle point is in an edge's interior is at distance D from that edge's
+    // line; if it is a vertex v (angle a_v), at distance >= D sin(a_v/2) from the
+    // line of one of v's two edges. So the most negative exact sub-area is
+    // <= -G D / 2 with G = min(e_min, min_v min(adjacent edges) sin(a_v/2)).
+    const double g0 = std::min(e01, e20) * std::sin(0.5 * a0);
+    const double g1 = std::min(e01, e12) * std::sin(0.5 * a1);
+    const double g2 = std::min(e12, e20) * std::sin(0.5 * a2);
+    const double G = std::min(emin, std::min(g0, std::min(g1, g2)));
+    // Error: 11.25 u |a||b| for the sub-area arithmetic, plus the misalignment
+    // of the float normal N = normalize(cross(v1 - v0, v2 - v0)) (~3u / sin a0).
+    const double kappa = 16.0 + 4.0 / std::sin(a0);
     const double ep = emax + std::ldexp(S, -10);  // + off-plane height and rounding slack
-    const double a = kappa * kU, b = emin * s;
+    const double a = kappa * kU, b = G;
     const double bb = b - 2 * a * ep;
     const double disc = bb * bb - 4 * a * a * ep * ep;
     if (!(bb > 0) || !(disc > 0)) return r;
@@ -89,7 +98,9 @@ TriBounds analyse(const rt_prim& p, double S, double inflate) {
     // near hit points lie within D_lo of the triangle; the rest of the float
     // error budget is carried by the fat-ray slab test (rt_isect.h)
     r.delta = std::max(std::max(inflate * emin, std::ldexp(S, -20)), 2.0 * r.dlo);
-    r.ok = std::isfinite(r.dhi) && std::isfinite(r.delta);
+    // D_hi must clear the origin distances of rays from inside the scene
+    // (|o| + sqrt3 S), else the triangle is simply tested for every ray
+    r.ok = std::isfinite(r.dhi) && std::isfinite(r.delta) && r.dhi > 8.0 * S;
     return r;
 }
 
@@ -349,6 +360,7 @@ bool build_bvh(const rt_prim* prims, int n, BvhBuild& out) {
             for (const FarTri& t : out.far_tris) ts.push_back(t.dhi);
             std::nth_element(ts.begin(), ts.begin() + ts.size() / 2, ts.end());
             F.t_typ = std::max(ts[ts.size() / 2], 1.0f);
+            out.dhi_median = ts[ts.size() / 2];
         }
         F.build(0, 0, nt, 0);
         out.far_depth = F.depth;

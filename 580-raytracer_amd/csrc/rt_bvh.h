@@ -29,8 +29,8 @@
 //     the triangles' planes (normal boxes + D ranges) that enumerates every
 //     plane the ray crosses beyond T_j, with exact interval padding; those
 //     candidates get the full reference test.
-// Triangles for which the analysis does not give a usable split (slivers,
-// degenerate) and all spheres are tested brute force for every ray.
+// Triangles for which the analysis does not give a usable split (degenerate,
+// or D_hi below 8 S) and all spheres are tested brute force for every ray.
 #pragma once
 #include <stdint.h>
 
@@ -86,6 +86,7 @@ struct BvhBuild {
     int max_leaf = 0;
     int n_tri = 0;
     int n_far = 0;                  // far_tris.size() (kept after the host copy is dropped)
+    float dhi_median = 0.0f;        // typical D_hi (routing of far-origin rays)
     double inflate = 0.0;           // delta_j / e_min(j)
     double build_ms = 0.0;
 };

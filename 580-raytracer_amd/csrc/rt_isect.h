@@ -104,7 +104,7 @@ struct BvhView {
     const uint32_t* brute;      // spheres + unanalysable triangles, ascending
     int n_brute;
     int n_far;                  // far_tris entries
-    float far_root_min_dhi;     // smallest D_hi of the plane tree (root bound)
+    float dhi_median;           // typical D_hi (routing of far-origin rays)
     int has_tree, has_far;
     float scale;                // S
 };

@@ -106,6 +106,8 @@ hipError_t launch_row_counts(const DevScene& S, const DevFrame& F, const DevWork
 hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, const uint64_t* row_base_global,
                        hipStream_t s);
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s);
+// The launcher step that ran last (for error messages).
+const char* launch_where();
 // Temporary storage of the far-queue radix sort for `cap` rays.
 size_t far_sort_tmp_bytes(uint32_t cap);
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s);

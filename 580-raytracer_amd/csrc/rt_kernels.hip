@@ -30,6 +30,7 @@
 #include <stdlib.h>
 
 #include <hipcub/hipcub.hpp>
+#include <cstdarg>
 #include <cstdio>
 #include <vector>
 
@@ -331,12 +332,13 @@ __device__ __forceinline__ void wave_alloc2(uint32_t* counter, bool fa, bool fb,
 #define RT_KEY_BRUTE (1u << 24)  // far-origin rays: brute-force scan, sorted after every direction key
 
 // Rays whose origin is so far out (a child of one of the reference's far hits)
-// that no triangle can be culled (T_root <= 0) or the fat-ray margin covers the
-// scene: the reference's own loop over every primitive (far_scan_kernel) is
-// cheaper than any traversal for them. Routing only; the results are the same.
-__device__ __forceinline__ bool far_origin(const DevScene& S, rv3 o, float root_min_dhi) {
+// that a typical triangle cannot be culled (T <= 0) or the fat-ray margin
+// covers the scene: the reference's own loop over every primitive
+// (far_scan_kernel) is cheaper than any traversal for them. Routing only; the
+// results are the same.
+__device__ __forceinline__ bool far_origin(const DevScene& S, rv3 o) {
     const float oi = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
-    return oi > 64.0f * S.bv.scale || !(far_T(far_ray(S.bv, o), root_min_dhi) > 0.0f);
+    return oi > 64.0f * S.bv.scale || !(far_T(far_ray(S.bv, o), 0.5f * S.bv.dhi_median) > 0.0f);
 }
 __device__ __forceinline__ uint32_t dir_key(rv3 d) {
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
@@ -417,7 +419,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
         h.t = 0; h.prim = 0;
         if (PHASE == 1) {
             const FarNode root = load_far_node(S.bv.far_nodes, 0);
-            const bool brute = active && far_origin(S, o, root.min_dhi);
+            const bool brute = active && far_origin(S, o);
             const bool nh = active && !brute && bvh_closest(S.bv, o, d, h, /*with_far=*/false);
             bool q = false;
             if (active) {
@@ -755,7 +757,7 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
             if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
             o = v3_add(hp, v3_scale(v, 0.2f));
             d = (VARIANT & 128) ? v : v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
-            if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o, S.bv.far_root_min_dhi);
+            if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o);
         }
         const bool hit = (VARIANT & 32) ? (d.x > 2.0f)  // DIAGNOSTIC ablation only
                        : (VARIANT & 512) ? (active && !ao_brute && bvh_any(S.bv, o, d, /*with_far=*/false))
@@ -1147,8 +1149,32 @@ void upload_minstd_table(hipStream_t s) {
     (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
 }
 
+// Which launcher step failed last (error messages of the shim).
+static const char* g_where = "";
+const char* launch_where() { return g_where; }
+#define RT_STEP(what) (g_where = (what))
+
+// RT580_PROGRESS=1: a stderr line per trace level / AO chunk of the BVH path
+// (those already synchronize), so multi-minute frames show progress.
+static void progress(const char* fmt, ...) {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("RT580_PROGRESS");
+        on = e && atoi(e) > 0;
+    }
+    if (!on) return;
+    va_list ap;
+    va_start(ap, fmt);
+    fprintf(stderr, "[rt580] ");
+    vfprintf(stderr, fmt, ap);
+    fprintf(stderr, "\n");
+    fflush(stderr);
+    va_end(ap);
+}
+
 // Sort the far queue (W.far_count entries) by direction key; returns its length.
 static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
+    RT_STEP("far queue count D2H");
     hipError_t e = hipMemcpyAsync(W.far_count_host, W.far_count, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
@@ -1156,11 +1182,13 @@ static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, 
     nb = W.far_count_host[1];  // far-origin rays: keyed to sort last
     if (nq == 0) return hipSuccess;
     size_t tmp = W.sort_tmp_bytes;
+    RT_STEP("far queue radix sort");
     return hipcub::DeviceRadixSort::SortPairs(W.sort_tmp, tmp, W.far_keys, W.far_keys_alt, W.far_vals,
                                               W.far_vals_alt, (int)nq, 0, RT_DIR_KEY_BITS, s);
 }
 
 hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
+    (void)hipGetLastError();  // launch checks below must not see a stale error
     const uint64_t npix = (uint64_t)F.n_rows * F.width;
     hipError_t e = hipMemsetAsync(W.lvl, 0, sizeof(uint32_t) * 2 * LVL_BASE, s);
     if (e != hipSuccess) return e;
@@ -1170,6 +1198,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
             // near phase, sorted far pass, shading; in chunks of the far queue's capacity
             uint32_t count = (uint32_t)npix;
             if (level > 0) {
+                RT_STEP("level count D2H");
                 if ((e = hipMemcpyAsync(W.far_count_host, W.lvl + level, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
                     (e = hipStreamSynchronize(s)) != hipSuccess)
                     return e;
@@ -1184,11 +1213,13 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 const uint32_t c1 = count - c0 > W.far_cap ? c0 + W.far_cap : count;
                 const int grid = grid_for(c1 - c0, 1 << 20);
                 if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
+                RT_STEP("trace near phase");
                 hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 uint32_t nq = 0, nb = 0;
                 if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
                 if (nb) {
+                    RT_STEP("trace brute scan");
                     hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W,
                                        nq - nb, nq, 1, (int)S.bv.n_far, 1);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1206,6 +1237,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                     }
                 }
                 if (nq) {
+                    RT_STEP("trace far pass");
                     const int fm = far_mode(nq);
                     if (fm == 1)
                         hipLaunchKernelGGL(far_closest_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
@@ -1216,8 +1248,10 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                                            W, 0u, nq, 1, (int)S.bv.n_far, 0);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                 }
+                RT_STEP("trace shade phase");
                 hipLaunchKernelGGL((trace_kernel<true, 2>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
+                progress("trace level %d: rays [%u, %u) of %u, far queue %u (brute %u)", level, c0, c1, count, nq + nb, nb);
             }
             continue;
         }
@@ -1262,6 +1296,7 @@ static int ao_variant() {
 }
 
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
+    (void)hipGetLastError();  // launch checks below must not see a stale error
     if (!F.ao_enabled || S.n_ambient == 0 || F.n_rows == 0) return hipSuccess;
     if (S.use_bvh) {
         // chunks of the AO items: near pass + queue, sort the misses by
@@ -1286,6 +1321,8 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 nq -= nb;
             }
+            progress("AO items [%llu, %llu) of %llu: far queue %u (brute %u)", (unsigned long long)b,
+                     (unsigned long long)e1, (unsigned long long)items, nq, nb);
             if (nq == 0) continue;
             const int fm = far_mode(nq);
             if (fm == 1)

@@ -141,7 +141,7 @@ DevScene dev_scene(const rt_render_params* p) {
     v.brute = (const uint32_t*)g.brute.p;
     v.n_brute = (int)g.bvh.brute.size();
     v.n_far = g.bvh.n_far;
-    v.far_root_min_dhi = g.bvh.far_nodes.empty() ? 0.0f : g.bvh.far_nodes[0].min_dhi;
+    v.dhi_median = g.bvh.dhi_median;
     v.has_tree = !g.bvh.nodes.empty();
     v.has_far = !g.bvh.far_nodes.empty();
     {   // DIAGNOSTIC (timing ablation only, wrong results): RT580_BVH_DIAG=1 skips the far search
@@ -279,7 +279,10 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
     const DevScene sc = dev_scene(p);
     g.last_accel = sc.use_bvh != 0;
-    HIP_TRY(launch_trace(sc, f, dev_work(), g.stream));
+    {
+        const hipError_t e = launch_trace(sc, f, dev_work(), g.stream);
+        if (e != hipSuccess) return fail("launch_trace (%s): %s", launch_where(), hipGetErrorString(e));
+    }
     HIP_TRY(launch_row_counts(sc, f, dev_work(), g.stream));
     HIP_TRY(hipEventRecord(g.ev[EV_TRACE], g.stream));
     g.last_rows = n_rows;
@@ -553,15 +556,17 @@ int rt_gpu_last_stats(rt_render_stats* st) {
     if (hipEventElapsedTime(&ms, g.ev[EV_TRACE], g.ev[EV_RANK]) == hipSuccess) st->ms_scan = ms;
     if (hipEventElapsedTime(&ms, g.ev[EV_RANK], g.ev[EV_RESOLVE]) == hipSuccess) st->ms_render = ms;
     if (hipEventElapsedTime(&ms, g.ev[EV_START], g.ev[EV_RESOLVE]) == hipSuccess) st->ms_total = ms;
+    (void)hipGetLastError();  // an unrecorded event must not leave a sticky error for the next launch
     return RT_SUCCESS;
 }
 
 int rt_gpu_profile(int enable) {
     if (!g.inited) return fail("rt_gpu_init not called");
     HIP_TRY(hipStreamSynchronize(g.stream));
+    // keep g.ev on the last profiled frame's events so rt_gpu_last_stats stays valid
+    if (enable || g.prof_frames == 0) g.ev = g.ev_default.data();
     g.profiling = enable != 0;
     g.prof_frames = 0;
-    g.ev = g.ev_default.data();
     return RT_SUCCESS;
 }
 

@@ -46,7 +46,7 @@ WORKLOADS = {
                         "north_star target: 100k-triangle field 1920x1080 depth=4 AO=64"),
     "field100k": ("field100k.json", True, 3840, 2160, 6, 256, (4, 3, 6, 64),
                   "BASELINE config 4: 100k-triangle field 3840x2160 depth=6 AO=256"),
-    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, (2, 1, 8, 4),
+    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, (2, 2, 8, 2),
                 "BASELINE config 5: 1M-triangle field 7680x4320 depth=8 AO=256"),
 }
 
@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     ap.add_argument("--check", action="store_true", help="verify the frame against the golden sha256 (config2)")
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
+    ap.add_argument("--row-sample", type=int, default=1,
+                    help="N=1 only: time rows r = 0 mod K of the frame (rank 0's exact share of a K-way "
+                         "interleaved split; RNG bases from an untimed full-frame count), for huge frames")
     args = ap.parse_args()
     global SCENE, WIDTH, HEIGHT, DEPTH, AO, CPU_SAMPLE, LABEL, SYNTH
     SCENE, SYNTH, WIDTH, HEIGHT, DEPTH, AO, CPU_SAMPLE, LABEL = WORKLOADS[args.workload]
@@ -112,10 +115,23 @@ def main():
     n_sph = len(prims) - n_tri
 
     fbp = ctypes.c_void_p()
-    dist_mod = helpers.rt580_dist() if world > 1 else None
-    backend = dist_mod.GpuRows(rt580, params, torch, device) if world > 1 else None
+    K = max(args.row_sample, 1) if world == 1 else 1
+    dist_mod = helpers.rt580_dist() if (world > 1 or K > 1) else None
+    backend = dist_mod.GpuRows(rt580, params, torch, device) if (world > 1 or K > 1) else None
+    sample_base = None
+    if K > 1:
+        # exact global RNG bases: every row's AO-call count, once, outside the timed region
+        log("row sample 1/%d: full-frame count pass" % K)
+        cnt = backend.count(0, 1)[:HEIGHT].to(torch.int64)
+        base = torch.cumsum(cnt, 0) - cnt
+        n_loc = dist_mod.n_local_rows(HEIGHT, 0, K)
+        sample_base = torch.zeros(dist_mod.n_max_rows(HEIGHT, K), dtype=torch.int64, device=device)
+        sample_base[:n_loc] = base[0::K][:n_loc]
 
     def step():
+        if K > 1:
+            backend.count(0, K)
+            return backend.shade(0, K, sample_base)
         if world == 1:
             rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(fbp)), "rt_gpu_render_device")
             return None
@@ -210,6 +226,9 @@ def main():
                 "rng": "minstd_rand0 (libstdc++ default_random_engine)",
                 "rays_per_frame": rays_frame,
                 "parallelism": "interleaved rows x%d + RCCL all_gather/gather" % world if world > 1 else "1 GPU",
+                "row_sample": ("rows r = 0 mod %d only (the exact pixels of rank 0 in a %d-way interleaved split; "
+                               "RNG bases from a full-frame count outside the timed region); value and "
+                               "rays_per_frame refer to the sample" % (K, K)) if K > 1 else None,
                 "scene_query": "exact BVH + plane tree (rt_bvh.h)" if lib.rt_gpu_accel_active() else
                                "brute force (every primitive per ray, as the reference)",
             },
