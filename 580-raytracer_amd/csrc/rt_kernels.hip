@@ -1118,6 +1118,39 @@ __global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, Dev
     fb[(size_t)p * 3 + 2] = (int16_t)ret.b;
 }
 
+// Exclusive raster-order scan of all ranks' per-row AO calls (one workgroup),
+// written out at this rank's rows (rt_gpu_row_bases).
+__global__ void __launch_bounds__(1024) row_bases_kernel(const int32_t* __restrict__ gathered, int world, int n_max,
+                                                         int height, int rank, uint64_t* __restrict__ out) {
+    __shared__ uint64_t part[1024];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    for (int j = threadIdx.x; j < n_max; j += 1024) out[j] = 0;
+    __syncthreads();
+    for (int b = 0; b < height; b += 1024) {
+        const int y = b + threadIdx.x;
+        const uint64_t v = y < height ? (uint64_t)(uint32_t)gathered[(y % world) * n_max + y / world] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int s = 1; s < 1024; s <<= 1) {
+            const uint64_t add = threadIdx.x >= s ? part[threadIdx.x - s] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (y < height && y % world == rank) out[y / world] = carry + part[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += part[1023];
+        __syncthreads();
+    }
+}
+
+hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* out,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(row_bases_kernel, dim3(1), dim3(1024), 0, s, gathered, world, n_max, height, rank, out);
+    return hipGetLastError();
+}
+
 __global__ void copy_rows_kernel(const int16_t* __restrict__ src, int width, int row_begin, int row_step, int n_rows,
                                  int16_t* __restrict__ dst) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -522,6 +522,16 @@ int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device
     return shade_rows(p, p->row_begin, p->row_step, n_selected_rows(p), row_base_device, fb_device);
 }
 
+int rt_gpu_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* row_base) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (!gathered || !row_base) return fail("rt_gpu_row_bases: NULL buffer");
+    if (world <= 0 || rank < 0 || rank >= world || height < 0 || n_max < (height + world - 1) / world)
+        return fail("rt_gpu_row_bases: bad world/rank/n_max/height");
+    HIP_TRY(hipSetDevice(g.device));
+    HIP_TRY(launch_row_bases(gathered, world, n_max, height, rank, row_base, g.stream));
+    return RT_SUCCESS;
+}
+
 int rt_gpu_set_accel(int mode) {
     if (mode != RT_ACCEL_BRUTE && mode != RT_ACCEL_AUTO) return fail("bad accel mode %d", mode);
     g.accel = mode;

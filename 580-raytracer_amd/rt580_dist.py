@@ -14,6 +14,12 @@ one exchange step is therefore:
 
 Backends: GpuRows (lib580rt.so through the C ABI, device tensors) and, for the
 CPU tests of this logic with gloo, OracleRows in tests/.
+
+render_frame() is the plain one-frame form. DistFrame is the steady-state form
+used by bench.py: persistent buffers, all_gather_into_tensor, the row-base scan
+as one kernel (rt_gpu_row_bases), and a double-buffered asynchronous gather of
+frame N that overlaps frame N+1's kernels (rank 0 de-interleaves frame N after
+frame N+1 is queued; finish() completes the last one).
 """
 import ctypes
 
@@ -46,12 +52,19 @@ class GpuRows:
         self.rt580.check(self.lib.rt_gpu_count_rows(ctypes.byref(self._pc), out.data_ptr()), "rt_gpu_count_rows")
         return out
 
-    def shade(self, rank, world, local_base):
+    def shade(self, rank, world, local_base, out=None):
         t = self.torch
-        fb = t.empty(n_max_rows(self.height, world) * self.width * 3, dtype=t.int16, device=self.device)
+        fb = out if out is not None else \
+            t.empty(n_max_rows(self.height, world) * self.width * 3, dtype=t.int16, device=self.device)
         self.rt580.check(self.lib.rt_gpu_shade_rows(ctypes.byref(self._pc), local_base.data_ptr(), fb.data_ptr()),
                          "rt_gpu_shade_rows")
         return fb
+
+    def row_bases(self, gathered, rank, world, out):
+        """gathered: int32[world * n_max] on the device -> out: int64[n_max] (one kernel)."""
+        self.rt580.check(self.lib.rt_gpu_row_bases(gathered.data_ptr(), world, n_max_rows(self.height, world),
+                                                   self.height, rank, out.data_ptr()), "rt_gpu_row_bases")
+        return out
 
 
 def render_frame(backend, dist, torch, height, width, rank, world, gather=True):
@@ -90,3 +103,61 @@ def render_frame(backend, dist, torch, height, width, rank, world, gather=True):
         return frame.reshape(n_max * world, width, 3)[:height]
     dist.gather(fb_bytes, dst=0)
     return None
+
+
+class DistFrame:
+    """Steady-state multi-rank frames on the GPU backend over RCCL (see module doc)."""
+
+    def __init__(self, backend, dist, torch, height, width, rank, world, device):
+        self.b, self.dist, self.t = backend, dist, torch
+        self.h, self.w, self.rank, self.world = height, width, rank, world
+        self.n_max = n_max_rows(height, world)
+        tile = self.n_max * width * 3
+        self.gathered = torch.empty(world * self.n_max, dtype=torch.int32, device=device)
+        self.base = torch.empty(self.n_max, dtype=torch.int64, device=device)
+        self.fb = [torch.empty(tile, dtype=torch.int16, device=device) for _ in range(2)]
+        self.tiles = [torch.empty(world * tile * 2, dtype=torch.uint8, device=device) for _ in range(2)] \
+            if rank == 0 else None
+        self.frame = torch.empty(self.n_max * world, width, 3, dtype=torch.int16, device=device) if rank == 0 else None
+        self.work = [None, None]
+        self.i = 0
+        self.pending = None  # buffer index whose gather is in flight and not yet de-interleaved
+
+    def _assemble(self, k):
+        if self.work[k] is not None:
+            self.work[k].wait()  # stream-level: the compute stream waits for the collective
+            self.work[k] = None
+        if self.rank == 0:
+            tiles = self.tiles[k].view(self.t.int16).view(self.world, self.n_max, self.w, 3)
+            self.frame.view(self.n_max, self.world, self.w, 3).copy_(tiles.transpose(0, 1))
+
+    def render(self):
+        k = self.i
+        if self.work[k] is not None:  # buffer k's gather (two frames ago) must be done before reuse
+            self._assemble(k)
+            self.pending = None
+        counts = self.b.count(self.rank, self.world)
+        self.dist.all_gather_into_tensor(self.gathered, counts)
+        self.b.row_bases(self.gathered, self.rank, self.world, self.base)
+        fb = self.b.shade(self.rank, self.world, self.base, out=self.fb[k])
+        if self.pending is not None:  # frame N-1: de-interleave now that frame N is queued
+            self._assemble(self.pending)
+        src = fb.view(self.t.uint8)
+        if self.rank == 0:
+            self.work[k] = self.dist.gather(src, gather_list=list(self.tiles[k].chunk(self.world)), dst=0,
+                                            async_op=True)
+        else:
+            self.work[k] = self.dist.gather(src, dst=0, async_op=True)
+        self.pending = k
+        self.i ^= 1
+
+    def finish(self):
+        """Complete the last frame; returns the (H, W, 3) int16 frame on rank 0."""
+        if self.pending is not None:
+            self._assemble(self.pending)
+            self.pending = None
+        for k in range(2):
+            if self.work[k] is not None:
+                self.work[k].wait()
+                self.work[k] = None
+        return self.frame[:self.h] if self.rank == 0 else None

@@ -128,6 +128,11 @@ def main():
         sample_base = torch.zeros(dist_mod.n_max_rows(HEIGHT, K), dtype=torch.int64, device=device)
         sample_base[:n_loc] = base[0::K][:n_loc]
 
+    # steady-state multi-rank frames (RCCL): persistent buffers, async gather
+    # overlapped with the next frame; gloo (rehearsal) uses the plain form
+    dframe = dist_mod.DistFrame(backend, dist, torch, HEIGHT, WIDTH, rank, world, device) \
+        if (world > 1 and args.backend == "nccl") else None
+
     def step():
         if K > 1:
             backend.count(0, K)
@@ -135,7 +140,13 @@ def main():
         if world == 1:
             rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(fbp)), "rt_gpu_render_device")
             return None
+        if dframe is not None:
+            dframe.render()
+            return None
         return dist_mod.render_frame(backend, dist, torch, HEIGHT, WIDTH, rank, world)
+
+    def finish():
+        return dframe.finish() if dframe is not None else None
 
     def barrier():
         if world > 1:
@@ -144,6 +155,8 @@ def main():
     frame = None
     for i in range(max(args.warmup, 1 if args.check else 0)):
         frame = step()
+        if dframe is not None:
+            frame = finish()
         if SYNTH:
             torch.cuda.synchronize()
             log("warmup step %d done" % i)
@@ -166,6 +179,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
+        if i == args.steps - 1:
+            finish()  # the last frame's gather + de-interleave belong to the timed region
         if SYNTH:  # long frames: keep a progress line per step (sync costs microseconds)
             torch.cuda.synchronize()
             if rank == 0:

@@ -171,6 +171,12 @@ int rt_gpu_render_device(const rt_render_params* params, int16_t** fb_device);
 int rt_gpu_count_rows(const rt_render_params* params, uint32_t* row_calls_device);
 int rt_gpu_shade_rows(const rt_render_params* params, const uint64_t* row_base_device,
                       int16_t* fb_device);
+/* Between the two phases: from the all-gathered per-row counts
+ * (gathered_device: int32[world][n_max], rank k's local row j = frame row
+ * k + j*world), the exclusive raster-order scan's values at this rank's rows
+ * -> row_base_device (uint64[n_max], zero padded). One kernel on the shim's stream. */
+int rt_gpu_row_bases(const int32_t* gathered_device, int world, int n_max, int height, int rank,
+                     uint64_t* row_base_device);
 /* Scene-query acceleration. RT_ACCEL_BRUTE tests every primitive per ray, as
  * the reference's IntersectScene does (Raytracer.cpp:473-526); RT_ACCEL_AUTO
  * (default) uses the exact-semantics BVH for triangle scenes larger than one

@@ -157,10 +157,24 @@ class OracleRows:
         assert self.lib.oracle_count_rows(*self.args, rank, world, n_loc, out.ctypes.data) == 0
         return self.torch.from_numpy(out.astype(np.int32))
 
-    def shade(self, rank, world, local_base):
+    def shade(self, rank, world, local_base, out=None):
         d = rt580_dist()
         n_loc, n_max = d.n_local_rows(self.height, rank, world), d.n_max_rows(self.height, world)
         base = np.ascontiguousarray(local_base.numpy().astype(np.uint64))
         fb = np.zeros(n_max * self.width * 3, dtype=np.int16)
         assert self.lib.oracle_shade_rows(*self.args, rank, world, n_loc, base.ctypes.data, fb.ctypes.data) == 0
+        if out is not None:
+            out.copy_(self.torch.from_numpy(fb))
+            return out
         return self.torch.from_numpy(fb)
+
+    def row_bases(self, gathered, rank, world, out):
+        """Same contract as rt_gpu_row_bases (torch on the CPU)."""
+        t = self.torch
+        n_max = rt580_dist().n_max_rows(self.height, world)
+        full = gathered.view(world, n_max).t().reshape(-1)[:self.height].to(t.int64)
+        base = t.cumsum(full, 0) - full
+        out.zero_()
+        mine = base[rank::world]
+        out[:mine.numel()] = mine
+        return out

@@ -117,6 +117,10 @@ def test_multi_rank_split_on_one_gpu(world):
         lb = torch.zeros(n_max, dtype=torch.int64, device=dev)
         mine = base[r::world]
         lb[:mine.numel()] = mine
+        # the one-kernel form used by DistFrame (rt_gpu_row_bases) gives the same bases
+        gathered = torch.stack([c.to(torch.int32) for c in counts]).reshape(-1).contiguous()
+        lb2 = backend.row_bases(gathered, r, world, torch.empty(n_max, dtype=torch.int64, device=dev))
+        assert torch.equal(lb, lb2)
         tiles.append(backend.shade(r, world, lb).view(n_max, w, 3).clone())
     frame = torch.stack(tiles, dim=1).reshape(n_max * world, w, 3)[:h].cpu().numpy()
     rt580.check(lib.rt_gpu_set_stream(lib.rt_gpu_own_stream()), "stream")

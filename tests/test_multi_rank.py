@@ -38,6 +38,34 @@ def _worker(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
+def _worker_steady(rank, world, port, out_path):
+    """DistFrame (bench.py's steady-state path): three frames back to back with the
+    double-buffered asynchronous gather; the last assembled frame must be exact."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scene, w, h, depth, ao = CASE
+        backend = helpers.OracleRows(scene, w, h, depth, ao)
+        df = helpers.rt580_dist().DistFrame(backend, dist, torch, h, w, rank, world, torch.device("cpu"))
+        for _ in range(3):
+            df.render()
+        frame = df.finish()
+        if rank == 0:
+            np.save(out_path, frame.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_steady_state_dist_frame(world, tmp_path):
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_worker_steady, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    scene, w, h, depth, ao = CASE
+    ref, _ = helpers.oracle_render(scene, w, h, depth, ao, True)
+    assert np.array_equal(np.load(out), ref)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_interleaved_rows_match_single_rank(world, tmp_path):
     out = str(tmp_path / "frame.npy")
