@@ -118,9 +118,11 @@ int Raytracer::FlushFrameBufferToPPM(std::string outputName) {
     // Gamma 1/2.2 of c/255 (Raytracer.cpp:816-818). Pixels are clamped to [0,255]
     // (Raycast returns clamp()); a 256-entry table of the same glibc powf
     // expression is the identical mapping.
+    // glibc powf at run time (a volatile pointer: no compile-time folding)
+    float (*volatile pf)(float, float) = ::powf;
     unsigned char lut[256];
     for (int c = 0; c < 256; c++)
-        lut[c] = static_cast<unsigned char>(std::pow(c / 255.0f, 1.0f / 2.2f) * 255.0f);
+        lut[c] = static_cast<unsigned char>(pf(c / 255.0f, 1.0f / 2.2f) * 255.0f);
     outfile << "P6\n" << mWidth << " " << mHeight << "\n255\n";
     std::vector<unsigned char> row((size_t)mWidth * 3);
     for (int y = 0; y < mHeight; y++) {
@@ -130,7 +132,7 @@ int Raytracer::FlushFrameBufferToPPM(std::string outputName) {
             for (int k = 0; k < 3; k++)
                 row[(size_t)x * 3 + k] = (c[k] >= 0 && c[k] <= 255)
                                              ? lut[c[k]]
-                                             : static_cast<unsigned char>(std::pow(c[k] / 255.0f, 1.0f / 2.2f) * 255.0f);
+                                             : static_cast<unsigned char>(pf(c[k] / 255.0f, 1.0f / 2.2f) * 255.0f);
         }
         outfile.write((const char*)row.data(), (std::streamsize)row.size());
     }

@@ -113,6 +113,8 @@ size_t far_sort_tmp_bytes(uint32_t cap);
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s);
 hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* out,
                             hipStream_t s);
+void upload_gamma_lut(const uint8_t* lut, hipStream_t s);
+hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows,
                             int16_t* dst, hipStream_t s);
 

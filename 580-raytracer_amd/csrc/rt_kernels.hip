@@ -1151,6 +1151,31 @@ hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int h
     return hipGetLastError();
 }
 
+static int grid_for(uint64_t items, int cap) {
+    uint64_t b = (items + TB - 1) / TB;
+    if (b < 1) b = 1;
+    return (int)(b < (uint64_t)cap ? b : (uint64_t)cap);
+}
+
+__constant__ uint8_t c_gamma_lut[256];
+
+__global__ void gamma_u8_kernel(const int16_t* __restrict__ fb, uint64_t n, uint8_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int v = fb[i];
+        out[i] = c_gamma_lut[v < 0 ? 0 : (v > 255 ? 255 : v)];
+    }
+}
+
+void upload_gamma_lut(const uint8_t* lut, hipStream_t s) {
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_gamma_lut), lut, 256, 0, hipMemcpyHostToDevice, s);
+}
+
+hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gamma_u8_kernel, dim3(grid_for(n, 8192)), dim3(TB), 0, s, fb, n, out);
+    return hipGetLastError();
+}
+
 __global__ void copy_rows_kernel(const int16_t* __restrict__ src, int width, int row_begin, int row_step, int n_rows,
                                  int16_t* __restrict__ dst) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1161,11 +1186,6 @@ __global__ void copy_rows_kernel(const int16_t* __restrict__ src, int width, int
 }
 
 // ---------------------------------------------------------------- launchers
-static int grid_for(uint64_t items, int cap) {
-    uint64_t b = (items + TB - 1) / TB;
-    if (b < 1) b = 1;
-    return (int)(b < (uint64_t)cap ? b : (uint64_t)cap);
-}
 
 void upload_minstd_table(hipStream_t s) {
     uint32_t pw[32];

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -371,6 +372,13 @@ int rt_gpu_init(int device) {
     HIP_TRY(hipHostMalloc((void**)&g.needed_host, 64, hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&g.far_count_host, 64, hipHostMallocDefault));
     upload_minstd_table(g.stream);
+    {   // FlushFrameBufferToPPM's mapping, with this host's glibc powf (Raytracer.cpp:816-818);
+        // called through a volatile pointer so no compiler constant-folds it
+        float (*volatile pf)(float, float) = ::powf;
+        static uint8_t lut[256];
+        for (int c = 0; c < 256; c++) lut[c] = static_cast<unsigned char>(pf(c / 255.0f, 1.0f / 2.2f) * 255.0f);
+        upload_gamma_lut(lut, g.stream);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(g.stream));
     g.inited = true;
@@ -520,6 +528,14 @@ int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device
     HIP_TRY(hipSetDevice(g.device));
     g.split_ready = false;
     return shade_rows(p, p->row_begin, p->row_step, n_selected_rows(p), row_base_device, fb_device);
+}
+
+int rt_gpu_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (n && (!fb || !out)) return fail("rt_gpu_gamma_u8: NULL buffer");
+    HIP_TRY(hipSetDevice(g.device));
+    HIP_TRY(launch_gamma_u8(fb, n, out, g.stream));
+    return RT_SUCCESS;
 }
 
 int rt_gpu_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* row_base) {

@@ -60,6 +60,11 @@ class GpuRows:
                          "rt_gpu_shade_rows")
         return fb
 
+    def gamma_u8(self, fb, out):
+        """FlushFrameBufferToPPM's pixel mapping on the device (rt_gpu_gamma_u8)."""
+        self.rt580.check(self.lib.rt_gpu_gamma_u8(fb.data_ptr(), fb.numel(), out.data_ptr()), "rt_gpu_gamma_u8")
+        return out
+
     def row_bases(self, gathered, rank, world, out):
         """gathered: int32[world * n_max] on the device -> out: int64[n_max] (one kernel)."""
         self.rt580.check(self.lib.rt_gpu_row_bases(gathered.data_ptr(), world, n_max_rows(self.height, world),
@@ -106,19 +111,25 @@ def render_frame(backend, dist, torch, height, width, rank, world, gather=True):
 
 
 class DistFrame:
-    """Steady-state multi-rank frames on the GPU backend over RCCL (see module doc)."""
+    """Steady-state multi-rank frames on the GPU backend over RCCL (see module doc).
+    u8=True: each rank applies FlushFrameBufferToPPM's gamma mapping to its rows
+    before the gather (3 B/px on the wire instead of 6), and rank 0
+    assembles the PPM body; u8=False gathers the int16 Pixel framebuffer."""
 
-    def __init__(self, backend, dist, torch, height, width, rank, world, device):
+    def __init__(self, backend, dist, torch, height, width, rank, world, device, u8=True):
         self.b, self.dist, self.t = backend, dist, torch
         self.h, self.w, self.rank, self.world = height, width, rank, world
+        self.u8 = u8
         self.n_max = n_max_rows(height, world)
         tile = self.n_max * width * 3
         self.gathered = torch.empty(world * self.n_max, dtype=torch.int32, device=device)
         self.base = torch.empty(self.n_max, dtype=torch.int64, device=device)
         self.fb = [torch.empty(tile, dtype=torch.int16, device=device) for _ in range(2)]
-        self.tiles = [torch.empty(world * tile * 2, dtype=torch.uint8, device=device) for _ in range(2)] \
-            if rank == 0 else None
-        self.frame = torch.empty(self.n_max * world, width, 3, dtype=torch.int16, device=device) if rank == 0 else None
+        self.fb8 = [torch.empty(tile, dtype=torch.uint8, device=device) for _ in range(2)] if u8 else None
+        self.tiles = [torch.empty(world * tile * (1 if u8 else 2), dtype=torch.uint8, device=device)
+                      for _ in range(2)] if rank == 0 else None
+        self.frame = torch.empty(self.n_max * world, width, 3, dtype=torch.uint8 if u8 else torch.int16,
+                                 device=device) if rank == 0 else None
         self.work = [None, None]
         self.i = 0
         self.pending = None  # buffer index whose gather is in flight and not yet de-interleaved
@@ -128,7 +139,8 @@ class DistFrame:
             self.work[k].wait()  # stream-level: the compute stream waits for the collective
             self.work[k] = None
         if self.rank == 0:
-            tiles = self.tiles[k].view(self.t.int16).view(self.world, self.n_max, self.w, 3)
+            tiles = (self.tiles[k] if self.u8 else self.tiles[k].view(self.t.int16)).view(
+                self.world, self.n_max, self.w, 3)
             self.frame.view(self.n_max, self.world, self.w, 3).copy_(tiles.transpose(0, 1))
 
     def render(self):
@@ -142,7 +154,7 @@ class DistFrame:
         fb = self.b.shade(self.rank, self.world, self.base, out=self.fb[k])
         if self.pending is not None:  # frame N-1: de-interleave now that frame N is queued
             self._assemble(self.pending)
-        src = fb.view(self.t.uint8)
+        src = self.b.gamma_u8(fb, self.fb8[k]) if self.u8 else fb.view(self.t.uint8)
         if self.rank == 0:
             self.work[k] = self.dist.gather(src, gather_list=list(self.tiles[k].chunk(self.world)), dst=0,
                                             async_op=True)
@@ -152,7 +164,8 @@ class DistFrame:
         self.i ^= 1
 
     def finish(self):
-        """Complete the last frame; returns the (H, W, 3) int16 frame on rank 0."""
+        """Complete the last frame; returns the (H, W, 3) frame on rank 0 (uint8
+        PPM pixels with u8=True, else the int16 Pixel framebuffer)."""
         if self.pending is not None:
             self._assemble(self.pending)
             self.pending = None

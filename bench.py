@@ -164,15 +164,19 @@ def main():
     check_ok = None
     if args.check and rank == 0:
         # the frame of the (last warm-up) step vs the reference's config-2 hash
+        import numpy as np
         if world == 1:
-            import numpy as np
             host = np.zeros(WIDTH * HEIGHT * 3, dtype=np.int16)
             rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
             frame_np = host.reshape(HEIGHT, WIDTH, 3)
         else:
             frame_np = frame.cpu().numpy()
         want = next(e for e in helpers.golden_entries(False) if e["name"] == "config2_1080p_d4_ao64")["sha256"]
-        check_ok = helpers.sha256(rt580.ppm_bytes(frame_np)) == want
+        if frame_np.dtype == np.uint8:  # DistFrame(u8=True): already the PPM body
+            ppm = b"P6\n%d %d\n255\n" % (WIDTH, HEIGHT) + frame_np.tobytes()
+        else:
+            ppm = rt580.ppm_bytes(frame_np)
+        check_ok = helpers.sha256(ppm) == want
     rt580.check(lib.rt_gpu_profile(1), "rt_gpu_profile")
     barrier()
     torch.cuda.synchronize()

@@ -177,6 +177,12 @@ int rt_gpu_shade_rows(const rt_render_params* params, const uint64_t* row_base_d
  * -> row_base_device (uint64[n_max], zero padded). One kernel on the shim's stream. */
 int rt_gpu_row_bases(const int32_t* gathered_device, int world, int n_max, int height, int rank,
                      uint64_t* row_base_device);
+/* FlushFrameBufferToPPM's pixel mapping on the device (Raytracer.cpp:812-818):
+ * (unsigned char)(powf(c / 255.0f, 1.0f / 2.2f) * 255.0f) per int16 channel,
+ * through a 256-entry table built with the host's glibc powf (frame values are
+ * clamped to [0, 255] by Raycast). n_values int16 -> n_values bytes = the PPM
+ * body; used before the multi-GPU gather (half the bytes). */
+int rt_gpu_gamma_u8(const int16_t* fb_device, uint64_t n_values, uint8_t* out_device);
 /* Scene-query acceleration. RT_ACCEL_BRUTE tests every primitive per ray, as
  * the reference's IntersectScene does (Raytracer.cpp:473-526); RT_ACCEL_AUTO
  * (default) uses the exact-semantics BVH for triangle scenes larger than one

@@ -168,6 +168,12 @@ class OracleRows:
             return out
         return self.torch.from_numpy(fb)
 
+    def gamma_u8(self, fb, out):
+        """Same contract as rt_gpu_gamma_u8 (the glibc-powf table on the CPU)."""
+        lut = self.torch.from_numpy(rt580().gamma_lut().astype(np.uint8))
+        out.copy_(lut[fb.to(self.torch.int64).clamp(0, 255)])
+        return out
+
     def row_bases(self, gathered, rank, world, out):
         """Same contract as rt_gpu_row_bases (torch on the CPU)."""
         t = self.torch

@@ -151,3 +151,28 @@ def test_bvh_equals_brute_force(scene, w, h, depth, ao):
     assert lib.rt_gpu_accel_active() == 1
     assert np.array_equal(fb_b, fb_v), "%d pixels differ" % int((fb_b != fb_v).any(axis=2).sum())
     assert st_b["rays_total"] == st_v["rays_total"]
+
+
+def test_gamma_u8_on_device_matches_ppm_writer():
+    """rt_gpu_gamma_u8 (FlushFrameBufferToPPM's mapping before the multi-GPU
+    gather) == the glibc-powf table of the host writer, over every channel value
+    and on a rendered frame."""
+    import torch
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    assert lib.rt_gpu_init(0) == 0
+    dev = torch.device("cuda", 0)
+    assert lib.rt_gpu_set_stream(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)) == 0
+    vals = torch.arange(256, dtype=torch.int16, device=dev)
+    out = torch.empty(256, dtype=torch.uint8, device=dev)
+    assert lib.rt_gpu_gamma_u8(vals.data_ptr(), 256, out.data_ptr()) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), rt580.gamma_lut())
+    fb, _ = render_gpu("simpleSphereScene.json", 64, 48, 2, 8, True)
+    t = torch.from_numpy(np.ascontiguousarray(fb)).to(dev)
+    o = torch.empty(t.numel(), dtype=torch.uint8, device=dev)
+    assert lib.rt_gpu_set_stream(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)) == 0
+    assert lib.rt_gpu_gamma_u8(t.data_ptr(), t.numel(), o.data_ptr()) == 0
+    torch.cuda.synchronize()
+    assert o.cpu().numpy().tobytes() == rt580.ppm_bytes(fb).split(b"\n", 3)[3]
+    lib.rt_gpu_set_stream(lib.rt_gpu_own_stream())

@@ -38,7 +38,7 @@ def _worker(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
-def _worker_steady(rank, world, port, out_path):
+def _worker_steady(rank, world, port, out_path, u8):
     """DistFrame (bench.py's steady-state path): three frames back to back with the
     double-buffered asynchronous gather; the last assembled frame must be exact."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -47,7 +47,7 @@ def _worker_steady(rank, world, port, out_path):
     try:
         scene, w, h, depth, ao = CASE
         backend = helpers.OracleRows(scene, w, h, depth, ao)
-        df = helpers.rt580_dist().DistFrame(backend, dist, torch, h, w, rank, world, torch.device("cpu"))
+        df = helpers.rt580_dist().DistFrame(backend, dist, torch, h, w, rank, world, torch.device("cpu"), u8=u8)
         for _ in range(3):
             df.render()
         frame = df.finish()
@@ -57,13 +57,18 @@ def _worker_steady(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_steady_state_dist_frame(world, tmp_path):
+@pytest.mark.parametrize("world,u8", [(2, False), (3, False), (2, True), (3, True)])
+def test_steady_state_dist_frame(world, u8, tmp_path):
     out = str(tmp_path / "frame.npy")
-    mp.start_processes(_worker_steady, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker_steady, args=(world, _free_port(), out, u8), nprocs=world, join=True,
+                       start_method="spawn")
     scene, w, h, depth, ao = CASE
     ref, _ = helpers.oracle_render(scene, w, h, depth, ao, True)
-    assert np.array_equal(np.load(out), ref)
+    got = np.load(out)
+    if u8:  # the PPM body the reference writes
+        assert got.tobytes() == helpers.rt580().ppm_bytes(ref).split(b"\n", 3)[3]
+    else:
+        assert np.array_equal(got, ref)
 
 
 @pytest.mark.parametrize("world", [2, 3])
