@@ -70,6 +70,10 @@ RTM_HD bool sph_test(const rt_prim& P, rv3 o, rv3 d, float& t) {
     rv3 oc = v3_sub(o, ld3(P.p0));
     float b = 2.0f * v3_dot(d, oc);
     float c = v3_dot(oc, oc) - P.d;
+    // Origin outside (c >= 0) and moving away (b > 0): disc <= RN(b*b), so
+    // sqrtf(disc) <= b (tests/native/eps_check.cpp) and t0, t1 <= 0 -- the
+    // reference rejects, decided here without the square root.
+    if (b > 0.0f && c >= 0.0f && b < 0x1p60f) return false;
     float disc = (b * b) - (4.0f * c);
     if (rt_lt_eps(disc)) return false;
     float sq = sqrtf(disc);

@@ -95,6 +95,11 @@ struct DevWork {
     // far phases of a BVH trace level: (t, alpha, beta, gamma), prim (-1: none)
     float4* hit4;          // [node_cap]
     int32_t* hit_prim;     // [node_cap]
+    // AO samples whose fast sincos rounding test failed (rt_libm.h), recomputed
+    // exactly by ao_fix_kernel: item ids, count (may exceed the capacity)
+    uint64_t* aofix_items; // [aofix_cap]
+    uint32_t* aofix_count; // [1]
+    uint32_t aofix_cap;
 };
 
 void upload_minstd_table(hipStream_t s);
@@ -115,6 +120,7 @@ hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int h
                             hipStream_t s);
 void upload_gamma_lut(const uint8_t* lut, hipStream_t s);
 hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
+hipError_t launch_math_selftest(uint64_t seed, uint64_t n, unsigned long long* bad, hipStream_t s);
 hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows,
                             int16_t* dst, hipStream_t s);
 

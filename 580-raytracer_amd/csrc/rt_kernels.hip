@@ -679,12 +679,33 @@ __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWor
 }
 
 // ---------------------------------------------------------------- AO
+// The two draws of sample s of the AO call whose first draw's RNG position is
+// rbase (minstd state / mt19937 call index): z's, then the angle's.
+__device__ __forceinline__ void ao_draws(const DevFrame& F, const DevWork& W, uint64_t rbase, uint32_t s, float& u0,
+                                         float& u1) {
+    if (F.rng_engine == RT_RNG_MINSTD_RAND0) {
+        uint32_t st = mersenne31_mul((uint32_t)rbase, c_minstd_j1[s]);
+        u0 = canon_minstd(st);
+        st = mersenne31_mul(st, 16807u);
+        u1 = canon_minstd(st);
+    } else {
+        const uint64_t k = rbase * 2ull * (uint64_t)F.ao_samples + 2ull * s;
+        u0 = canon_mt(W.mt_stream[k]);
+        u1 = canon_mt(W.mt_stream[k + 1]);
+    }
+}
+
 // CalculateAmbientOcclusion (Raytracer.cpp:315-330) + RandomInHemisphere (:283-292)
 // + RandomUnitVector (:269-281): one lane per (call, sample).
 // VARIANT bits (A/B switches, results identical): 1 = sincos table in LDS,
 // 2 = scalar per-call data (readfirstlane), 4 = sign-decided triangle rejects,
 // 8 = scalar (wave-uniform) scene loop, 16 = 8-waves/SIMD register cap,
-// 512 = exact BVH queries (triangle scenes; rt_isect.h).
+// 512 = exact BVH queries (triangle scenes; rt_isect.h), 1024 = polynomial
+// sincos with exact glibc fallback (rt_ao_dir_xy), 2048 = range-restricted
+// sqrt/division sequences for the unit vectors (v3_normalize_unit), 4096 = with
+// 1024: samples whose fast rounding test fails are queued (W.aofix_*) for
+// ao_fix_kernel instead of running glibc's sincos inline (keeps the rarely
+// taken fallback's registers out of the hot loop).
 // AO items [item_begin, item_end) (item = call * N + sample).
 template <int VARIANT>
 __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, const DevWork& W,
@@ -706,7 +727,7 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
     const bool resident = (VARIANT & (8 | 512)) ? true : stage_resident(S, tile);
     for (uint64_t b0 = item_begin + (uint64_t)blockIdx.x * TB; b0 < items; b0 += (uint64_t)gridDim.x * TB) {
         const uint64_t item = b0 + threadIdx.x;
-        const bool active = item < items;
+        bool active = item < items;
         uint64_t c = 0;
         uint32_t s = 0;
         if (active) {
@@ -715,6 +736,7 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
         }
         rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
         bool ao_brute = false;
+        bool fix = false;  // VARIANT & 4096: this sample goes to ao_fix_kernel
         if (active) {
             // With N a multiple of 64 a wave serves one call: keep its data scalar.
             uint32_t cc = (uint32_t)c;
@@ -735,29 +757,55 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                         __builtin_amdgcn_readfirstlane((uint32_t)rbase);
             }
             float u0, u1;
-            if (F.rng_engine == RT_RNG_MINSTD_RAND0) {
-                uint32_t st = mersenne31_mul((uint32_t)rbase, c_minstd_j1[s]);
-                u0 = canon_minstd(st);
-                st = mersenne31_mul(st, 16807u);
-                u1 = canon_minstd(st);
-            } else {
-                const uint64_t k = rbase * 2ull * (uint64_t)N + 2ull * s;
-                u0 = canon_mt(W.mt_stream[k]);
-                u1 = canon_mt(W.mt_stream[k + 1]);
-            }
+            ao_draws(F, W, rbase, s, u0, u1);
             // uniform_real_distribution<float>: canonical * (b - a) + a
             const float z = u0 * (1.0f - (-1.0f)) + (-1.0f);
             const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
-            const float r = sqrtf(1 - z * z);
-            double sa, ca;
-            if (VARIANT & 64) { sa = ang; ca = z; }  // DIAGNOSTIC ablation only (wrong output)
-            else rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
-            rv3 v = v3((float)((double)r * ca), (float)((double)r * sa), z);
-            if (!(VARIANT & 128)) v = v3_normalize(v);
+            // Ranges for the 2048 sequences (rt_math.h): z is 0 or a multiple of
+            // 2^-30 in [-1, 1), so 1 - z*z (float) is +0 or >= 2^-24 and r is 0 or
+            // >= 2^-12; |cos|, |sin| of a float angle in [0, 2pi) are 0 or > 2^-27,
+            // so v's components are 0 or in [2^-39, 1] and |v| ~ 1 (also after the
+            // first normalize).
+            const float r = (VARIANT & 2048) ? rt_sqrt_nr(1 - z * z) : sqrtf(1 - z * z);
+            rv3 v;
+            if (VARIANT & 4096) {
+                double sa, ca;
+                rt_fast_sincos((double)ang, &sa, &ca);
+                const double X = (double)r * ca, Y = (double)r * sa;
+                const float fx = (float)X, fy = (float)Y;
+                fix = !(rt_f32_round_safe(X, fx) && rt_f32_round_safe(Y, fy));
+                v = v3(fx, fy, z);
+            } else if (VARIANT & 1024) {
+                float vx, vy;
+                rt_ao_dir_xy(rt_dev::rt_sincostab, r, ang, &vx, &vy);
+                v = v3(vx, vy, z);
+            } else {
+                double sa, ca;
+                if (VARIANT & 64) { sa = ang; ca = z; }  // DIAGNOSTIC ablation only (wrong output)
+                else rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
+                v = v3((float)((double)r * ca), (float)((double)r * sa), z);
+            }
+            if (!(VARIANT & 128)) v = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
             if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
             o = v3_add(hp, v3_scale(v, 0.2f));
-            d = (VARIANT & 128) ? v : v3_normalize(v);  // Ray constructor (Raytracer.h:431-433)
+            // Ray constructor (Raytracer.h:431-433)
+            d = (VARIANT & 128) ? v : ((VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v));
             if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o);
+        }
+        if (VARIANT & 4096) {
+            const uint64_t fm = __ballot(fix);
+            if (fm) {
+                const int leader = __ffsll((unsigned long long)fm) - 1;
+                uint32_t fb = 0;
+                if ((threadIdx.x & 63) == leader) fb = atomicAdd(W.aofix_count, (uint32_t)__popcll(fm));
+                fb = __shfl(fb, leader);
+                if (fix) {
+                    const uint32_t slot = fb + (uint32_t)__popcll(fm & lanemask_lt());
+                    if (slot < W.aofix_cap) W.aofix_items[slot] = item;
+                    active = false;
+                    ao_brute = false;
+                }
+            }
         }
         const bool hit = (VARIANT & 32) ? (d.x > 2.0f)  // DIAGNOSTIC ablation only
                        : (VARIANT & 512) ? (active && !ao_brute && bvh_any(S.bv, o, d, /*with_far=*/false))
@@ -797,9 +845,73 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
     ao_body<VARIANT>(S, F, W);
 }
 
+// ---------------------------------------------------------------- AO fix-up
+// Samples of ao_body<... | 4096> whose fast rounding test failed (rt_libm.h
+// rt_f32_round_safe; ~1e-5 of samples): the exact sample with glibc's sincos,
+// then the same scene query as the main pass (BVH scenes: near + far search, or
+// the reference's loop for far origins), counted into the call's occlusion.
+__device__ bool ao_exact_sample(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t item,
+                                uint32_t& call) {
+    const uint32_t N = (uint32_t)F.ao_samples;
+    const uint64_t c = item / N;
+    const uint32_t s = (uint32_t)(item - c * N);
+    call = (uint32_t)c;
+    const NodeRec& nd = W.nodes[W.call_node[c]];
+    const rv3 hp = ld3(nd.hp), n = ld3(nd.n);
+    float u0, u1;
+    ao_draws(F, W, W.call_rng[c], s, u0, u1);
+    const float z = u0 * (1.0f - (-1.0f)) + (-1.0f);
+    const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
+    const float r = sqrtf(1 - z * z);
+    double sa, ca;
+    rt_glibc_sincos_simd_t(rt_dev::rt_sincostab, (double)ang, &sa, &ca);
+    rv3 v = v3_normalize(v3((float)((double)r * ca), (float)((double)r * sa), z));
+    if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
+    const rv3 o = v3_add(hp, v3_scale(v, 0.2f));
+    const rv3 d = v3_normalize(v);
+    if (S.use_bvh && !(S.bv.has_far && far_origin(S, o))) return bvh_any(S.bv, o, d, /*with_far=*/true);
+    for (int j = 0; j < S.n_prims; j++)
+        if (prim_test_any(S.prims[j], o, d)) return true;
+    return false;
+}
+
+// The queued items, unless the queue overflowed.
+__global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevWork W) {
+    const uint32_t n = *W.aofix_count;
+    if (n > W.aofix_cap) return;
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
+        uint32_t call;
+        if (ao_exact_sample(S, F, W, W.aofix_items[i], call)) atomicAdd(&W.occ[call], 1u);
+    }
+}
+
+// Overflow (more failing samples than queue slots): every item of [b, e) is
+// re-tested and the failing ones recomputed; the queue is ignored.
+__global__ void __launch_bounds__(TB) ao_fixall_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
+    if (*W.aofix_count <= W.aofix_cap) return;
+    const uint64_t items_all = W.totals[0] * (uint64_t)F.ao_samples;
+    if (e > items_all) e = items_all;
+    const uint32_t N = (uint32_t)F.ao_samples;
+    for (uint64_t item = b + (uint64_t)blockIdx.x * TB + threadIdx.x; item < e; item += (uint64_t)gridDim.x * TB) {
+        const uint64_t c = item / N;
+        const uint32_t s = (uint32_t)(item - c * N);
+        float u0, u1;
+        ao_draws(F, W, W.call_rng[c], s, u0, u1);
+        const float z = u0 * (1.0f - (-1.0f)) + (-1.0f);
+        const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
+        const float r = rt_sqrt_nr(1 - z * z);
+        double sa, ca;
+        rt_fast_sincos((double)ang, &sa, &ca);
+        const double X = (double)r * ca, Y = (double)r * sa;
+        if (rt_f32_round_safe(X, (float)X) && rt_f32_round_safe(Y, (float)Y)) continue;
+        uint32_t call;
+        if (ao_exact_sample(S, F, W, item, call)) atomicAdd(&W.occ[call], 1u);
+    }
+}
+
 // BVH scenes: near any-hit of AO items [b, e); misses are queued (far pass below).
 __global__ void __launch_bounds__(TB) ao_near_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
-    ao_body<513>(S, F, W, b, e);
+    ao_body<512 | 1024 | 2048 | 4096>(S, F, W, b, e);
 }
 
 // ---------------------------------------------------------------- far-hit pass
@@ -1176,6 +1288,73 @@ hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStrea
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- math self-test
+// The device-only fast sequences against the plain operations they replace:
+//  [0] rt_sqrt_nr vs sqrtf over EVERY float in [2^-96, 2^126] and +0
+//  [1] rt_div_nr vs '/' for n random pairs (|num| in [2^-60, 4] or +-0, den in [0.5, 2])
+//  [2] v3_normalize_unit vs v3_normalize for n random vectors (|v| in ~[0.5, 2])
+//  [3] rt_ao_dir_xy vs glibc sincos (rt_glibc_sincos_simd_t) for n random AO samples
+__device__ __forceinline__ uint64_t st_mix(uint64_t x) {  // splitmix64
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+__device__ __forceinline__ float st_float(uint64_t r, int emin, int emax) {  // random sign/exponent/mantissa
+    const int e = emin + (int)((r >> 24) % (uint64_t)(emax - emin + 1));
+    const uint32_t bits = ((uint32_t)(e + 127) << 23) | (uint32_t)(r & 0x7fffffu) | ((uint32_t)(r >> 63) << 31);
+    return __uint_as_float(bits);
+}
+__global__ void math_selftest_kernel(uint64_t seed, uint64_t n, unsigned long long* bad) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lo = __float_as_uint(0x1p-96f), hi = __float_as_uint(0x1p126f);
+    unsigned long long b[4] = {0, 0, 0, 0};
+    for (uint64_t u = i0; u <= (uint64_t)(hi - lo) + 1; u += stride) {
+        const float x = u == (uint64_t)(hi - lo) + 1 ? 0.0f : __uint_as_float(lo + (uint32_t)u);
+        if (__float_as_uint(rt_sqrt_nr(x)) != __float_as_uint(sqrtf(x))) b[0]++;
+    }
+    for (uint64_t i = i0; i < n; i += stride) {
+        const uint64_t r0 = st_mix(seed ^ (i * 4)), r1 = st_mix(seed ^ (i * 4 + 1)), r2 = st_mix(seed ^ (i * 4 + 2));
+        const uint64_t r3 = st_mix(seed ^ (i * 4 + 3));
+        // [1] division
+        float num = st_float(r0, -60, 1);
+        if ((r0 & 0xff00000000ull) == 0) num = (r0 & 1) ? -0.0f : 0.0f;
+        const float den = fabsf(st_float(r1, -1, 0));
+        const float y0 = __builtin_amdgcn_rcpf(den);
+        const float y = __builtin_fmaf(__builtin_fmaf(-den, y0, 1.0f), y0, y0);
+        if (__float_as_uint(rt_div_nr(num, den, y)) != __float_as_uint(num / den)) b[1]++;
+        // [2] normalize: components of a vector of length ~[0.5, 2], some exact zeros
+        rv3 v = v3(st_float(r1, -30, 0), st_float(r2, -30, 0), st_float(r3, -30, 0));
+        const float sc = 0.5f + (float)(r0 & 0xffff) * (1.5f / 65536.0f);
+        v = v3_scale(v3_normalize(v), sc);
+        if ((r3 & 0xf) == 0) v.x = 0.0f;
+        if ((r3 & 0xf0) == 0) v.y = -0.0f;
+        const rv3 a = v3_normalize_unit(v), e = v3_normalize(v);
+        if (__float_as_uint(a.x) != __float_as_uint(e.x) || __float_as_uint(a.y) != __float_as_uint(e.y) ||
+            __float_as_uint(a.z) != __float_as_uint(e.z)) b[2]++;
+        // [3] AO direction from the sampler's canonical floats (Raytracer.cpp:270-278)
+        const float u0 = canon_minstd(1u + (uint32_t)(r2 % 2147483646u));
+        const float u1 = canon_minstd(1u + (uint32_t)(r3 % 2147483646u));
+        const float z = u0 * (1.0f - (-1.0f)) + (-1.0f);
+        const float ang = u1 * ((float)(2 * 3.14159265) - 0.0f) + 0.0f;
+        const float rr = sqrtf(1 - z * z);
+        float fx, fy;
+        rt_ao_dir_xy(rt_dev::rt_sincostab, rr, ang, &fx, &fy);
+        double sa, ca;
+        rt_glibc_sincos_simd_t(rt_dev::rt_sincostab, (double)ang, &sa, &ca);
+        if (__float_as_uint(fx) != __float_as_uint((float)((double)rr * ca)) ||
+            __float_as_uint(fy) != __float_as_uint((float)((double)rr * sa))) b[3]++;
+    }
+    for (int k = 0; k < 4; k++)
+        if (b[k]) atomicAdd(bad + k, b[k]);
+}
+
+hipError_t launch_math_selftest(uint64_t seed, uint64_t n, unsigned long long* bad, hipStream_t s) {
+    hipLaunchKernelGGL(math_selftest_kernel, dim3(16384), dim3(TB), 0, s, seed, n, bad);
+    return hipGetLastError();
+}
+
 __global__ void copy_rows_kernel(const int16_t* __restrict__ src, int width, int row_begin, int row_step, int n_rows,
                                  int16_t* __restrict__ dst) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1343,10 +1522,14 @@ static int ao_variant() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_AO_VARIANT");
-        v = e ? (atoi(e) & 255) : 25;  // measured best: LDS sincos table + scalar scene + 8 waves/SIMD
+        v = e ? atoi(e) : (8 | 16 | 1024 | 2048 | 4096);  // scalar scene, 8 waves/SIMD, fast sincos/normalize
     }
     return v;
 }
+
+hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t b, uint64_t e,
+                         hipStream_t s);
+hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v);
 
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     (void)hipGetLastError();  // launch checks below must not see a stale error
@@ -1363,8 +1546,10 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         for (uint64_t b = 0; b < items; b += chunk) {
             const uint64_t e1 = b + chunk < items ? b + chunk : items;
             if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(W.aofix_count, 0, 4, s)) != hipSuccess) return e;
             hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = launch_ao_fix(S, F, W, b, e1, s)) != hipSuccess) return e;
             if (!S.bv.has_far) continue;
             uint32_t nq = 0, nb = 0;
             if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
@@ -1390,10 +1575,31 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         return hipSuccess;
     }
     const int v = ao_variant();
+    if (v & 4096) {
+        const hipError_t e = hipMemsetAsync(W.aofix_count, 0, 4, s);
+        if (e != hipSuccess) return e;
+    }
+    const hipError_t e = launch_ao_small(S, F, W, s, v);
+    if (e != hipSuccess || !(v & 4096)) return e;
+    return launch_ao_fix(S, F, W, 0, ~0ull, s);
+}
+
+// Exact recompute of the samples the fast pass queued (or, on queue overflow,
+// of every failing sample of items [b, e)); both kernels exit at once when
+// they have nothing to do.
+hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t b, uint64_t e,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(ao_fix_kernel, dim3(64), dim3(TB), 0, s, S, F, W);
+    hipLaunchKernelGGL(ao_fixall_kernel, dim3(8192), dim3(TB), 0, s, S, F, W, b, e);
+    return hipGetLastError();
+}
+
+hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v) {
     if (v & 16) {
-        switch (v & 15) {
+        switch (v & ~16) {
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
-            RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8)
+            RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8) RT_AO_CASE(1032) RT_AO_CASE(2056) RT_AO_CASE(3080)
+            RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;
         }
@@ -1403,6 +1609,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         switch (v) {
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
             RT_AO_CASE(41) RT_AO_CASE(73) RT_AO_CASE(137) RT_AO_CASE(105) RT_AO_CASE(233)
+            RT_AO_CASE(1032) RT_AO_CASE(3080) RT_AO_CASE(3084) RT_AO_CASE(7176)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;
         }

@@ -320,3 +320,72 @@ RT_HD void rt_glibc_sincos(double x, double* sinx, double* cosx) {
     // inf/nan -> x/x (NaN); huge finite arguments are outside the path's domain
     *sinx = *cosx = (x - x) / (x - x);
 }
+
+// ---------------------------------------------------------------------------
+// AO hemisphere direction, x = (float)((double)r * cos(a)), y = (float)((double)r * sin(a))
+// (RandomUnitVector, Raytracer.cpp:277-278), fast path with an exact fallback.
+//
+// rt_fast_sincos: Cody-Waite reduction by pi/2 (k <= 4) and Taylor polynomials
+// (sin to x^13, cos to x^14; truncation < 2e-15 on |x| <= pi/4), Horner with
+// fma. Its distance from glibc's sincos is at most RT_AO_SC_ERR for every float
+// angle in [0, 2*pi) (exhaustive: tests/native/libm_check.cpp "aodir").
+//
+// Only the float rounding of r*cos(a) reaches the output. With r <= 1 and
+// E = RT_AO_SC_ERR, the reference's double product X_g and ours X_f differ by at
+// most B = E + 2^-53 (one half-ulp of each product). If X_f lies farther than B
+// from every float rounding boundary around f = (float)X_f, the reference rounds
+// to the same f. Otherwise (rare: |r cos a| tiny) the lane takes glibc's exact
+// sincos (rt_glibc_sincos_simd_t).
+// ---------------------------------------------------------------------------
+#define RT_AO_SC_ERR 0x1p-44
+
+RT_HD void rt_fast_sincos(double a, double* sinx, double* cosx) {
+    const double kd = rint(a * 0x1.45f306dc9c883p-1);          // round(a * 2/pi)
+    double x = fma(-kd, 0x1.921fb54442d18p+0, a);               // a - k*pi/2 (head, one rounding)
+    x = fma(-kd, 0x1.1a62633145c07p-54, x);                     // - k*(pi/2 tail)
+    const double x2 = x * x;
+    double ps = 0x1.6124613a86d09p-33;                          //  1/13!
+    ps = fma(ps, x2, -0x1.ae64567f544e4p-26);                   // -1/11!
+    ps = fma(ps, x2, 0x1.71de3a556c734p-19);                    //  1/9!
+    ps = fma(ps, x2, -0x1.a01a01a01a01ap-13);                   // -1/7!
+    ps = fma(ps, x2, 0x1.1111111111111p-7);                     //  1/5!
+    ps = fma(ps, x2, -0x1.5555555555555p-3);                    // -1/3!
+    const double s = fma(x * x2, ps, x);
+    double pc = 0x1.93974a8c07c9dp-37;                          //  1/14!
+    pc = fma(pc, x2, -0x1.1eed8eff8d898p-29);                   // -1/12!
+    pc = fma(pc, x2, 0x1.27e4fb7789f5cp-22);                    //  1/10!
+    pc = fma(pc, x2, -0x1.a01a01a01a01ap-16);                   // -1/8!
+    pc = fma(pc, x2, 0x1.6c16c16c16c17p-10);                    //  1/6!
+    pc = fma(pc, x2, -0x1.5555555555555p-5);                    // -1/4!
+    pc = fma(pc, x2, 0.5);
+    const double c = fma(-x2, pc, 1.0);                         // 1 - x^2/2 + x^4/4! - ...
+    const int q = (int)kd & 3;
+    const double sv = (q & 1) ? c : s, cv = (q & 1) ? s : c;
+    *sinx = (q & 2) ? -sv : sv;
+    *cosx = ((q + 1) & 2) ? -cv : cv;
+}
+
+// Would RN_float(X_g) equal f = RN_float(X) for every X_g within RT_AO_SC_ERR + 2^-53
+// of X? For a normal f = m 2^e (m in [0.5, 1)) the rounding boundaries are
+// 2^(e-25) away from f, or 2^(e-26) below a power of two (m = 0.5).
+RT_HD bool rt_f32_round_safe(double X, float f) {
+    int e;
+    (void)frexpf(f, &e);
+    const double h = ldexp(1.0, (rt_f2u(f) & 0x7fffffu) ? e - 25 : e - 26);
+    return fabs(X - (double)f) + (RT_AO_SC_ERR + 0x1p-53) < h;
+}
+
+// r in [0, 1], a in [0, 2*pi); tab = __sincostab for the fallback.
+RT_HD void rt_ao_dir_xy(const double* tab, float r, float a, float* xo, float* yo) {
+    double sa, ca;
+    rt_fast_sincos((double)a, &sa, &ca);
+    double X = (double)r * ca, Y = (double)r * sa;
+    float fx = (float)X, fy = (float)Y;
+    if (!(rt_f32_round_safe(X, fx) && rt_f32_round_safe(Y, fy))) {
+        rt_glibc_sincos_simd_t(tab, (double)a, &sa, &ca);
+        fx = (float)((double)r * ca);
+        fy = (float)((double)r * sa);
+    }
+    *xo = fx;
+    *yo = fy;
+}

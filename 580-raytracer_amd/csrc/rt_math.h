@@ -35,6 +35,48 @@ RTM_HD rv3 v3_normalize(rv3 a) {
     if (len > 0) { a.x /= len; a.y /= len; a.z /= len; }
     return a;
 }
+// v3_normalize for |a| in [0.5, 2] with components 0 or in [2^-60, 4] (the AO
+// sampler's unit vectors), on the device: the instruction sequences hipcc emits
+// for correctly rounded sqrtf and fp32 division, minus their range scaling and
+// fixup (identities in this range), the three divisions sharing one refined
+// reciprocal. Same bits as v3_normalize (GPU self-test rt580_selftest_math).
+// The host build is v3_normalize.
+#if defined(__HIP_DEVICE_COMPILE__)
+// rt_sqrt_nr: s = +0 or s in [2^-96, 2^126] (sqrt(+0) = +0 falls out of the sequence)
+__device__ __forceinline__ float rt_sqrt_nr(float s) {
+    const float y = __builtin_amdgcn_sqrtf(s);
+    const float ym = __uint_as_float(__float_as_uint(y) - 1u);
+    const float yp = __uint_as_float(__float_as_uint(y) + 1u);
+    float r = y;
+    if (__builtin_fmaf(-ym, y, s) <= 0.0f) r = ym;
+    if (__builtin_fmaf(-yp, y, s) > 0.0f) r = yp;
+    return r;
+}
+__device__ __forceinline__ float rt_div_nr(float n, float d, float y) {  // y = refined 1/d
+    float q = n * y;
+    const float e1 = __builtin_fmaf(-d, q, n);
+    q = __builtin_fmaf(e1, y, q);
+    const float e2 = __builtin_fmaf(-d, q, n);
+    q = __builtin_fmaf(e2, y, q);
+    return n == 0.0f ? n : q;
+}
+__device__ __forceinline__ bool rt_div_nr_ok(float n) {
+    const float a = fabsf(n);
+    return n == 0.0f || (a >= 0x1p-60f && a <= 4.0f);
+}
+// Callers guarantee the range: the AO sampler's vectors (rt_kernels.hip ao_body).
+__device__ __forceinline__ rv3 v3_normalize_unit(rv3 a) {
+    const float s = a.x * a.x + a.y * a.y + a.z * a.z;
+    const float len = rt_sqrt_nr(s);
+    const float y0 = __builtin_amdgcn_rcpf(len);
+    const float y = __builtin_fmaf(__builtin_fmaf(-len, y0, 1.0f), y0, y0);
+    return v3(rt_div_nr(a.x, len, y), rt_div_nr(a.y, len, y), rt_div_nr(a.z, len, y));
+}
+#else
+RTM_HD rv3 v3_normalize_unit(rv3 a) { return v3_normalize(a); }
+RTM_HD float rt_sqrt_nr(float s) { return sqrtf(s); }
+RTM_HD float rt_div_nr(float n, float d, float) { return n / d; }
+#endif
 RTM_HD float v3_length(rv3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
 // Vector3::reflect (Raytracer.h:143-148)
 RTM_HD rv3 v3_reflect(rv3 I, rv3 N) {

@@ -52,6 +52,7 @@ struct State {
     DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
         row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream;
     DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim;
+    DevBuf aofix_items, aofix_count;
     uint32_t* far_count_host = nullptr;  // pinned
     uint32_t far_cap = 0;
     uint32_t node_cap = 0, call_cap = 0;
@@ -219,6 +220,9 @@ DevWork dev_work() {
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
     w.hit4 = split ? (float4*)g.hit4.p : nullptr;
     w.hit_prim = split ? (int32_t*)g.hit_prim.p : nullptr;
+    w.aofix_items = (uint64_t*)g.aofix_items.p;
+    w.aofix_count = (uint32_t*)g.aofix_count.p;
+    w.aofix_cap = (uint32_t)(g.aofix_items.bytes / 8);
     return w;
 }
 
@@ -253,7 +257,7 @@ int ensure_work(const rt_render_params* p, int n_rows) {
         ensure(g.row_calls, (size_t)n_rows * 4) || ensure(g.row_hits, (size_t)n_rows * 4) ||
         ensure(g.row_nodes, (size_t)n_rows * 4) || ensure(g.row_base_local, (size_t)n_rows * 8) ||
         ensure(g.totals, 64) || ensure(g.call_node, ccap * 4) || ensure(g.call_rng, ccap * 8) ||
-        ensure(g.occ, ccap * 4))
+        ensure(g.occ, ccap * 4) || ensure(g.aofix_items, (size_t)8 << 20) || ensure(g.aofix_count, 64))
         return RT_FAILURE;
     g.node_cap = (uint32_t)cap;
     g.call_cap = (uint32_t)ccap;
@@ -538,6 +542,21 @@ int rt_gpu_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out) {
     return RT_SUCCESS;
 }
 
+int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (!mismatches) return fail("rt580_selftest_math: NULL output");
+    HIP_TRY(hipSetDevice(g.device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 4 * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), g.stream);
+    if (e == hipSuccess) e = launch_math_selftest(seed, n, d, g.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(mismatches, d, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    (void)hipFree(d);
+    HIP_TRY(e);
+    return RT_SUCCESS;
+}
+
 int rt_gpu_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* row_base) {
     if (!g.inited) return fail("rt_gpu_init not called");
     if (!gathered || !row_base) return fail("rt_gpu_row_bases: NULL buffer");
@@ -623,7 +642,7 @@ void rt_gpu_shutdown(void) {
     (void)hipStreamSynchronize(g.stream);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
                       &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
-                      &g.hit4, &g.hit_prim})
+                      &g.hit4, &g.hit_prim, &g.aofix_items, &g.aofix_count})
         release(*b);
     for (DevBuf* b : {&g.prims, &g.shade, &g.mats, &g.lights, &g.nodes, &g.rays, &g.lvl, &g.needed, &g.pix_hits,
                       &g.pix_nodes, &g.pix_prefix, &g.row_calls, &g.row_hits, &g.row_nodes, &g.row_base_local,

@@ -70,6 +70,7 @@ SIGNATURES = [
     ("rt_gpu_row_bases", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p]),
     ("rt_gpu_accel_active", ctypes.c_int, []),
+    ("rt580_selftest_math", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_gpu_last_error", ctypes.c_char_p, []),
     ("rt_gpu_shutdown", None, []),
     ("rt580_create", ctypes.c_void_p, [ctypes.c_int, ctypes.c_int]),

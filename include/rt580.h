@@ -183,6 +183,12 @@ int rt_gpu_row_bases(const int32_t* gathered_device, int world, int n_max, int h
  * clamped to [0, 255] by Raycast). n_values int16 -> n_values bytes = the PPM
  * body; used before the multi-GPU gather (half the bytes). */
 int rt_gpu_gamma_u8(const int16_t* fb_device, uint64_t n_values, uint8_t* out_device);
+/* Self-test of the device's range-restricted math sequences (rt_math.h,
+ * rt_libm.h) against the plain operations: mismatches[0] sqrt over every float
+ * in [2^-96, 2^126], [1] division, [2] unit-vector normalize, [3] AO direction
+ * (fast sincos + exact fallback), the last three on n seeded random inputs.
+ * Blocking. Test hook; not part of the reference's surface. */
+int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches);
 /* Scene-query acceleration. RT_ACCEL_BRUTE tests every primitive per ray, as
  * the reference's IntersectScene does (Raytracer.cpp:473-526); RT_ACCEL_AUTO
  * (default) uses the exact-semantics BVH for triangle scenes larger than one

@@ -33,6 +33,10 @@ int main() {
                 if (rt_lt_eps(x) != (d <= 1e-6)) b++;
                 if (rt_gt_eps(x) != (d > 1e-6)) b++;
                 if (rt_f2s(x) != (int32_t)(int16_t)(uint16_t)(uint32_t)cvttss2si(x)) b++;
+                // sph_test's sign rejection (rt_isect.h): sqrtf(b*b) <= b whenever b > 0
+                // and b*b is finite and above the discriminant's EPSILON
+                const float bb = x * x;
+                if (x > 0 && rt_gt_eps(bb) && bb < INFINITY && sqrtf(bb) > x) b++;
             }
             bad += b;
         });

@@ -2,6 +2,9 @@
 //   libm_check sincos            all float a in [0, 2*pi)   (AO angle domain, Raytracer.cpp:270-278)
 //   libm_check powf  y1 y2 ...   all float x in [0, 1.0001] for each exponent y (Raytracer.cpp:253)
 //   libm_check powf_random N     N random (x, y) pairs over the whole float range
+//   libm_check aodir N           rt_fast_sincos within RT_AO_SC_ERR of glibc for all float a
+//                                in [0, 2*pi), then N random AO samples (z, a) through
+//                                rt_ao_dir_xy vs the reference's (float)((double)r*cos(a))
 // Prints "mismatches=<n> checked=<m>" and the first few mismatches; exit 1 if any.
 #include "../../580-raytracer_amd/csrc/rt_libm.h"
 #include <cstdio>
@@ -83,6 +86,57 @@ int main(int argc, char** argv) {
             }
             g_bad += bad; g_checked += (long)(hi - lo);
         });
+    } else if (!std::strcmp(argv[1], "aodir")) {
+        uint32_t hi = rt_f2u(6.2831855f);
+        std::atomic<uint64_t> max_err_bits{0};
+        parallel(hi, [&](uint64_t lo, uint64_t hi) {
+            long bad = 0;
+            double mx = 0;
+            for (uint64_t u = lo; u < hi; u++) {
+                double a = (double)rt_u2f((uint32_t)u);
+                double s0, c0, s1, c1;
+                sincos(a, &s0, &c0);
+                rt_fast_sincos(a, &s1, &c1);
+                double e = fmax(fabs(s0 - s1), fabs(c0 - c1));
+                if (!(e <= RT_AO_SC_ERR)) { bad++; report("fast_sincos_err", a, e, s1, s0); }
+                if (e > mx) mx = e;
+            }
+            uint64_t b = rt_d2u(mx), cur = max_err_bits.load();
+            while (b > cur && !max_err_bits.compare_exchange_weak(cur, b)) {}
+            g_bad += bad; g_checked += (long)(hi - lo);
+        });
+        std::printf("max_abs_err=%a bound=%a\n", rt_u2d(max_err_bits.load()), RT_AO_SC_ERR);
+        uint64_t n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 100000000ull;
+        std::atomic<long> fallback{0};
+        parallel(n, [&](uint64_t lo, uint64_t hi) {
+            std::mt19937_64 g(lo * 2654435761ull + 581);
+            long bad = 0, fb = 0;
+            for (uint64_t i = lo; i < hi; i++) {
+                uint64_t w = g();
+                // the sampler's values: canonical floats k / 2^31 (Raytracer.cpp:270-276)
+                float u0 = (float)(uint32_t)(w & 0x7fffffffu) / 2147483648.0f;
+                float u1 = (float)(uint32_t)((w >> 32) & 0x7fffffffu) / 2147483648.0f;
+                if (i % 7 == 0) u0 = rt_u2f(rt_f2u(0.5f) + (uint32_t)(w >> 40) % 64) ;  // z near 0
+                if (i % 11 == 0) u1 = rt_u2f(rt_f2u(0.25f) + (uint32_t)((w >> 20) % 4096) - 2048);  // a near pi/2
+                if (u0 >= 1.0f) u0 = 0.99999994f;
+                if (u1 >= 1.0f) u1 = 0.99999994f;
+                const float z = u0 * (1.0f - (-1.0f)) + (-1.0f);
+                const float ang = u1 * ((float)(2 * 3.14159265) - 0.0f) + 0.0f;
+                const float r = sqrtf(1 - z * z);
+                double sg, cg;
+                sincos((double)ang, &sg, &cg);
+                const float x0 = (float)((double)r * cg), y0 = (float)((double)r * sg);
+                float x1, y1;
+                rt_ao_dir_xy(RT_T(rt_sincostab), r, ang, &x1, &y1);
+                double sa, ca;
+                rt_fast_sincos((double)ang, &sa, &ca);
+                if (!(rt_f32_round_safe((double)r * ca, (float)((double)r * ca)) &&
+                      rt_f32_round_safe((double)r * sa, (float)((double)r * sa)))) fb++;
+                if (rt_f2u(x0) != rt_f2u(x1) || rt_f2u(y0) != rt_f2u(y1)) { bad++; report("aodir", r, ang, x1, x0); }
+            }
+            g_bad += bad; g_checked += (long)(hi - lo); fallback += fb;
+        });
+        std::printf("fallback=%ld of %llu samples\n", fallback.load(), (unsigned long long)n);
     } else {
         return 2;
     }

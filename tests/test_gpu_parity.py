@@ -176,3 +176,16 @@ def test_gamma_u8_on_device_matches_ppm_writer():
     torch.cuda.synchronize()
     assert o.cpu().numpy().tobytes() == rt580.ppm_bytes(fb).split(b"\n", 3)[3]
     lib.rt_gpu_set_stream(lib.rt_gpu_own_stream())
+
+
+def test_device_math_sequences_match_plain_operations():
+    """The AO kernel's range-restricted sqrt/division sequences and its
+    polynomial sincos with exact fallback give the same bits as the plain
+    correctly rounded operations / glibc sincos (rt580_selftest_math): sqrt over
+    every float in [2^-96, 2^126], 2^26 random cases of each of the others."""
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    assert lib.rt_gpu_init(0) == 0
+    bad = (ctypes.c_uint64 * 4)()
+    assert lib.rt580_selftest_math(580, 1 << 26, bad) == 0, lib.rt_gpu_last_error()
+    assert list(bad) == [0, 0, 0, 0], "mismatches sqrt/div/normalize/aodir: %s" % list(bad)

@@ -35,6 +35,15 @@ def test_sincos_exhaustive_over_ao_angles():
     assert "checked=1086918619" in out
 
 
+def test_ao_direction_fast_sincos_bound_and_samples():
+    """rt_fast_sincos is within RT_AO_SC_ERR of glibc's sincos for EVERY float
+    angle in [0, 2*pi) (the bound rt_ao_dir_xy's rounding test relies on), and
+    rt_ao_dir_xy reproduces (float)((double)r*cos(a)), (float)((double)r*sin(a))
+    on 5e7 random AO samples, biased towards z ~ 0 and a ~ pi/2."""
+    out = _run(_build("libm_check"), "aodir", "50000000")
+    assert "checked=1136918619" in out
+
+
 def test_powf_exhaustive_over_scene_exponents():
     """Every float x in [0, 1.0001] for each specular exponent in the scene assets
     (Raytracer.cpp:253; fmax(dot(V,R),0) of unit vectors)."""
