@@ -24,12 +24,15 @@ struct Hit {
 
 RTM_HD rv3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
 
-// (num / den) < 0 exactly as the division would decide it, dividing only when
-// the signs do not already decide it (the quotient can still round to -0).
+// (num / den) < 0 exactly as the division would decide it, without dividing.
+// With opposite signs the quotient is negative unless |num/den| rounds to -0,
+// i.e. |num| / |den| <= 2^-150 (half the least denormal; the tie rounds to 0):
+// so test |num| * 2^150 > |den|, the scaling exact (or +inf when the quotient is
+// far from that bound). den = +-0 gives +-inf (< 0 when signs differ) as here.
 RTM_HD bool quot_lt0(float num, float den) {
     if (num != num || den != den || num == 0.0f) return false;  // NaN, or +-0 / den
     if (signbit(num) == signbit(den)) return false;             // > 0, +0 or +inf
-    return (num / den) < 0.0f;
+    return (fabsf(num) * 0x1p100f) * 0x1p50f > fabsf(den);
 }
 
 // IntersectTriangle. WANT_BARY: also return alpha/beta/gamma (closest hit); the
@@ -76,7 +79,7 @@ RTM_HD bool sph_test(const rt_prim& P, rv3 o, rv3 d, float& t) {
     if (b > 0.0f && c >= 0.0f && b < 0x1p60f) return false;
     float disc = (b * b) - (4.0f * c);
     if (rt_lt_eps(disc)) return false;
-    float sq = sqrtf(disc);
+    float sq = rt_sqrt_nr(disc);  // == sqrtf: disc > EPSILON or NaN here (rt_math.h)
     float t0 = (-b + sq) / 2.0f;
     float t1 = (-b - sq) / 2.0f;
     bool g0 = rt_gt_eps(t0), g1 = rt_gt_eps(t1);

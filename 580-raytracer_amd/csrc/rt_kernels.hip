@@ -158,12 +158,14 @@ __device__ __forceinline__ rt_prim load_prim_scalar(const rt_prim* prims, int j)
     return P;
 }
 
-__device__ bool closest_hit_scalar(const DevScene& S, rv3 o, rv3 d, Hit& h) {
+template <bool SIGN = false>
+__device__ bool closest_hit_scalar(const DevScene& S, bool active, rv3 o, rv3 d, Hit& h) {
     bool found = false;
     for (int j = 0; j < S.n_prims; j++) {
         const rt_prim P = load_prim_scalar(S.prims, j);
         float t, a = 0, b = 0, g = 0;
-        const bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test<true, false>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+        const bool hit = active && (P.kind == RT_PRIM_TRIANGLE ? tri_test<true, SIGN>(P, o, d, t, a, b, g)
+                                                               : sph_test(P, o, d, t));
         if (hit && (!found || t < h.t)) {
             found = true;
             h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
@@ -380,7 +382,9 @@ __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { retu
 // provisional hit stored per node and rays that may still have a far hit
 // queued (sorted far_closest_kernel in between); PHASE 2 = shading from the
 // stored hit. Items [i0, i1) of the level.
-template <bool BVH, int PHASE>
+// SCALAR (small brute-force scenes): wave-uniform scalar scene loads and the
+// division-free sign rejections (tri_test<SIGN>) instead of the LDS tile.
+template <bool BVH, int PHASE, bool SCALAR = false>
 __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
                                                    uint32_t i1) {
     __shared__ rt_prim tile[TILE];
@@ -395,7 +399,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
     const uint32_t next_base = base_id + count_all;
     if (blockIdx.x == 0 && threadIdx.x == 0) W.lvl[LVL_BASE + level + 1] = next_base;
     const int bounces = F.depth - level;
-    const bool resident = BVH ? false : stage_resident(S, tile);
+    const bool resident = (BVH || SCALAR) ? false : stage_resident(S, tile);
 
     for (uint32_t b0 = i0 + blockIdx.x * TB; b0 < count; b0 += gridDim.x * TB) {
         const uint32_t item = b0 + threadIdx.x;
@@ -455,7 +459,9 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                 h.t = hv.x; h.a = hv.y; h.b = hv.z; h.g = hv.w; h.prim = hp;
             }
         } else {
-            hit = BVH ? (active && bvh_closest(S.bv, o, d, h)) : closest_hit(S, tile, resident, active, o, d, h);
+            hit = BVH ? (active && bvh_closest(S.bv, o, d, h))
+                      : SCALAR ? closest_hit_scalar<true>(S, active, o, d, h)
+                               : closest_hit(S, tile, resident, active, o, d, h);
         }
 
         HitInfo hi;
@@ -493,12 +499,15 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             }
             bool occluded;
             if (l.kind == RT_LIGHT_DIRECTIONAL) {
-                occluded = BVH ? (hit && bvh_any(S.bv, so, L2)) : any_hit(S, tile, resident, hit, so, L2);
+                occluded = BVH ? (hit && bvh_any(S.bv, so, L2))
+                               : SCALAR ? any_hit_scalar<true>(S, hit, so, L2)
+                                        : any_hit(S, tile, resident, hit, so, L2);
             } else {
                 Hit sh;
                 sh.t = 0;
                 const bool shit = BVH ? (hit && bvh_closest(S.bv, so, L2, sh))
-                                      : closest_hit(S, tile, resident, hit, so, L2, sh);
+                                  : SCALAR ? closest_hit_scalar<true>(S, hit, so, L2, sh)
+                                           : closest_hit(S, tile, resident, hit, so, L2, sh);
                 occluded = shit && !(sh.t > dist);
             }
             if (hit && !occluded) local = px_add(local, local_color(S, F, hi, l, m, L));
@@ -1290,7 +1299,7 @@ hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStrea
 
 // ---------------------------------------------------------------- math self-test
 // The device-only fast sequences against the plain operations they replace:
-//  [0] rt_sqrt_nr vs sqrtf over EVERY float in [2^-96, 2^126] and +0
+//  [0] rt_sqrt_nr vs sqrtf over EVERY float in [2^-96, +inf] and +0
 //  [1] rt_div_nr vs '/' for n random pairs (|num| in [2^-60, 4] or +-0, den in [0.5, 2])
 //  [2] v3_normalize_unit vs v3_normalize for n random vectors (|v| in ~[0.5, 2])
 //  [3] rt_ao_dir_xy vs glibc sincos (rt_glibc_sincos_simd_t) for n random AO samples
@@ -1308,7 +1317,7 @@ __device__ __forceinline__ float st_float(uint64_t r, int emin, int emax) {  // 
 __global__ void math_selftest_kernel(uint64_t seed, uint64_t n, unsigned long long* bad) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lo = __float_as_uint(0x1p-96f), hi = __float_as_uint(0x1p126f);
+    const uint32_t lo = __float_as_uint(0x1p-96f), hi = 0x7f800000u;  // +inf
     unsigned long long b[4] = {0, 0, 0, 0};
     for (uint64_t u = i0; u <= (uint64_t)(hi - lo) + 1; u += stride) {
         const float x = u == (uint64_t)(hi - lo) + 1 ? 0.0f : __uint_as_float(lo + (uint32_t)u);
@@ -1419,6 +1428,16 @@ static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, 
                                               W.far_vals_alt, (int)nq, 0, RT_DIR_KEY_BITS, s);
 }
 
+// Small brute-force scenes: scalar-load trace kernel (RT580_TRACE_SCALAR=0: LDS tile, A/B only).
+static bool trace_scalar() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_TRACE_SCALAR");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     (void)hipGetLastError();  // launch checks below must not see a stale error
     const uint64_t npix = (uint64_t)F.n_rows * F.width;
@@ -1490,6 +1509,8 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
         // level 0 has exactly npix rays; deeper levels read their count on the device
         const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, 4096);
         if (S.use_bvh) hipLaunchKernelGGL((trace_kernel<true, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
+        else if (S.n_prims <= TILE && trace_scalar())
+            hipLaunchKernelGGL((trace_kernel<false, 0, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
         else hipLaunchKernelGGL((trace_kernel<false, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
@@ -1522,7 +1543,7 @@ static int ao_variant() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_AO_VARIANT");
-        v = e ? atoi(e) : (8 | 16 | 1024 | 2048 | 4096);  // scalar scene, 8 waves/SIMD, fast sincos/normalize
+        v = e ? atoi(e) : (4 | 8 | 16 | 1024 | 2048 | 4096);  // scalar scene, 8 waves/SIMD, fast sincos/normalize, sign rejects
     }
     return v;
 }
@@ -1599,7 +1620,7 @@ hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& 
         switch (v & ~16) {
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
             RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8) RT_AO_CASE(1032) RT_AO_CASE(2056) RT_AO_CASE(3080)
-            RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128)
+            RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128) RT_AO_CASE(7180)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;
         }

@@ -42,7 +42,8 @@ RTM_HD rv3 v3_normalize(rv3 a) {
 // reciprocal. Same bits as v3_normalize (GPU self-test rt580_selftest_math).
 // The host build is v3_normalize.
 #if defined(__HIP_DEVICE_COMPILE__)
-// rt_sqrt_nr: s = +0 or s in [2^-96, 2^126] (sqrt(+0) = +0 falls out of the sequence)
+// rt_sqrt_nr: s = +0, NaN or s in [2^-96, +inf] (sqrt(+0) = +0 and sqrt(+inf) =
+// +inf fall out of the sequence; no residual fma overflows)
 __device__ __forceinline__ float rt_sqrt_nr(float s) {
     const float y = __builtin_amdgcn_sqrtf(s);
     const float ym = __uint_as_float(__float_as_uint(y) - 1u);

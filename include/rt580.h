@@ -185,7 +185,7 @@ int rt_gpu_row_bases(const int32_t* gathered_device, int world, int n_max, int h
 int rt_gpu_gamma_u8(const int16_t* fb_device, uint64_t n_values, uint8_t* out_device);
 /* Self-test of the device's range-restricted math sequences (rt_math.h,
  * rt_libm.h) against the plain operations: mismatches[0] sqrt over every float
- * in [2^-96, 2^126], [1] division, [2] unit-vector normalize, [3] AO direction
+ * in [2^-96, +inf], [1] division, [2] unit-vector normalize, [3] AO direction
  * (fast sincos + exact fallback), the last three on n seeded random inputs.
  * Blocking. Test hook; not part of the reference's surface. */
 int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches);

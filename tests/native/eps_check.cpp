@@ -3,7 +3,7 @@
 //   (double)x < 1e-6  (Raytracer.cpp:17, :427),  (double)x <= 1e-6 (:382),
 //   (double)x > 1e-6  (GreaterThanZero, Raytracer.h:558-560),
 // and that rt_f2s matches the x86-64 cvttss2si-based static_cast<short>(float).
-#include "../../580-raytracer_amd/csrc/rt_math.h"
+#include "../../580-raytracer_amd/csrc/rt_isect.h"
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -37,6 +37,9 @@ int main() {
                 // and b*b is finite and above the discriminant's EPSILON
                 const float bb = x * x;
                 if (x > 0 && rt_gt_eps(bb) && bb < INFINITY && sqrtf(bb) > x) b++;
+                // tri_test's division-free barycentric sign (rt_isect.h quot_lt0)
+                for (float den : {1.0f, -0.75f, 3e-38f, -1e30f, 1e-44f})
+                    if (rt580::quot_lt0(x, den) != ((x / den) < 0.0f)) b++;
             }
             bad += b;
         });
