@@ -856,15 +856,14 @@ __global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork 
 
 // ---------------------------------------------------------------- AO fix-up
 // Samples of ao_body<... | 4096> whose fast rounding test failed (rt_libm.h
-// rt_f32_round_safe; ~1e-5 of samples): the exact sample with glibc's sincos,
-// then the same scene query as the main pass (BVH scenes: near + far search, or
-// the reference's loop for far origins), counted into the call's occlusion.
-__device__ bool ao_exact_sample(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t item,
-                                uint32_t& call) {
+// rt_f32_round_safe; ~3e-5 of samples): the exact sample with glibc's sincos,
+// then the main pass's scene query. Brute-force scenes test every primitive;
+// BVH scenes run the near query and send misses (and far-origin rays) to the
+// chunk's sorted far queue, like ao_body's own misses.
+__device__ void ao_fix_item(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t item) {
     const uint32_t N = (uint32_t)F.ao_samples;
     const uint64_t c = item / N;
     const uint32_t s = (uint32_t)(item - c * N);
-    call = (uint32_t)c;
     const NodeRec& nd = W.nodes[W.call_node[c]];
     const rv3 hp = ld3(nd.hp), n = ld3(nd.n);
     float u0, u1;
@@ -878,20 +877,30 @@ __device__ bool ao_exact_sample(const DevScene& S, const DevFrame& F, const DevW
     if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
     const rv3 o = v3_add(hp, v3_scale(v, 0.2f));
     const rv3 d = v3_normalize(v);
-    if (S.use_bvh && !(S.bv.has_far && far_origin(S, o))) return bvh_any(S.bv, o, d, /*with_far=*/true);
-    for (int j = 0; j < S.n_prims; j++)
-        if (prim_test_any(S.prims[j], o, d)) return true;
-    return false;
+    bool hit = false;
+    if (S.use_bvh) {
+        const bool brute = S.bv.has_far && far_origin(S, o);
+        hit = !brute && bvh_any(S.bv, o, d, /*with_far=*/!S.bv.has_far);
+        if (!hit && S.bv.has_far) {
+            if (brute) atomicAdd(W.far_count + 1, 1u);
+            const uint32_t slot = atomicAdd(W.far_count, 1u);
+            W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
+            W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+            W.far_keys[slot] = brute ? RT_KEY_BRUTE : dir_key(d);
+            W.far_vals[slot] = slot;
+            return;
+        }
+    } else {
+        for (int j = 0; j < S.n_prims && !hit; j++) hit = prim_test_any(S.prims[j], o, d);
+    }
+    if (hit) atomicAdd(&W.occ[c], 1u);
 }
 
 // The queued items, unless the queue overflowed.
 __global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevWork W) {
     const uint32_t n = *W.aofix_count;
     if (n > W.aofix_cap) return;
-    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
-        uint32_t call;
-        if (ao_exact_sample(S, F, W, W.aofix_items[i], call)) atomicAdd(&W.occ[call], 1u);
-    }
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) ao_fix_item(S, F, W, W.aofix_items[i]);
 }
 
 // Overflow (more failing samples than queue slots): every item of [b, e) is
@@ -912,9 +921,7 @@ __global__ void __launch_bounds__(TB) ao_fixall_kernel(DevScene S, DevFrame F, D
         double sa, ca;
         rt_fast_sincos((double)ang, &sa, &ca);
         const double X = (double)r * ca, Y = (double)r * sa;
-        if (rt_f32_round_safe(X, (float)X) && rt_f32_round_safe(Y, (float)Y)) continue;
-        uint32_t call;
-        if (ao_exact_sample(S, F, W, item, call)) atomicAdd(&W.occ[call], 1u);
+        if (!(rt_f32_round_safe(X, (float)X) && rt_f32_round_safe(Y, (float)Y))) ao_fix_item(S, F, W, item);
     }
 }
 
@@ -1570,6 +1577,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if ((e = hipMemsetAsync(W.aofix_count, 0, 4, s)) != hipSuccess) return e;
             hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+            // exact recompute of the fast pass's failing samples; their misses join the far queue
             if ((e = launch_ao_fix(S, F, W, b, e1, s)) != hipSuccess) return e;
             if (!S.bv.has_far) continue;
             uint32_t nq = 0, nb = 0;
@@ -1610,7 +1618,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
 // they have nothing to do.
 hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t b, uint64_t e,
                          hipStream_t s) {
-    hipLaunchKernelGGL(ao_fix_kernel, dim3(64), dim3(TB), 0, s, S, F, W);
+    hipLaunchKernelGGL(ao_fix_kernel, dim3(2048), dim3(TB), 0, s, S, F, W);
     hipLaunchKernelGGL(ao_fixall_kernel, dim3(8192), dim3(TB), 0, s, S, F, W, b, e);
     return hipGetLastError();
 }
