@@ -85,9 +85,16 @@ TriBounds analyse(const rt_prim& p, double S, double inflate) {
     const double g1 = std::min(e01, e12) * std::sin(0.5 * a1);
     const double g2 = std::min(e12, e20) * std::sin(0.5 * a2);
     const double G = std::min(emin, std::min(g0, std::min(g1, g2)));
-    // Error: 11.25 u |a||b| for the sub-area arithmetic, plus the misalignment
-    // of the float normal N = normalize(cross(v1 - v0, v2 - v0)) (~3u / sin a0).
-    const double kappa = 16.0 + 4.0 / std::sin(a0);
+    // Error of a computed sub-area s = dot(cross(A, B), N) (twice the area;
+    // A = fl(v_i - Pp), B = fl(v_j - Pp) or one short edge), standard model,
+    // u = 2^-24: each cross component is off by <= gamma3 (|A_j B_k| + |A_k B_j|)
+    // + u |X_i|, the dot adds gamma3 sum |c_i N_i|; with sum_i |N_i| <= sqrt3 |N|
+    // and |X| <= |A||B|: |s - S| <= (3 sqrt3 + 4)(1 + 10u) u |A||B| < 9.25 u |A||B|.
+    // S (exact, float inputs) is twice the signed area of the projection onto
+    // the plane normal to the float N: Pp's offset along N cancels, and the
+    // float N's tilt (~u / sin a0) changes the projected geometry only at
+    // second order, so G below (from the exact triangle) applies.
+    const double kappa = 9.25 * (1.0 + 1e-6);
     const double ep = emax + std::ldexp(S, -10);  // + off-plane height and rounding slack
     const double a = kappa * kU, b = G;
     const double bb = b - 2 * a * ep;

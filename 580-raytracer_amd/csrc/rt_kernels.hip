@@ -328,6 +328,32 @@ __device__ __forceinline__ void wave_alloc2(uint32_t* counter, bool fa, bool fb,
     sb = base + na + (uint32_t)__popcll(mb & lt);
 }
 
+// Same, one atomic per workgroup: the waves' totals meet in LDS (every thread
+// of the block must call it, in the same iteration).
+__device__ __forceinline__ void block_alloc2(uint32_t* counter, bool fa, bool fb, uint32_t& sa, uint32_t& sb) {
+    __shared__ uint32_t wtot[TB / 64 + 1];
+    const uint64_t ma = __ballot(fa), mb = __ballot(fb);
+    const uint32_t na = (uint32_t)__popcll(ma), nb = (uint32_t)__popcll(mb);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) wtot[wave] = na + nb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t sum = 0;
+        for (int w = 0; w < TB / 64; w++) {
+            const uint32_t c = wtot[w];
+            wtot[w] = sum;
+            sum += c;
+        }
+        wtot[TB / 64] = sum ? atomicAdd(counter, sum) : 0u;
+    }
+    __syncthreads();
+    const uint32_t base = wtot[TB / 64] + wtot[wave];
+    __syncthreads();  // wtot is reused by the next call
+    const uint64_t lt = lanemask_lt();
+    sa = base + (uint32_t)__popcll(ma & lt);
+    sb = base + na + (uint32_t)__popcll(mb & lt);
+}
+
 // Octahedral direction key (12 + 12 bits): groups rays of similar direction
 // for the far-hit passes (grouping only; never affects a result).
 #define RT_DIR_KEY_BITS 25
@@ -540,7 +566,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             }
         }
         uint32_t sa, sb;
-        wave_alloc2(&W.lvl[level + 1], want_refl, want_refr, sa, sb);
+        block_alloc2(&W.lvl[level + 1], want_refl, want_refr, sa, sb);
         int32_t child0 = -1, child1 = -1;
         if (want_refl) {
             const uint32_t id = next_base + sa;
@@ -1628,7 +1654,7 @@ hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& 
         switch (v & ~16) {
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
             RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8) RT_AO_CASE(1032) RT_AO_CASE(2056) RT_AO_CASE(3080)
-            RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128) RT_AO_CASE(7180)
+            RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128) RT_AO_CASE(7180) RT_AO_CASE(7182)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;
         }
@@ -1638,7 +1664,7 @@ hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& 
         switch (v) {
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
             RT_AO_CASE(41) RT_AO_CASE(73) RT_AO_CASE(137) RT_AO_CASE(105) RT_AO_CASE(233)
-            RT_AO_CASE(1032) RT_AO_CASE(3080) RT_AO_CASE(3084) RT_AO_CASE(7176)
+            RT_AO_CASE(1032) RT_AO_CASE(3080) RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(7180) RT_AO_CASE(7182)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;
         }
