@@ -922,17 +922,16 @@ __device__ void ao_fix_item(const DevScene& S, const DevFrame& F, const DevWork&
     if (hit) atomicAdd(&W.occ[c], 1u);
 }
 
-// The queued items, unless the queue overflowed.
-__global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevWork W) {
+// The queued items; if the queue overflowed (more failing samples than slots),
+// every item of [b, e) is re-tested and the failing ones recomputed instead.
+__global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
     const uint32_t n = *W.aofix_count;
-    if (n > W.aofix_cap) return;
-    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) ao_fix_item(S, F, W, W.aofix_items[i]);
-}
-
-// Overflow (more failing samples than queue slots): every item of [b, e) is
-// re-tested and the failing ones recomputed; the queue is ignored.
-__global__ void __launch_bounds__(TB) ao_fixall_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
-    if (*W.aofix_count <= W.aofix_cap) return;
+    if (n == 0) return;
+    if (n <= W.aofix_cap) {
+        for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB)
+            ao_fix_item(S, F, W, W.aofix_items[i]);
+        return;
+    }
     const uint64_t items_all = W.totals[0] * (uint64_t)F.ao_samples;
     if (e > items_all) e = items_all;
     const uint32_t N = (uint32_t)F.ao_samples;
@@ -1272,6 +1271,51 @@ __global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, Dev
     fb[(size_t)p * 3 + 2] = (int16_t)ret.b;
 }
 
+// Level-by-level form of the same blend: one launch per recursion level, from
+// the deepest up. A node's value (Raycast's return) is combined from its own
+// local colour and its children's values, stored by the previous launch in the
+// children's NodeRec.pad; level 0 writes the framebuffer. Coalesced over each
+// level's contiguous node ids, no per-thread stack.
+__device__ __forceinline__ rpix node_val_load(const DevWork& W, int32_t id) {
+    if (id < 0) return px(0, 0, 0);
+    const int2 v = *reinterpret_cast<const int2*>(W.nodes[id].pad);
+    return px((int16_t)(v.x & 0xffff), (int16_t)(v.x >> 16), (int16_t)(v.y & 0xffff));
+}
+
+__global__ void __launch_bounds__(TB) resolve_level_kernel(DevScene S, DevFrame F, DevWork W, int level,
+                                                           int16_t* __restrict__ fb) {
+    const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
+    uint32_t base = 0, count = npix;
+    if (level > 0) {  // the trace's own clamp to the node capacity
+        base = W.lvl[LVL_BASE + level];
+        const uint32_t room = W.node_cap > base ? W.node_cap - base : 0u;
+        count = W.lvl[level] < room ? W.lvl[level] : room;
+    }
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < count; i += gridDim.x * TB) {
+        const uint32_t node = base + i;
+        const NodeRec nd = W.nodes[node];
+        const int flags = nd.local_b_flags >> 16;
+        rpix v;
+        if (!(flags & RT_NODE_HIT)) {
+            v = px(254, 64, 205);  // BG_COLOR (Raytracer.h:597)
+        } else {
+            const rt_material m = S.mats[nd.shape];
+            const rpix local = node_local(S, F, W, nd, m);
+            v = (flags & RT_NODE_LEAF) ? px_clamp(local)
+                                       : combine(local, node_val_load(W, nd.child[0]), node_val_load(W, nd.child[1]),
+                                                 nd.kr, nd.kt, m.ks, m.kt);
+        }
+        if (level == 0) {
+            fb[(size_t)node * 3 + 0] = (int16_t)v.r;
+            fb[(size_t)node * 3 + 1] = (int16_t)v.g;
+            fb[(size_t)node * 3 + 2] = (int16_t)v.b;
+        } else {
+            *reinterpret_cast<int2*>(W.nodes[node].pad) =
+                make_int2((int32_t)(((uint32_t)v.r & 0xffffu) | ((uint32_t)v.g << 16)), (int32_t)((uint32_t)v.b & 0xffffu));
+        }
+    }
+}
+
 // Exclusive raster-order scan of all ranks' per-row AO calls (one workgroup),
 // written out at this rank's rows (rt_gpu_row_bases).
 __global__ void __launch_bounds__(1024) row_bases_kernel(const int32_t* __restrict__ gathered, int world, int n_max,
@@ -1461,6 +1505,16 @@ static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, 
                                               W.far_vals_alt, (int)nq, 0, RT_DIR_KEY_BITS, s);
 }
 
+// Per-frame counters, one launch: level counts/bases, the node-capacity probe,
+// the AO fix-up queue count.
+__global__ void frame_init_kernel(DevWork W) {
+    for (int i = threadIdx.x; i < 2 * LVL_BASE; i += blockDim.x) W.lvl[i] = 0;
+    if (threadIdx.x == 0) {
+        *W.needed = 0;
+        *W.aofix_count = 0;
+    }
+}
+
 // Small brute-force scenes: scalar-load trace kernel (RT580_TRACE_SCALAR=0: LDS tile, A/B only).
 static bool trace_scalar() {
     static int v = -1;
@@ -1474,7 +1528,8 @@ static bool trace_scalar() {
 hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     (void)hipGetLastError();  // launch checks below must not see a stale error
     const uint64_t npix = (uint64_t)F.n_rows * F.width;
-    hipError_t e = hipMemsetAsync(W.lvl, 0, sizeof(uint32_t) * 2 * LVL_BASE, s);
+    hipLaunchKernelGGL(frame_init_kernel, dim3(1), dim3(64), 0, s, W);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const bool split = S.use_bvh && S.bv.has_far && W.hit4 && W.far_cap;
     for (int level = 0; level <= F.depth; level++) {
@@ -1629,23 +1684,17 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         }
         return hipSuccess;
     }
-    const int v = ao_variant();
-    if (v & 4096) {
-        const hipError_t e = hipMemsetAsync(W.aofix_count, 0, 4, s);
-        if (e != hipSuccess) return e;
-    }
+    const int v = ao_variant();  // (frame_init_kernel zeroed W.aofix_count)
     const hipError_t e = launch_ao_small(S, F, W, s, v);
     if (e != hipSuccess || !(v & 4096)) return e;
     return launch_ao_fix(S, F, W, 0, ~0ull, s);
 }
 
 // Exact recompute of the samples the fast pass queued (or, on queue overflow,
-// of every failing sample of items [b, e)); both kernels exit at once when
-// they have nothing to do.
+// of every failing sample of items [b, e)); exits at once with nothing to do.
 hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t b, uint64_t e,
                          hipStream_t s) {
-    hipLaunchKernelGGL(ao_fix_kernel, dim3(2048), dim3(TB), 0, s, S, F, W);
-    hipLaunchKernelGGL(ao_fixall_kernel, dim3(8192), dim3(TB), 0, s, S, F, W, b, e);
+    hipLaunchKernelGGL(ao_fix_kernel, dim3(2048), dim3(TB), 0, s, S, F, W, b, e);
     return hipGetLastError();
 }
 
@@ -1681,10 +1730,27 @@ hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& 
     return hipGetLastError();
 }
 
+// RT580_RESOLVE=0: the per-pixel stack form (A/B only).
+static bool resolve_by_level() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_RESOLVE");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s) {
     const uint64_t npix = (uint64_t)F.n_rows * F.width;
     if (npix == 0) return hipSuccess;
-    hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)((npix + TB - 1) / TB)), dim3(TB), 0, s, S, F, W, fb);
+    if (!resolve_by_level()) {
+        hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)((npix + TB - 1) / TB)), dim3(TB), 0, s, S, F, W, fb);
+        return hipGetLastError();
+    }
+    for (int level = F.depth; level >= 0; level--) {
+        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, 4096);
+        hipLaunchKernelGGL(resolve_level_kernel, dim3(grid), dim3(TB), 0, s, S, F, W, level, fb);
+    }
     return hipGetLastError();
 }
 

@@ -279,8 +279,7 @@ int ensure_work(const rt_render_params* p, int n_rows) {
 
 // Phase 1: trace every level of the selected rows and count their AO calls.
 int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_rows) {
-    if (ensure_work(p, n_rows)) return RT_FAILURE;
-    HIP_TRY(hipMemsetAsync(g.needed.p, 0, 4, g.stream));
+    if (ensure_work(p, n_rows)) return RT_FAILURE;  // (launch_trace zeroes the per-frame counters)
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
     const DevScene sc = dev_scene(p);
     g.last_accel = sc.use_bvh != 0;
