@@ -27,6 +27,13 @@ struct DevBuf {
 
 enum { EV_START, EV_TRACE, EV_RANK, EV_AO, EV_RESOLVE, EV_N };
 
+struct Slot {
+    hipStream_t stream = nullptr;  // frame stream (non-blocking)
+    hipEvent_t done = nullptr;     // end of the slot's last enqueued phase
+    DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
+        row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream, aofix_items, aofix_count;
+};
+
 struct State {
     bool inited = false;
     int device = 0;
@@ -48,11 +55,15 @@ struct State {
     int accel = RT_ACCEL_AUTO;
     bool last_accel = false;
     uint64_t scene_gen = 0;
-    // workspace
-    DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
-        row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream;
+    // per-frame workspace: two slots, so that consecutive frames overlap on
+    // two streams (frame pipelining, see begin_slot)
+    Slot slot[2];
+    int cur = 0;               // slot of the frame being enqueued
+    uint64_t frames = 0;       // frames begun (selects the slot)
+    hipEvent_t user_mark[2] = {nullptr, nullptr};  // the caller's stream at the start of a frame call
+    bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
+    // BVH far-queue buffers (BVH frames always run serialized on slot 0)
     DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim;
-    DevBuf aofix_items, aofix_count;
     uint32_t* far_count_host = nullptr;  // pinned
     uint32_t far_cap = 0;
     uint32_t node_cap = 0, call_cap = 0;
@@ -72,6 +83,11 @@ struct State {
 
 State g;
 char g_err[512] = "";
+#define SL (g.slot[g.cur])
+
+// Stream of the frame being enqueued.
+hipStream_t fs() { return g.pipeline ? g.slot[g.cur].stream : g.stream; }
+
 
 int fail(const char* fmt, ...) {
     va_list ap;
@@ -88,9 +104,62 @@ int fail(const char* fmt, ...) {
         if (e_ != hipSuccess) return fail("%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
+// Frame pipelining. Frame k runs on slot k & 1 (its own stream and workspace),
+// so frame k+1's latency-bound trace overlaps frame k's AO kernel. Ordering:
+//  - frame k waits on the caller's stream as it was at the START of call k-1
+//    (user_mark): that covers whatever the caller queued against frame k-2's
+//    framebuffer (same slot, overwritten now) before it asked for frame k-1;
+//  - the caller's stream waits for the frame (end_slot), so work the caller
+//    queues after the call sees its results ("asynchronous on the shim's stream").
+// BVH frames (host syncs inside, shared far-queue buffers) run on slot 0 after
+// everything the caller's stream holds, i.e. serialized.
+int begin_slot(bool serialize) {
+    if (!g.pipeline) {
+        g.cur = 0;
+        return RT_SUCCESS;
+    }
+    const int k = (int)(g.frames & 1);
+    HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));
+    g.cur = serialize ? 0 : k;
+    const hipEvent_t wait = (g.frames == 0 || serialize) ? g.user_mark[k] : g.user_mark[k ^ 1];
+    HIP_TRY(hipStreamWaitEvent(SL.stream, wait, 0));
+    g.frames++;
+    return RT_SUCCESS;
+}
+
+// The caller's stream waits for what the current slot has enqueued.
+int end_slot() {
+    if (!g.pipeline) return RT_SUCCESS;
+    HIP_TRY(hipEventRecord(SL.done, SL.stream));
+    HIP_TRY(hipStreamWaitEvent(g.stream, SL.done, 0));
+    return RT_SUCCESS;
+}
+
+// The current slot waits for what the caller's stream holds now (inputs the
+// caller produced there, e.g. the all-gathered row bases of rt_gpu_shade_rows).
+int slot_wait_user() {
+    if (!g.pipeline) return RT_SUCCESS;
+    const int k = (int)(g.frames & 1);  // the mark the next begin_slot overwrites, unused until then
+    HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));
+    HIP_TRY(hipStreamWaitEvent(SL.stream, g.user_mark[k], 0));
+    return RT_SUCCESS;
+}
+
+bool frame_uses_bvh(const rt_render_params* p) {
+    return g.accel == RT_ACCEL_AUTO && g.bvh_ok && bvh_usable(g.bvh, p->cam_from);
+}
+
+// Wait for every enqueued frame (both slots) and the caller's stream.
+int sync_all() {
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    if (g.pipeline)
+        for (auto& sl : g.slot) HIP_TRY(hipStreamSynchronize(sl.stream));
+    return RT_SUCCESS;
+}
+
 int ensure(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return RT_SUCCESS;
-    if (b.p) { (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
+    if (b.p) { (void)hipDeviceSynchronize(); (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
     if (bytes == 0) bytes = 64;
     size_t want = bytes + bytes / 8 + 256;
     HIP_TRY(hipMalloc(&b.p, want));
@@ -189,22 +258,22 @@ DevFrame dev_frame(const rt_render_params* p, int row_begin, int row_step, int n
 
 DevWork dev_work() {
     DevWork w;
-    w.nodes = (NodeRec*)g.nodes.p;
-    w.rays = (RayItem*)g.rays.p;
-    w.lvl = (uint32_t*)g.lvl.p;
-    w.needed = (uint32_t*)g.needed.p;
-    w.pix_hits = (uint32_t*)g.pix_hits.p;
-    w.pix_nodes = (uint32_t*)g.pix_nodes.p;
-    w.pix_prefix = (uint32_t*)g.pix_prefix.p;
-    w.row_calls = (uint32_t*)g.row_calls.p;
-    w.row_hits = (uint32_t*)g.row_hits.p;
-    w.row_nodes = (uint32_t*)g.row_nodes.p;
-    w.row_base_local = (uint64_t*)g.row_base_local.p;
-    w.totals = (uint64_t*)g.totals.p;
-    w.call_node = (uint32_t*)g.call_node.p;
-    w.call_rng = (uint64_t*)g.call_rng.p;
-    w.occ = (uint32_t*)g.occ.p;
-    w.mt_stream = (const uint32_t*)g.mt_stream.p;
+    w.nodes = (NodeRec*)SL.nodes.p;
+    w.rays = (RayItem*)SL.rays.p;
+    w.lvl = (uint32_t*)SL.lvl.p;
+    w.needed = (uint32_t*)SL.needed.p;
+    w.pix_hits = (uint32_t*)SL.pix_hits.p;
+    w.pix_nodes = (uint32_t*)SL.pix_nodes.p;
+    w.pix_prefix = (uint32_t*)SL.pix_prefix.p;
+    w.row_calls = (uint32_t*)SL.row_calls.p;
+    w.row_hits = (uint32_t*)SL.row_hits.p;
+    w.row_nodes = (uint32_t*)SL.row_nodes.p;
+    w.row_base_local = (uint64_t*)SL.row_base_local.p;
+    w.totals = (uint64_t*)SL.totals.p;
+    w.call_node = (uint32_t*)SL.call_node.p;
+    w.call_rng = (uint64_t*)SL.call_rng.p;
+    w.occ = (uint32_t*)SL.occ.p;
+    w.mt_stream = (const uint32_t*)SL.mt_stream.p;
     w.node_cap = g.node_cap;
     w.call_cap = g.call_cap;
     w.far_rays = (float4*)g.far_rays.p;
@@ -220,9 +289,9 @@ DevWork dev_work() {
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
     w.hit4 = split ? (float4*)g.hit4.p : nullptr;
     w.hit_prim = split ? (int32_t*)g.hit_prim.p : nullptr;
-    w.aofix_items = (uint64_t*)g.aofix_items.p;
-    w.aofix_count = (uint32_t*)g.aofix_count.p;
-    w.aofix_cap = (uint32_t)(g.aofix_items.bytes / 8);
+    w.aofix_items = (uint64_t*)SL.aofix_items.p;
+    w.aofix_count = (uint32_t*)SL.aofix_count.p;
+    w.aofix_cap = (uint32_t)(SL.aofix_items.bytes / 8);
     return w;
 }
 
@@ -251,13 +320,13 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     if (cap > 0xffffff00ull) return fail("node capacity exceeds 2^32");
     const uint64_t ccap = cap * (uint64_t)(g.n_ambient > 0 ? g.n_ambient : 1);
     if (ccap > 0xffffff00ull) return fail("AO-call capacity exceeds 2^32");
-    if (ensure(g.nodes, cap * sizeof(NodeRec)) || ensure(g.rays, cap * sizeof(RayItem)) ||
-        ensure(g.lvl, 4 * (RT_MAX_DEPTH + 2) * sizeof(uint32_t)) || ensure(g.needed, 64) ||
-        ensure(g.pix_hits, npix * 4) || ensure(g.pix_nodes, npix * 4) || ensure(g.pix_prefix, npix * 4) ||
-        ensure(g.row_calls, (size_t)n_rows * 4) || ensure(g.row_hits, (size_t)n_rows * 4) ||
-        ensure(g.row_nodes, (size_t)n_rows * 4) || ensure(g.row_base_local, (size_t)n_rows * 8) ||
-        ensure(g.totals, 64) || ensure(g.call_node, ccap * 4) || ensure(g.call_rng, ccap * 8) ||
-        ensure(g.occ, ccap * 4) || ensure(g.aofix_items, (size_t)8 << 20) || ensure(g.aofix_count, 64))
+    if (ensure(SL.nodes, cap * sizeof(NodeRec)) || ensure(SL.rays, cap * sizeof(RayItem)) ||
+        ensure(SL.lvl, 4 * (RT_MAX_DEPTH + 2) * sizeof(uint32_t)) || ensure(SL.needed, 64) ||
+        ensure(SL.pix_hits, npix * 4) || ensure(SL.pix_nodes, npix * 4) || ensure(SL.pix_prefix, npix * 4) ||
+        ensure(SL.row_calls, (size_t)n_rows * 4) || ensure(SL.row_hits, (size_t)n_rows * 4) ||
+        ensure(SL.row_nodes, (size_t)n_rows * 4) || ensure(SL.row_base_local, (size_t)n_rows * 8) ||
+        ensure(SL.totals, 64) || ensure(SL.call_node, ccap * 4) || ensure(SL.call_rng, ccap * 8) ||
+        ensure(SL.occ, ccap * 4) || ensure(SL.aofix_items, (size_t)8 << 20) || ensure(SL.aofix_count, 64))
         return RT_FAILURE;
     g.node_cap = (uint32_t)cap;
     g.call_cap = (uint32_t)ccap;
@@ -284,11 +353,11 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     const DevScene sc = dev_scene(p);
     g.last_accel = sc.use_bvh != 0;
     {
-        const hipError_t e = launch_trace(sc, f, dev_work(), g.stream);
+        const hipError_t e = launch_trace(sc, f, dev_work(), fs());
         if (e != hipSuccess) return fail("launch_trace (%s): %s", launch_where(), hipGetErrorString(e));
     }
-    HIP_TRY(launch_row_counts(sc, f, dev_work(), g.stream));
-    HIP_TRY(hipEventRecord(g.ev[EV_TRACE], g.stream));
+    HIP_TRY(launch_row_counts(sc, f, dev_work(), fs()));
+    HIP_TRY(hipEventRecord(g.ev[EV_TRACE], fs()));
     g.last_rows = n_rows;
     g.last_width = p->width;
     g.last_ao_samples = p->ao_samples;
@@ -302,15 +371,15 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
 int prepare_mt_stream(const rt_render_params* p) {
     if (p->rng_engine != RT_RNG_MT19937 || !p->ao_enabled || g.n_ambient == 0) return RT_SUCCESS;
     uint64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, g.totals.p, 8, hipMemcpyDeviceToHost, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    HIP_TRY(hipMemcpyAsync(&total, SL.totals.p, 8, hipMemcpyDeviceToHost, fs()));
+    HIP_TRY(hipStreamSynchronize(fs()));
     const uint64_t n = total * 2ull * (uint64_t)p->ao_samples;
-    if (ensure(g.mt_stream, n * 4 + 8)) return RT_FAILURE;
+    if (ensure(SL.mt_stream, n * 4 + 8)) return RT_FAILURE;
     std::vector<uint32_t> host(n);
     std::mt19937 gen(p->rng_seed);
     for (uint64_t i = 0; i < n; i++) host[i] = (uint32_t)gen();
-    if (n) HIP_TRY(hipMemcpyAsync(g.mt_stream.p, host.data(), n * 4, hipMemcpyHostToDevice, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    if (n) HIP_TRY(hipMemcpyAsync(SL.mt_stream.p, host.data(), n * 4, hipMemcpyHostToDevice, fs()));
+    HIP_TRY(hipStreamSynchronize(fs()));
     return RT_SUCCESS;
 }
 
@@ -319,14 +388,14 @@ int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
                int16_t* fb_out) {
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
     const DevScene sc = dev_scene(p);
-    HIP_TRY(launch_rank(sc, f, dev_work(), row_base_global, g.stream));
-    HIP_TRY(hipEventRecord(g.ev[EV_RANK], g.stream));
+    HIP_TRY(launch_rank(sc, f, dev_work(), row_base_global, fs()));
+    HIP_TRY(hipEventRecord(g.ev[EV_RANK], fs()));
     if (prepare_mt_stream(p)) return RT_FAILURE;
     DevWork w = dev_work();
-    HIP_TRY(launch_ao(sc, f, w, g.stream));
-    HIP_TRY(hipEventRecord(g.ev[EV_AO], g.stream));
-    HIP_TRY(launch_resolve(sc, f, w, fb_out, g.stream));
-    HIP_TRY(hipEventRecord(g.ev[EV_RESOLVE], g.stream));
+    HIP_TRY(launch_ao(sc, f, w, fs()));
+    HIP_TRY(hipEventRecord(g.ev[EV_AO], fs()));
+    HIP_TRY(launch_resolve(sc, f, w, fb_out, fs()));
+    HIP_TRY(hipEventRecord(g.ev[EV_RESOLVE], fs()));
     return RT_SUCCESS;
 }
 
@@ -337,8 +406,8 @@ int check_capacity(const rt_render_params* p, bool& retry) {
     retry = false;
     if (g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0)
         return RT_SUCCESS;
-    HIP_TRY(hipMemcpyAsync(g.needed_host, g.needed.p, 4, hipMemcpyDeviceToHost, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    HIP_TRY(hipMemcpyAsync(g.needed_host, SL.needed.p, 4, hipMemcpyDeviceToHost, fs()));
+    HIP_TRY(hipStreamSynchronize(fs()));
     const uint32_t need = *g.needed_host;
     if (need > g.node_cap) {
         const uint64_t npix = (uint64_t)g.last_rows * p->width;
@@ -371,6 +440,15 @@ int rt_gpu_init(int device) {
     HIP_TRY(hipStreamCreateWithFlags(&g.own_stream, hipStreamNonBlocking));
     g.stream = g.own_stream;
     for (auto& ev : g.ev_default) HIP_TRY(hipEventCreate(&ev));
+    {
+        const char* e = std::getenv("RT580_PIPELINE");
+        g.pipeline = !(e && std::atoi(e) == 0);
+    }
+    for (auto& sl : g.slot) {
+        HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+    for (auto& ev : g.user_mark) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     g.ev = g.ev_default.data();
     HIP_TRY(hipHostMalloc((void**)&g.needed_host, 64, hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&g.far_count_host, 64, hipHostMallocDefault));
@@ -390,7 +468,7 @@ int rt_gpu_init(int device) {
 
 int rt_gpu_set_stream(void* s) {
     if (!g.inited) return fail("rt_gpu_init not called");
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    if (sync_all()) return RT_FAILURE;
     g.stream = (hipStream_t)s;  // NULL: the HIP null stream (e.g. PyTorch's default stream)
     return RT_SUCCESS;
 }
@@ -410,7 +488,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         if (s->lights[i].kind < RT_LIGHT_DIRECTIONAL || s->lights[i].kind > RT_LIGHT_AMBIENT)
             return fail("light %d: bad kind", i);
     HIP_TRY(hipSetDevice(g.device));
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    if (sync_all()) return RT_FAILURE;  // frames in flight still read the old scene
     if (ensure(g.prims, sizeof(rt_prim) * (size_t)s->n_prims + 64) ||
         ensure(g.shade, sizeof(rt_prim_shade) * (size_t)s->n_prims + 64) ||
         ensure(g.mats, sizeof(rt_material) * (size_t)s->n_materials + 64) ||
@@ -461,27 +539,29 @@ int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     // The RNG offsets need every row before a selected one: render the prefix
     // [0, row_end) and copy the selected rows out when the selection is sparse.
     const int n_rows = prefix ? n_sel : p->row_end;
+    if (begin_slot(frame_uses_bvh(p))) return RT_FAILURE;
     for (int attempt = 0; attempt < 4; attempt++) {
         if (begin_frame()) return RT_FAILURE;
-        HIP_TRY(hipEventRecord(g.ev[EV_START], g.stream));
+        HIP_TRY(hipEventRecord(g.ev[EV_START], fs()));
         if (trace_rows(p, 0, 1, n_rows)) return RT_FAILURE;
         int16_t* out;
         if (prefix) {
-            if (ensure(g.fb, (size_t)n_rows * p->width * 6)) return RT_FAILURE;
-            out = (int16_t*)g.fb.p;
+            if (ensure(SL.fb, (size_t)n_rows * p->width * 6)) return RT_FAILURE;
+            out = (int16_t*)SL.fb.p;
         } else {
-            if (ensure(g.fb_full, (size_t)n_rows * p->width * 6)) return RT_FAILURE;
-            out = (int16_t*)g.fb_full.p;
+            if (ensure(SL.fb_full, (size_t)n_rows * p->width * 6)) return RT_FAILURE;
+            out = (int16_t*)SL.fb_full.p;
         }
         if (shade_rows(p, 0, 1, n_rows, nullptr, out)) return RT_FAILURE;
         if (!prefix) {
-            if (ensure(g.fb, (size_t)n_sel * p->width * 6)) return RT_FAILURE;
-            HIP_TRY(launch_copy_rows(out, p->width, p->row_begin, p->row_step, n_sel, (int16_t*)g.fb.p, g.stream));
+            if (ensure(SL.fb, (size_t)n_sel * p->width * 6)) return RT_FAILURE;
+            HIP_TRY(launch_copy_rows(out, p->width, p->row_begin, p->row_step, n_sel, (int16_t*)SL.fb.p, fs()));
         }
         bool retry = false;
         if (check_capacity(p, retry)) return RT_FAILURE;
         if (!retry) {
-            if (fb_device) *fb_device = (int16_t*)g.fb.p;
+            if (end_slot()) return RT_FAILURE;
+            if (fb_device) *fb_device = (int16_t*)SL.fb.p;
             return RT_SUCCESS;
         }
         if (g.profiling) g.prof_frames--;
@@ -503,9 +583,10 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
     if (!row_calls_device) return fail("row_calls_device is NULL");
     HIP_TRY(hipSetDevice(g.device));
     const int n_rows = n_selected_rows(p);
+    if (begin_slot(frame_uses_bvh(p))) return RT_FAILURE;
     for (int attempt = 0; attempt < 4; attempt++) {
         if (begin_frame()) return RT_FAILURE;
-        HIP_TRY(hipEventRecord(g.ev[EV_START], g.stream));
+        HIP_TRY(hipEventRecord(g.ev[EV_START], fs()));
         if (trace_rows(p, p->row_begin, p->row_step, n_rows)) return RT_FAILURE;
         bool retry = false;
         if (check_capacity(p, retry)) return RT_FAILURE;
@@ -514,8 +595,9 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
         if (g.profiling) g.prof_frames--;
     }
     if (n_rows)
-        HIP_TRY(hipMemcpyAsync(row_calls_device, g.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToDevice,
-                               g.stream));
+        HIP_TRY(hipMemcpyAsync(row_calls_device, SL.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToDevice,
+                               fs()));
+    if (end_slot()) return RT_FAILURE;  // the caller's stream (all-gather) sees the counts
     g.split_params = *p;
     g.split_ready = true;
     return RT_SUCCESS;
@@ -530,7 +612,9 @@ int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device
         return fail("rt_gpu_shade_rows must follow rt_gpu_count_rows with the same params");
     HIP_TRY(hipSetDevice(g.device));
     g.split_ready = false;
-    return shade_rows(p, p->row_begin, p->row_step, n_selected_rows(p), row_base_device, fb_device);
+    if (slot_wait_user()) return RT_FAILURE;  // the row bases were produced on the caller's stream
+    if (shade_rows(p, p->row_begin, p->row_step, n_selected_rows(p), row_base_device, fb_device)) return RT_FAILURE;
+    return end_slot();
 }
 
 int rt_gpu_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out) {
@@ -579,13 +663,13 @@ int rt_gpu_last_stats(rt_render_stats* st) {
     if (!st) return RT_INVALID_ARG;
     std::memset(st, 0, sizeof *st);
     if (!g.last_valid) return fail("no frame rendered yet");
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    if (sync_all()) return RT_FAILURE;
     const int n = g.last_rows;
     std::vector<uint32_t> rc(n), rh(n), rn(n);
     if (n) {
-        HIP_TRY(hipMemcpy(rc.data(), g.row_calls.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(rh.data(), g.row_hits.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(rn.data(), g.row_nodes.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(rc.data(), SL.row_calls.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(rh.data(), SL.row_hits.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(rn.data(), SL.row_nodes.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     }
     uint64_t calls = 0, hits = 0, tree = 0;
     for (int i = 0; i < n; i++) { calls += rc[i]; hits += rh[i]; tree += rn[i]; }
@@ -606,7 +690,7 @@ int rt_gpu_last_stats(rt_render_stats* st) {
 
 int rt_gpu_profile(int enable) {
     if (!g.inited) return fail("rt_gpu_init not called");
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    if (sync_all()) return RT_FAILURE;
     // keep g.ev on the last profiled frame's events so rt_gpu_last_stats stays valid
     if (enable || g.prof_frames == 0) g.ev = g.ev_default.data();
     g.profiling = enable != 0;
@@ -616,7 +700,7 @@ int rt_gpu_profile(int enable) {
 
 int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double* ms_resolve, int* frames) {
     if (!g.inited) return fail("rt_gpu_init not called");
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    if (sync_all()) return RT_FAILURE;
     double t[4] = {0, 0, 0, 0};
     for (int i = 0; i < g.prof_frames; i++) {
         for (int k = 0; k < 4; k++) {
@@ -638,15 +722,21 @@ const char* rt_gpu_last_error(void) { return g_err; }
 void rt_gpu_shutdown(void) {
     if (!g.inited) return;
     (void)hipSetDevice(g.device);
-    (void)hipStreamSynchronize(g.stream);
+    (void)sync_all();
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
                       &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
-                      &g.hit4, &g.hit_prim, &g.aofix_items, &g.aofix_count})
+                      &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights})
         release(*b);
-    for (DevBuf* b : {&g.prims, &g.shade, &g.mats, &g.lights, &g.nodes, &g.rays, &g.lvl, &g.needed, &g.pix_hits,
-                      &g.pix_nodes, &g.pix_prefix, &g.row_calls, &g.row_hits, &g.row_nodes, &g.row_base_local,
-                      &g.totals, &g.call_node, &g.call_rng, &g.occ, &g.fb, &g.fb_full, &g.mt_stream})
-        release(*b);
+    for (Slot& sl : g.slot) {
+        for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
+                          &sl.row_calls, &sl.row_hits, &sl.row_nodes, &sl.row_base_local, &sl.totals, &sl.call_node,
+                          &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.mt_stream, &sl.aofix_items, &sl.aofix_count})
+            release(*b);
+        if (sl.stream) (void)hipStreamDestroy(sl.stream);
+        if (sl.done) (void)hipEventDestroy(sl.done);
+    }
+    for (auto& ev : g.user_mark)
+        if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : g.ev_default)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& q : g.prof_pool)
