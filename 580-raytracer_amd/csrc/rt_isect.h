@@ -92,12 +92,12 @@ RTM_HD bool sph_test(const rt_prim& P, rv3 o, rv3 d, float& t) {
 
 RTM_HD bool prim_test_closest(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
     a = b = g = 0.0f;
-    return P.kind == RT_PRIM_TRIANGLE ? tri_test<true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+    return P.kind == RT_PRIM_TRIANGLE ? tri_test<true, true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
 }
 
 RTM_HD bool prim_test_any(const rt_prim& P, rv3 o, rv3 d) {
     float t, a, b, g;
-    return P.kind == RT_PRIM_TRIANGLE ? tri_test<false>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+    return P.kind == RT_PRIM_TRIANGLE ? tri_test<false, true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
 }
 
 // ---------------------------------------------------------------- BVH queries
@@ -265,7 +265,7 @@ RTM_HD bool far_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool found) {
             RT_CNT(far_tests, 1);
             const int j = (int)ft.id;
             float t, a, b, g;
-            if (tri_test<true>(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
+            if (tri_test<true, true>(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
                 found = true;
                 h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
             }
@@ -320,7 +320,7 @@ RTM_HD bool bvh_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool with_far = 
             RT_CNT(leaf_tris, n);
             for (int k = c; k < c + n; k++) {
                 float t, a, b, g;
-                if (tri_test<true>(V.prims[k], o, d, t, a, b, g)) {
+                if (tri_test<true, true>(V.prims[k], o, d, t, a, b, g)) {
                     const int id = (int)V.ids[k];
                     if (lex_better(t, id, found, h)) {
                         found = true;
@@ -405,7 +405,7 @@ RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true) {
             RT_CNT(leaf_tris, n);
             for (int k = c; k < c + n; k++) {
                 float t, a, b, g;
-                if (tri_test<false>(V.prims[k], o, d, t, a, b, g)) return true;
+                if (tri_test<false, true>(V.prims[k], o, d, t, a, b, g)) return true;
             }
         }
         if (sp == 0) break;

@@ -23,11 +23,17 @@
 
 using namespace rt580;
 
+// The reference's loop with the plain (dividing) tests: tri_test<..., false>.
+static bool ref_test(const rt_prim& p, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
+    a = b = g = 0.0f;
+    return p.kind == RT_PRIM_TRIANGLE ? tri_test<true, false>(p, o, d, t, a, b, g) : sph_test(p, o, d, t);
+}
+
 static bool brute_closest(const std::vector<rt_prim>& P, rv3 o, rv3 d, Hit& h) {
     bool found = false;
     for (int j = 0; j < (int)P.size(); j++) {
         float t, a, b, g;
-        if (prim_test_closest(P[j], o, d, t, a, b, g) && (!found || t < h.t)) {
+        if (ref_test(P[j], o, d, t, a, b, g) && (!found || t < h.t)) {
             found = true;
             h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
         }
@@ -36,8 +42,9 @@ static bool brute_closest(const std::vector<rt_prim>& P, rv3 o, rv3 d, Hit& h) {
 }
 
 static bool brute_any(const std::vector<rt_prim>& P, rv3 o, rv3 d) {
+    float t, a, b, g;
     for (const rt_prim& p : P)
-        if (prim_test_any(p, o, d)) return true;
+        if (ref_test(p, o, d, t, a, b, g)) return true;
     return false;
 }
 
