@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 namespace rt580 {
 namespace {
@@ -380,6 +381,187 @@ bool bvh_usable(const BvhBuild& b, const float cam_from[3]) {
     if (!(b.scale > 0.0f) || b.n_tri == 0) return false;
     // the bounds hold for any origin; keep the float ranges sane
     return max_abs3(cam_from) <= 1e6f * b.scale;
+}
+
+}  // namespace rt580
+
+namespace rt580 {
+
+// ---------------------------------------------------------------- direction grid
+// A far hit of triangle j (t >= T_j, rt_isect.h far_candidate) for a ray with
+// |o| <= R needs, besides the reference's own t test:
+//  (band)  |N.d| <= eps_j = |num| / (t nd-rounding) <= (R + |D|)(1 + 1e-5) / T_j + 2e-7;
+//  (wedge) the sub-areas through v0 not negative: bb = 0.5 dot(cross(Q, E2), N),
+//          Q = fl(Pp - v0), E2 = fl(v2 - v0) (gg alike with E1 = fl(v1 - v0)). With
+//          the 9.25u|Q||E| arithmetic bound (analyse), Pp = o + d t + dP,
+//          |dP| <= u(2t + |o|), |Q - (Pp - v0)| <= u|Pp - v0|, and t >= T_j:
+//            (d x E2).N >= -|E2| zeta_j,  (E1 x d).N >= -|E1| zeta_j,
+//            zeta_j = ((R + |v0|)(1 + 11u) + uR) / T_j + 12.4u  (x 1.001).
+// (The reference's acceptance is !(bb/area < 0); area > 0 for every far-set
+// triangle, and a quotient rounding to -0 only admits bb >= -area 2^-149, far
+// inside the slack.) So d lies in a thin arc-shaped patch: nearly in the plane
+// and inside the triangle's angle at v0 widened by ~zeta_j.
+// A direction d within chord rho of a cell centre c satisfies each condition
+// only if c does with rho|N| (resp. rho|E||N|) added to the bound; cell radii
+// come from the octahedral decode's Lipschitz bound (<= sqrt6 per map unit:
+// sqrt2 for the unnormalised vector, sqrt3 for normalising it, |v| >= 1/sqrt3)
+// times the cell's half diagonal, plus 1e-6 map units for the device's float
+// cell computation. A quadtree over the map lists every triangle in every cell
+// its patch can reach; the device tests far_candidate + the full reference
+// test on the listed triangles only.
+
+namespace {
+
+void oct_decode(double a, double b, double out[3]) {
+    double x = a, y = b;
+    const double z = 1.0 - std::fabs(a) - std::fabs(b);
+    if (z < 0) {
+        x = (1.0 - std::fabs(b)) * (a < 0 ? -1.0 : 1.0);
+        y = (1.0 - std::fabs(a)) * (b < 0 ? -1.0 : 1.0);
+    }
+    const double l = std::sqrt(x * x + y * y + z * z);
+    out[0] = x / l; out[1] = y / l; out[2] = z / l;
+}
+
+struct GridTri {
+    double n[3], ea[3], eb[3];  // N, E2 x N, N x E1
+    double band, wa, wb;        // eps, |E2| zeta, |E1| zeta
+    double nn, na, nb;          // |N|, |E2||N|, |E1||N|
+};
+
+bool grid_tri(const rt_prim& p, const FarTri& ft, double R, double S, GridTri& g) {
+    const double T = ((double)ft.dhi - (R * 1.0002 + 1.7322 * S)) * 0.9998;
+    if (!(T > 0)) return false;
+    double n[3], e1[3], e2[3], v0 = 0;
+    for (int k = 0; k < 3; k++) {
+        n[k] = p.nrm[k];
+        e1[k] = (double)(p.p1[k] - p.p0[k]);  // fl(v1 - v0), as the reference computes it
+        e2[k] = (double)(p.p2[k] - p.p0[k]);
+        v0 += (double)p.p0[k] * p.p0[k];
+    }
+    v0 = std::sqrt(v0);
+    const double l1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]) * (1 + 1e-9);
+    const double l2 = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]) * (1 + 1e-9);
+    g.nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]) * (1 + 1e-9);
+    const double u = std::ldexp(1.0, -24);
+    g.band = (R + std::fabs((double)p.d)) * (1 + 1e-5) / T + 2e-7;
+    const double zeta = (((R + v0) * (1 + 11 * u) + u * R) / T + 12.4 * u) * 1.001;
+    g.wa = l2 * zeta + 1e-12;
+    g.wb = l1 * zeta + 1e-12;
+    g.na = l2 * g.nn;
+    g.nb = l1 * g.nn;
+    for (int k = 0; k < 3; k++) g.n[k] = n[k];
+    // ea = E2 x N: (c x E2).N = c.(E2 x N); eb = N x E1: (E1 x c).N = c.(N x E1)
+    g.ea[0] = e2[1] * n[2] - e2[2] * n[1];
+    g.ea[1] = e2[2] * n[0] - e2[0] * n[2];
+    g.ea[2] = e2[0] * n[1] - e2[1] * n[0];
+    g.eb[0] = n[1] * e1[2] - n[2] * e1[1];
+    g.eb[1] = n[2] * e1[0] - n[0] * e1[2];
+    g.eb[2] = n[0] * e1[1] - n[1] * e1[0];
+    return true;
+}
+
+// Can a direction within chord rho of c satisfy triangle g's band and wedge?
+bool grid_reach(const GridTri& g, const double c[3], double rho) {
+    const double dn = g.n[0] * c[0] + g.n[1] * c[1] + g.n[2] * c[2];
+    if (std::fabs(dn) > g.band + rho * g.nn + 1e-12) return false;
+    const double da = g.ea[0] * c[0] + g.ea[1] * c[1] + g.ea[2] * c[2];
+    if (da < -(g.wa + rho * g.na)) return false;
+    const double db = g.eb[0] * c[0] + g.eb[1] * c[1] + g.eb[2] * c[2];
+    return !(db < -(g.wb + rho * g.nb));
+}
+
+}  // namespace
+
+void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells) {
+    const auto t0 = std::chrono::steady_clock::now();
+    out.grid_log2 = 0;
+    out.grid_start.clear();
+    out.grid_items.clear();
+    out.grid_always.clear();
+    if (out.far_tris.empty() || log2_cells <= 0) return;
+    const int L = log2_cells, M = 1 << L;
+    const double S = out.scale;
+    const double R = 4.0 * S;  // origins on (or 0.2 off) the scene's surfaces; farther ones walk the plane tree
+    std::vector<GridTri> gt(out.far_tris.size());
+    std::vector<uint8_t> ok(out.far_tris.size());
+    for (size_t k = 0; k < out.far_tris.size(); k++) {
+        const FarTri& ft = out.far_tris[k];
+        ok[k] = prims[ft.id].area > 0.0f && grid_tri(prims[ft.id], ft, R, S, gt[k]);
+        if (!ok[k]) out.grid_always.push_back((uint32_t)k);
+    }
+    // node radius (chord) of a map square of side 2/2^level, centre decoded
+    auto rho_of = [](int level) { return std::sqrt(6.0) * (std::sqrt(0.5) * 2.0 / (double)(1 << level) + 1e-6); };
+    unsigned nt = std::thread::hardware_concurrency();
+    if (nt < 1) nt = 1;
+    if (nt > 16) nt = 16;
+    const size_t n = out.far_tris.size(), ncell = (size_t)M * M;
+    // two passes over the same deterministic descent: per-thread counts per
+    // cell, then each thread fills its slice of every cell (ascending k per cell)
+    std::vector<std::vector<uint32_t>> cnt(nt, std::vector<uint32_t>(ncell, 0));
+    auto descend = [&](unsigned w, bool fill, std::vector<uint32_t>& cursor) {
+        const size_t lo = n * w / nt, hi = n * (w + 1) / nt;
+        struct Node { int level, i, j; };
+        std::vector<Node> stk;
+        for (size_t k = lo; k < hi; k++) {
+            if (!ok[k]) continue;
+            const GridTri& g = gt[k];
+            stk.clear();
+            for (int i = 0; i < 2; i++)
+                for (int j = 0; j < 2; j++) stk.push_back({1, i, j});
+            while (!stk.empty()) {
+                const Node nd = stk.back();
+                stk.pop_back();
+                const double side = 2.0 / (double)(1 << nd.level);
+                double c[3];
+                oct_decode(-1.0 + (nd.i + 0.5) * side, -1.0 + (nd.j + 0.5) * side, c);
+                if (!grid_reach(g, c, rho_of(nd.level))) continue;
+                if (nd.level == L) {
+                    const size_t cell = (size_t)nd.i * M + nd.j;
+                    if (fill) out.grid_items[cursor[cell]++] = (uint32_t)k;
+                    else cnt[w][cell]++;
+                    continue;
+                }
+                for (int a = 0; a < 2; a++)
+                    for (int b = 0; b < 2; b++) stk.push_back({nd.level + 1, 2 * nd.i + a, 2 * nd.j + b});
+            }
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        std::vector<uint32_t> none;
+        for (unsigned w = 0; w < nt; w++) th.emplace_back([&, w] { std::vector<uint32_t> c; descend(w, false, c); });
+        for (auto& t : th) t.join();
+    }
+    out.grid_start.assign(ncell + 1, 0);
+    uint64_t total = 0;
+    for (size_t c = 0; c < ncell; c++) {
+        out.grid_start[c] = (uint32_t)total;
+        for (unsigned w = 0; w < nt; w++) total += cnt[w][c];
+        if (total > 0xffffffffull) {  // beyond 32-bit offsets: keep the plane tree
+            out.grid_start.clear();
+            return;
+        }
+    }
+    out.grid_start[ncell] = (uint32_t)total;
+    out.grid_items.assign(total, 0);
+    {
+        std::vector<std::thread> th;
+        for (unsigned w = 0; w < nt; w++)
+            th.emplace_back([&, w] {
+                std::vector<uint32_t> cursor(ncell);
+                for (size_t c = 0; c < ncell; c++) {
+                    uint32_t off = out.grid_start[c];
+                    for (unsigned v = 0; v < w; v++) off += cnt[v][c];
+                    cursor[c] = off;
+                }
+                descend(w, true, cursor);
+            });
+        for (auto& t : th) t.join();
+    }
+    out.grid_log2 = L;
+    out.grid_r = (float)R;
+    out.grid_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 }  // namespace rt580

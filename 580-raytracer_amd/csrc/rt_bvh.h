@@ -15,20 +15,24 @@
 // dominated by rounding (measured: ~2.5e-4 of AO rays on a 100k-triangle
 // scene get such a "far hit" at t ~ 1e6-1e7). A culling structure must keep
 // those. Per triangle j (edges e_min..e_max, smallest angle a_min,
-// s = sin(a_min/2)), with u = 2^-24 and kappa = 16 + 4/sin(a_min):
-//   |computed sub-area - exact| <= kappa*u*|a||b|  (a, b = v - Pp, |.| <= D + e')
-//   exact negative sub-area of a point at in-plane distance D outside
-//     >= e_min * s * D / 2
+// s = sin(a_min/2)), with u = 2^-24 and kappa = 9.25 (rt_bvh.cpp analyse):
+//   |computed 2*sub-area - exact| <= kappa*u*|a||b|  (a, b = v - Pp, |.| <= D + e')
+//   exact most negative 2*sub-area of a point at in-plane distance D outside
+//     <= -G * D   (G from the edges and angles)
 // so an accepted hit point is either within D_lo of the triangle ("near") or
-// at distance >= D_hi ("far"), the roots of kappa*u*(D + e')^2 = e_min*s*D.
+// at distance >= D_hi ("far"), the roots of kappa*u*(D + e')^2 = G*D.
 //   near hits: found by a spatial BVH whose triangle boxes are inflated by
 //     delta_j >= 2 D_lo and tested with a "fat ray" (box grown by alpha + beta t
 //     covering the float error of the hit point and of the slab arithmetic,
 //     rt_isect.h), conservative at every t;
-//   far hits (t >= T_j = D_hi(j) - |o| - sqrt3*S): found by a second tree over
-//     the triangles' planes (normal boxes + D ranges) that enumerates every
-//     plane the ray crosses beyond T_j, with exact interval padding; those
-//     candidates get the full reference test.
+//   far hits (t >= T_j = D_hi(j) - |o| - sqrt3*S): candidates are planes the
+//     ray crosses beyond T_j. For origins near the scene they come from a
+//     direction grid: a far hit needs the ray nearly parallel to the plane AND
+//     pointing into the triangle's angle at v0 (the two sub-areas through v0
+//     are computed accurately), a thin arc of directions per triangle, listed
+//     in every octahedral direction cell it touches (build_dir_grid). Other
+//     origins walk a second tree over the triangles' planes (normal boxes + D
+//     ranges) with exact interval padding. Candidates get the full reference test.
 // Triangles for which the analysis does not give a usable split (degenerate,
 // or D_hi below 8 S) and all spheres are tested brute force for every ray.
 #pragma once
@@ -89,11 +93,24 @@ struct BvhBuild {
     float dhi_median = 0.0f;        // typical D_hi (routing of far-origin rays)
     double inflate = 0.0;           // delta_j / e_min(j)
     double build_ms = 0.0;
+    // Direction grid for the far search (build_dir_grid): for rays with |o| <= grid_r,
+    // the far_tris entries (indices) that can give a far hit for a direction in
+    // each octahedral cell; grid_always: entries to test for every such ray.
+    int grid_log2 = 0;              // M = 2^grid_log2 cells per axis; 0: no grid
+    float grid_r = 0.0f;
+    std::vector<uint32_t> grid_start;   // [M*M + 1]
+    std::vector<uint32_t> grid_items;
+    std::vector<uint32_t> grid_always;
+    double grid_ms = 0.0;
 };
 
 // Build over prims[0..n). Returns false if there are no triangles or a tree
 // would exceed the device stack (the caller then keeps brute force).
 bool build_bvh(const rt_prim* prims, int n, BvhBuild& out);
+
+// Build the far-search direction grid over out.far_tris (after build_bvh; the
+// query side is rt_isect.h grid_cell / far_any / far_closest).
+void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells);
 
 // Render-time guard for the camera (float ranges only; the bounds hold for any origin).
 bool bvh_usable(const BvhBuild& b, const float cam_from[3]);

@@ -114,7 +114,36 @@ struct BvhView {
     float dhi_median;           // typical D_hi (routing of far-origin rays)
     int has_tree, has_far;
     float scale;                // S
+    // far-search direction grid (rt_bvh.h build_dir_grid); grid_log2 == 0: none
+    const uint32_t* grid_start;
+    const uint32_t* grid_items;
+    const uint32_t* grid_always;
+    int n_always;
+    int grid_log2;
+    float grid_r;
 };
+
+// Octahedral cell of direction d, 2^L cells per axis: map coordinate
+// x = d.x / (|d.x| + |d.y| + |d.z|) (folded for d.z < 0), cell floor((x/2 + 1/2) 2^L).
+// build_dir_grid's cell radii allow 1e-6 map units for these float roundings.
+RTM_HD uint32_t grid_cell(rv3 d, int L) {
+    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float x = d.x / s, y = d.y / s;
+    if (d.z < 0.0f) {
+        const float ax = fabsf(x), ay = fabsf(y);
+        x = (1.0f - ay) * (x < 0.0f ? -1.0f : 1.0f);
+        y = (1.0f - ax) * (y < 0.0f ? -1.0f : 1.0f);
+    }
+    const float m = (float)(1 << L);
+    const uint32_t i = (uint32_t)fminf(fmaxf((x * 0.5f + 0.5f) * m, 0.0f), m - 1.0f);
+    const uint32_t j = (uint32_t)fminf(fmaxf((y * 0.5f + 0.5f) * m, 0.0f), m - 1.0f);
+    return (i << L) | j;
+}
+
+// Does this origin use the direction grid (|o| <= grid_r, with the float norm's rounding)?
+RTM_HD bool grid_origin(const BvhView& V, rv3 o) {
+    return V.grid_log2 > 0 && sqrtf(o.x * o.x + o.y * o.y + o.z * o.z) * 1.0001f <= V.grid_r;
+}
 
 #define RT_U 5.9604644775390625e-08f  // 2^-24
 
@@ -244,6 +273,24 @@ RTM_HD bool far_candidate(const FarTri& ft, const FarRay& r, rv3 o, rv3 d) {
 RTM_HD bool far_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool found) {
     if (dir_zero(d)) return found;
     const FarRay fr = far_ray(V, o);
+    if (grid_origin(V, o)) {
+        const uint32_t cell = grid_cell(d, V.grid_log2);
+        const uint32_t b = V.grid_start[cell], e = V.grid_start[cell + 1];
+        const int n_list = (int)(e - b);
+        for (int q = -V.n_always; q < n_list; q++) {
+            const FarTri& ft = V.far_tris[q < 0 ? V.grid_always[q + V.n_always] : V.grid_items[b + (uint32_t)q]];
+            RT_CNT(far_cands, 1);
+            if (!far_candidate(ft, fr, o, d)) continue;
+            RT_CNT(far_tests, 1);
+            const int j = (int)ft.id;
+            float t, a, bb, g;
+            if (tri_test<true, true>(V.all[j], o, d, t, a, bb, g) && lex_better(t, j, found, h)) {
+                found = true;
+                h.t = t; h.a = a; h.b = bb; h.g = g; h.prim = j;
+            }
+        }
+        return found;
+    }
     int32_t fstk[RT_BVH_STACK];
     int fsp = 0;
     fstk[fsp++] = 0;
@@ -348,6 +395,17 @@ RTM_HD bool bvh_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool with_far = 
 RTM_HD bool far_any(const BvhView& V, rv3 o, rv3 d) {
     if (dir_zero(d)) return false;
     const FarRay fr = far_ray(V, o);
+    if (grid_origin(V, o)) {
+        const uint32_t cell = grid_cell(d, V.grid_log2);
+        const uint32_t b = V.grid_start[cell], e = V.grid_start[cell + 1];
+        const int n_list = (int)(e - b);
+        for (int q = -V.n_always; q < n_list; q++) {
+            const FarTri& ft = V.far_tris[q < 0 ? V.grid_always[q + V.n_always] : V.grid_items[b + (uint32_t)q]];
+            RT_CNT(far_cands, 1);
+            if (far_candidate(ft, fr, o, d) && prim_test_any(V.all[ft.id], o, d)) return true;
+        }
+        return false;
+    }
     int32_t fstk[RT_BVH_STACK];
     int fsp = 0;
     fstk[fsp++] = 0;

@@ -956,6 +956,53 @@ __global__ void __launch_bounds__(TB) ao_near_kernel(DevScene S, DevFrame F, Dev
 }
 
 // ---------------------------------------------------------------- far-hit pass
+// Direction-grid candidates (rt_bvh.h build_dir_grid) of a lane whose origin is
+// within grid_r: the "always" entries, then its cell's list. When every grid
+// lane of the wave shares one cell, the list is read with wave-uniform scalar
+// loads. Each candidate gets far_candidate + the full reference test.
+template <bool CLOSEST>
+__device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o, rv3 d, const FarRay& fr, Hit& h,
+                                              bool& found) {
+    const BvhView& V = S.bv;
+    bool hit = false;
+    const uint32_t cell = gl ? grid_cell(d, V.grid_log2) : 0u;
+    const uint64_t glm = __ballot(gl);
+    uint32_t c0 = 0;
+    bool uniform = false;
+    if (glm) {
+        c0 = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)cell, __ffsll((unsigned long long)glm) - 1));
+        uniform = __ballot(gl && cell != c0) == 0;
+    }
+    auto test = [&](const FarTri& ft, bool uni) {
+        if (!(gl && !(CLOSEST ? false : hit))) return;
+        if (!far_candidate(ft, fr, o, d)) return;
+        const rt_prim P = uni ? load_prim_scalar(S.prims, (int)ft.id) : S.prims[ft.id];
+        if (CLOSEST) {
+            float t, a, b, g;
+            if (tri_test<true, true>(P, o, d, t, a, b, g) && lex_better(t, (int)ft.id, found, h)) {
+                found = true;
+                hit = true;
+                h.t = t; h.a = a; h.b = b; h.g = g; h.prim = (int)ft.id;
+            }
+        } else if (prim_test_any(P, o, d)) {
+            hit = true;
+        }
+    };
+    for (int q = 0; q < V.n_always; q++) test(load_far_tri(V.far_tris, (int)V.grid_always[q]), true);
+    if (uniform) {
+        const uint32_t b = V.grid_start[c0], e = V.grid_start[c0 + 1];
+        for (uint32_t k = b; k < e; k++) {
+            if (!CLOSEST && __ballot(gl && !hit) == 0) break;
+            const uint32_t idx = __builtin_amdgcn_readfirstlane(V.grid_items[k]);
+            test(load_far_tri(V.far_tris, (int)idx), true);
+        }
+    } else if (gl) {
+        const uint32_t b = V.grid_start[cell], e = V.grid_start[cell + 1];
+        for (uint32_t k = b; k < e && (CLOSEST || !hit); k++) test(V.far_tris[V.grid_items[k]], false);
+    }
+    return hit;
+}
+
 // The queued AO rays, sorted by direction key, 64 per wave: the wave walks the
 // plane tree once for all its lanes (a node is entered if any live lane may
 // have a far hit below it), each lane evaluating the exact tests of rt_isect.h
@@ -978,6 +1025,13 @@ __global__ void __launch_bounds__(TB) far_any_kernel(DevScene S, DevWork W, uint
         }
         const FarRay fr = far_ray(S.bv, o);
         bool hit = false;
+        {
+            const bool gl = live && grid_origin(S.bv, o);
+            Hit hd;
+            bool fd = false;
+            if (far_grid_lane<false>(S, gl, o, d, fr, hd, fd)) hit = true;
+            if (gl) live = false;  // done: the tree walk below serves the other lanes
+        }
         int sp = 0;
         stk[wave][sp++] = 0;  // every lane writes the same value: no cross-lane ordering needed
         while (sp > 0) {
@@ -1150,13 +1204,16 @@ __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, 
         }
         const FarRay fr = far_ray(S.bv, o);
         bool changed = false;
+        const bool gl = live && grid_origin(S.bv, o);
+        if (far_grid_lane<true>(S, gl, o, d, fr, h, found)) changed = true;
+        const bool walk = live && !gl;
         int sp = 0;
         stk[wave][sp++] = 0;
         while (sp > 0) {
             const int fnode = __builtin_amdgcn_readfirstlane(stk[wave][--sp]);
             const FarNode fn = load_far_node(S.bv.far_nodes, fnode);
             float T;
-            const bool may = live && far_node_may(fn, fr, o, d, T) && !(found && h.t < T);
+            const bool may = walk && far_node_may(fn, fr, o, d, T) && !(found && h.t < T);
             if (__ballot(may) == 0) continue;
             if (fn.count == 0) {
                 stk[wave][sp++] = fn.first + 1;

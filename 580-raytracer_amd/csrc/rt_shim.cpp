@@ -49,9 +49,10 @@ struct State {
     int n_prims = 0, n_lights = 0, n_ambient = 0, n_nonambient = 0;
     bool have_scene = false;
     // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
-    DevBuf bvh_nodes, bvh_prims, bvh_ids, far_nodes, far_tris, brute;
+    DevBuf bvh_nodes, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always;
     BvhBuild bvh;
     bool bvh_ok = false;
+    int grid_log2 = 0, grid_n_always = 0;  // far-search direction grid (uploaded; host copy dropped)
     int accel = RT_ACCEL_AUTO;
     bool last_accel = false;
     uint64_t scene_gen = 0;
@@ -224,6 +225,12 @@ DevScene dev_scene(const rt_render_params* p) {
         if (diag & 1) v.has_far = 0;
     }
     v.scale = g.bvh.scale;
+    v.grid_start = (const uint32_t*)g.grid_start.p;
+    v.grid_items = (const uint32_t*)g.grid_items.p;
+    v.grid_always = (const uint32_t*)g.grid_always.p;
+    v.n_always = g.grid_n_always;
+    v.grid_log2 = g.grid_log2;
+    v.grid_r = g.bvh.grid_r;
     return s;
 }
 
@@ -505,17 +512,29 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     // exact BVH for triangle scenes that do not fit one LDS tile (rt_bvh.h)
     g.bvh = BvhBuild();
     g.bvh_ok = false;
+    g.grid_log2 = g.grid_n_always = 0;
     if (s->n_prims > 64) {
         g.bvh_ok = build_bvh(s->prims, s->n_prims, g.bvh);
+        // far-search direction grid, 1024^2 cells (RT580_GRID_LOG2: other sizes, 0 = plane tree only)
+        int glog2 = 10;
+        if (const char* e = std::getenv("RT580_GRID_LOG2")) glog2 = std::atoi(e);
+        if (g.bvh_ok && glog2 > 0 && glog2 <= 12) build_dir_grid(s->prims, g.bvh, glog2);
         if (g.bvh_ok && (upload_vec(g.bvh_nodes, g.bvh.nodes) || upload_vec(g.bvh_prims, g.bvh.prims) ||
                          upload_vec(g.bvh_ids, g.bvh.ids) || upload_vec(g.far_nodes, g.bvh.far_nodes) ||
-                         upload_vec(g.far_tris, g.bvh.far_tris) || upload_vec(g.brute, g.bvh.brute)))
+                         upload_vec(g.far_tris, g.bvh.far_tris) || upload_vec(g.brute, g.bvh.brute) ||
+                         upload_vec(g.grid_start, g.bvh.grid_start) || upload_vec(g.grid_items, g.bvh.grid_items) ||
+                         upload_vec(g.grid_always, g.bvh.grid_always)))
             return RT_FAILURE;
+        g.grid_log2 = g.bvh.grid_start.empty() ? 0 : g.bvh.grid_log2;
+        g.grid_n_always = (int)g.bvh.grid_always.size();
         // the device needs only the arrays; keep the host copy small
         g.bvh.prims = std::vector<rt_prim>();
         g.bvh.ids = std::vector<uint32_t>();
         g.bvh.n_far = (int)g.bvh.far_tris.size();
         g.bvh.far_tris = std::vector<FarTri>();
+        g.bvh.grid_start = std::vector<uint32_t>();
+        g.bvh.grid_items = std::vector<uint32_t>();
+        g.bvh.grid_always = std::vector<uint32_t>();
     }
     HIP_TRY(hipStreamSynchronize(g.stream));
     g.n_prims = s->n_prims;
@@ -723,6 +742,8 @@ void rt_gpu_shutdown(void) {
     if (!g.inited) return;
     (void)hipSetDevice(g.device);
     (void)sync_all();
+    for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always})
+        release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
                       &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
                       &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights})

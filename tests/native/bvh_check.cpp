@@ -90,6 +90,17 @@ int main(int argc, char** argv) {
     V.has_tree = !B.nodes.empty();
     V.has_far = !B.far_nodes.empty();
     V.scale = B.scale;
+    // far search: the direction grid (default) or, with RT_FAR_TREE=1, the plane tree only
+    const bool use_grid = !(std::getenv("RT_FAR_TREE") && std::atoi(std::getenv("RT_FAR_TREE")) == 1);
+    if (use_grid) build_dir_grid(P.data(), B, 10);
+    V.grid_start = B.grid_start.empty() ? nullptr : B.grid_start.data();
+    V.grid_items = B.grid_items.data();
+    V.grid_always = B.grid_always.data();
+    V.n_always = (int)B.grid_always.size();
+    V.grid_log2 = B.grid_start.empty() ? 0 : B.grid_log2;
+    V.grid_r = B.grid_r;
+    std::printf("grid log2=%d r=%g items=%zu always=%zu build_ms=%.1f\n", V.grid_log2, V.grid_r, B.grid_items.size(),
+                B.grid_always.size(), B.grid_ms);
 
     const long nrays = std::atol(argv[3]);
     const unsigned seed = argc > 4 ? (unsigned)std::atoi(argv[4]) : 580u;

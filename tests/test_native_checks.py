@@ -61,15 +61,21 @@ def test_eps_compares_and_float_to_short_all_floats():
 CSRC = os.path.join(helpers.PKG, "csrc")
 
 
+@pytest.mark.parametrize("far", ["grid", "tree"])
 @pytest.mark.parametrize("scene,rays", [("cornell10k", 60000), ("field100k", 4000)])
-def test_bvh_queries_equal_brute_force(scene, rays):
-    """The exact-semantics BVH (rt_bvh.h / rt_isect.h) against the reference's
+def test_bvh_queries_equal_brute_force(scene, rays, far):
+    """The exact-semantics BVH (rt_bvh.h / rt_isect.h), with the far search by
+    direction grid or by plane tree, against the reference's
     brute-force IntersectScene loop on camera, AO, reflection and grazing rays:
     same primitive, bit-identical t and barycentrics, same any-hit boolean. The
     grazing rays provoke the reference's far "hits" (rt_bvh.h), which only the
     plane-tree search finds: the control count without it must be non-zero."""
     root = helpers.synthetic_root(scene)
     exe = _build("bvh_check", [os.path.join(CSRC, "rt_scene.cpp"), os.path.join(CSRC, "rt_bvh.cpp")])
-    out = _run(exe, root, scene + ".json", str(rays))
+    env = dict(os.environ, RT_FAR_TREE="1" if far == "tree" else "0")
+    p = subprocess.run([exe, root, scene + ".json", str(rays)], capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0 and "mismatches=0" in p.stdout, p.stdout + p.stderr
+    out = p.stdout
+    assert ("grid log2=10" in out) == (far == "grid"), out
     if scene == "cornell10k":
         assert "differ_without_far_search=0 " not in out, out
