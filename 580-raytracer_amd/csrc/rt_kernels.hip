@@ -1110,12 +1110,26 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
         const FarRay fr = far_ray(S.bv, o);
         if (!closest) {
             bool hit = false;
-            for (int k0 = 0; k0 < n_scan; k0 += 64) {
+            if (brute) {
+                // 4 records per lane in flight per step (256 per wave), then one
+                // ballot; any order gives the same boolean
+                for (int k0 = 0; k0 < n_scan; k0 += 256) {
+                    rt_prim p[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int k = k0 + u * 64 + lane;
+                        if (k < n_scan) p[u] = S.prims[k];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (k0 + u * 64 + lane < n_scan && prim_test_any(p[u], o, d)) hit = true;
+                    if (__ballot(hit)) break;
+                }
+            }
+            for (int k0 = 0; !brute && k0 < n_scan; k0 += 64) {
                 const int k = k0 + lane;
                 if (k < n_scan) {
-                    if (brute) {
-                        if (prim_test_any(S.prims[k], o, d)) hit = true;
-                    } else {
+                    {
                         const FarTri ft = S.bv.far_tris[k];
                         if (far_candidate(ft, fr, o, d) && prim_test_any(S.prims[ft.id], o, d)) hit = true;
                     }
@@ -1693,6 +1707,18 @@ static int ao_variant() {
     return v;
 }
 
+// Workgroups of the grid-stride small-scene AO launch (RT580_AO_GRID for A/B;
+// 8192 = 32 per CU; 2048-32768 measured within 2 % of each other on config 2).
+static unsigned ao_grid() {
+    static int g = -1;
+    if (g < 0) {
+        const char* e = getenv("RT580_AO_GRID");
+        g = e ? atoi(e) : 8192;
+        if (g < 256 || g > (1 << 20)) g = 8192;
+    }
+    return (unsigned)g;
+}
+
 hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t b, uint64_t e,
                          hipStream_t s);
 hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v);
@@ -1758,7 +1784,7 @@ hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W,
 hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v) {
     if (v & 16) {
         switch (v & ~16) {
-#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
+#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(ao_grid()), dim3(TB), 0, s, S, F, W); break;
             RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8) RT_AO_CASE(1032) RT_AO_CASE(2056) RT_AO_CASE(3080)
             RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128) RT_AO_CASE(7180) RT_AO_CASE(7182)
 #undef RT_AO_CASE
