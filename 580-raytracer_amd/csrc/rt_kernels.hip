@@ -1097,6 +1097,9 @@ __global__ void __launch_bounds__(TB) far_closest_lane_kernel(DevScene S, DevWor
 // for sparse queues, where sorted waves no longer share directions.
 // brute != 0: every primitive in scene order with the plain tests (the
 // reference's IntersectScene loop), for the far-origin rays.
+#ifndef BRUTE_ANY_U
+#define BRUTE_ANY_U 2  // far_scan_kernel brute any-hit: records per lane per ballot step
+#endif
 __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uint32_t first, uint32_t n, int closest,
                                                       int n_far, int brute) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1111,17 +1114,17 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
         if (!closest) {
             bool hit = false;
             if (brute) {
-                // 4 records per lane in flight per step (256 per wave), then one
+                // BRUTE_ANY_U records per lane in flight per step, then one
                 // ballot; any order gives the same boolean
-                for (int k0 = 0; k0 < n_scan; k0 += 256) {
-                    rt_prim p[4];
+                for (int k0 = 0; k0 < n_scan; k0 += BRUTE_ANY_U * 64) {
+                    rt_prim p[BRUTE_ANY_U];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
+                    for (int u = 0; u < BRUTE_ANY_U; u++) {
                         const int k = k0 + u * 64 + lane;
                         if (k < n_scan) p[u] = S.prims[k];
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; u++)
+                    for (int u = 0; u < BRUTE_ANY_U; u++)
                         if (k0 + u * 64 + lane < n_scan && prim_test_any(p[u], o, d)) hit = true;
                     if (__ballot(hit)) break;
                 }
