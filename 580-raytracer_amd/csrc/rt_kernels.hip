@@ -955,6 +955,24 @@ __global__ void __launch_bounds__(TB) ao_near_kernel(DevScene S, DevFrame F, Dev
     ao_body<512 | 1024 | 2048 | 4096>(S, F, W, b, e);
 }
 
+// Occupancy-capped flavours of ao_near_kernel (RT580_NEAR_WPE=0|5|6|8 for A/B;
+// 100k 1080p AO time: uncapped 169 ms (103 VGPRs, 4 waves/SIMD), 5: 161 ms, 6: 158 ms,
+// 8: 149 ms; the spills of the capped builds cost less than the latency they hide).
+template <int WPE>
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
+ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
+    ao_body<512 | 1024 | 2048 | 4096>(S, F, W, b, e);
+}
+
+static int near_wpe() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_NEAR_WPE");
+        v = e ? atoi(e) : 8;
+    }
+    return v;
+}
+
 // ---------------------------------------------------------------- far-hit pass
 // Direction-grid candidates (rt_bvh.h build_dir_grid) of a lane whose origin is
 // within grid_r: the "always" entries, then its cell's list. When every grid
@@ -1742,7 +1760,15 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             const uint64_t e1 = b + chunk < items ? b + chunk : items;
             if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(W.aofix_count, 0, 4, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+            const int wpe = near_wpe();
+            if (wpe == 5)
+                hipLaunchKernelGGL(ao_near_kernel_w<5>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+            else if (wpe == 6)
+                hipLaunchKernelGGL(ao_near_kernel_w<6>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+            else if (wpe == 8)
+                hipLaunchKernelGGL(ao_near_kernel_w<8>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+            else
+                hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             // exact recompute of the fast pass's failing samples; their misses join the far queue
             if ((e = launch_ao_fix(S, F, W, b, e1, s)) != hipSuccess) return e;
