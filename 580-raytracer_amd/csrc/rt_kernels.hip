@@ -1025,7 +1025,10 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
 // plane tree once for all its lanes (a node is entered if any live lane may
 // have a far hit below it), each lane evaluating the exact tests of rt_isect.h
 // for its own ray. Same candidates, same full tests as bvh_any's far search.
-__global__ void __launch_bounds__(TB) far_any_kernel(DevScene S, DevWork W, uint32_t n) {
+#ifndef FAR_ANY_WPE
+#define FAR_ANY_WPE 8
+#endif
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE))) far_any_kernel(DevScene S, DevWork W, uint32_t n) {
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * TB;
