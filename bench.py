@@ -217,9 +217,12 @@ def main():
         value = rays_frame * args.steps / dt / 1e6
         bytes_per_ray = 56 * n_tri + 16 * n_sph  # SoA primitive records, no reuse
         # dominant kernel: ao_kernel (one launch = this rank's AO rays of a frame)
-        # or, when it takes longer, trace_kernel (camera, reflection/refraction and
-        # shadow rays of all levels; per-level launches summed)
-        if per_frame[0] > per_frame[2]:
+        # or, when it takes clearly longer, trace_kernel (camera, reflection/refraction
+        # and shadow rays of all levels; per-level launches summed). With frame
+        # pipelining the trace events of frame k+1 span time shared with frame k's
+        # AO kernel, so they overstate trace's own GPU time (config 2: 1.36 ms by
+        # events vs 0.65 ms by rocprofv3); trace counts as dominant only above 2x.
+        if per_frame[0] > 2.0 * per_frame[2]:
             kname, kms = "trace_kernel", per_frame[0]
             krays = int(local["rays_primary"]) + int(local["rays_secondary"]) + int(local["rays_shadow"])
         else:
