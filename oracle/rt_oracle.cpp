@@ -6,6 +6,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -13,6 +14,7 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 // JSON tokenizer shared with the product loader (pure syntax; the scene
@@ -24,6 +26,11 @@ namespace ora {
 static const double kPI = 3.14159265;          // Raytracer.h:11
 static const double kEPS = 1e-6;               // Raytracer.h:12
 static const float kOFFSET = (float)0.2;       // SHADOW_CLIPPING_OFFSET, Raytracer.h:13 (used as float arg)
+
+// 0: hoisted (ray-invariant triangle data computed once per load; the default);
+// 1: ref-faithful cost model (oracle_set_mode; for the CPU baseline).
+static int g_faithful = 0;
+static volatile float g_sink;
 
 // ---------------------------------------------------------------- Vector3 (Raytracer.h:39-149)
 struct V3 {
@@ -89,8 +96,7 @@ struct M4 {
     static float det4(const M4& a) {  // Raytracer.h:257-274
         float det = 0;
         for (int i = 0; i < 4; i++) {
-            M4 sub;
-            std::memset(&sub, 0, sizeof sub);
+            M4 sub;  // uninitialised, as the reference's Matrix (no constructor); det3 reads the written 3x3
             for (int j = 1; j < 4; j++)
                 for (int k = 0; k < 4; k++) {
                     if (k < i) sub.m[j - 1][k] = a.m[j][k];
@@ -100,14 +106,10 @@ struct M4 {
         }
         return det;
     }
-    static bool inverse(const M4& a, M4& r) {  // Raytracer.h:276-296, :354-370
-        float det = det4(a);
-        if (std::fabs(det) < 1e-10) return false;
-        M4 adj;
+    static void adjoint(const M4& a, M4& adj) {  // Raytracer.h:276-296 (transposed cofactors)
         for (int i = 0; i < 4; i++)
             for (int j = 0; j < 4; j++) {
                 M4 sub;
-                std::memset(&sub, 0, sizeof sub);
                 int si = 0;
                 for (int k = 0; k < 4; k++) {
                     if (k == i) continue;
@@ -123,6 +125,12 @@ struct M4 {
                 if ((i + j) % 2 != 0) c = -c;
                 adj.m[j][i] = c;
             }
+    }
+    static bool inverse(const M4& a, M4& r) {  // Raytracer.h:354-370
+        float det = det4(a);
+        if (std::fabs(det) < 1e-10) return false;
+        M4 adj;
+        adjoint(a, adj);
         for (int i = 0; i < 4; i++)
             for (int j = 0; j < 4; j++) r.m[i][j] = adj.m[i][j] / det;
         return true;
@@ -161,13 +169,26 @@ struct Material {  // Raytracer.h:442-463
 };
 struct Tri { V3 p[3], nrm[3]; };
 struct Mesh { int type = 0; std::vector<Tri> tris; float radius = 0; };  // value-initialised (:605)
-struct Shape { Material mat; V3 S{1, 1, 1}, R, T; int mesh = -1; M4 model; };
+// The ray-invariant part of IntersectTriangle (Raytracer.cpp:353-365, :377, :389,
+// :403) for one triangle of one shape: world vertices, normal, plane offset,
+// signed area, hit normal. Computed once with the same float operations, so
+// the hoisted test rounds exactly like the per-call one.
+struct WTri { V3 v0, v1, v2, N, hn; float D, area; };
+struct Shape {
+    Material mat;
+    V3 S{1, 1, 1}, R, T;
+    int mesh = -1;
+    std::string geo;  // geometryId (meshMap key, Raytracer.cpp:477)
+    M4 model;
+    std::vector<WTri> wtris;
+};
 struct Light { int type = -1; V3 color, position, direction; float intensity = 0; };
 enum { LDIR = 0, LPOINT = 1, LAMB = 2 };
 struct Camera { V3 from, to; };
 struct Scene {
     std::vector<Shape> shapes;
     std::vector<Mesh> meshes;
+    std::unordered_map<std::string, int> mesh_by_name;  // meshMap (Raytracer.h:552)
     std::vector<Light> lights;
     Camera cam;
 };
@@ -204,6 +225,26 @@ static M4 model_matrix(const Shape& s) {
     return S * R * T;
 }
 
+// IntersectTriangle's ray-invariant values (Raytracer.cpp:353-365, :377, :389,
+// :403, :937-942), in the reference's operation order.
+static void hoist_triangles(Shape& s, const Mesh& m) {
+    s.wtris.resize(m.tris.size());
+    for (size_t i = 0; i < m.tris.size(); i++) {
+        WTri& w = s.wtris[i];
+        w.v0 = s.model.xform_point(m.tris[i].p[0]);
+        w.v1 = s.model.xform_point(m.tris[i].p[1]);
+        w.v2 = s.model.xform_point(m.tris[i].p[2]);
+        V3 e1 = w.v1 - w.v0, e2 = w.v2 - w.v0;
+        w.N = V3::cross(e1, e2);
+        w.N.normalize();
+        w.D = -w.N.dot(w.v0);
+        V3 ab = w.v1 - w.v0, ac = w.v2 - w.v0;
+        w.area = (float)(0.5 * V3::cross(ab, ac).dot(w.N));
+        w.hn = w.N;
+        w.hn.normalize();
+    }
+}
+
 static V3 vec3(const json_min::Value& a) { return {a.at(0).as_float(), a.at(1).as_float(), a.at(2).as_float()}; }
 
 // LoadMesh, Raytracer.cpp:589-643
@@ -236,6 +277,7 @@ static int load_mesh(Scene& sc, std::map<std::string, int>& cache, const std::st
     sc.meshes.push_back(mesh);
     idx = (int)sc.meshes.size() - 1;
     cache[name] = idx;
+    sc.mesh_by_name[name] = idx;
     return 0;
 }
 
@@ -254,6 +296,7 @@ static int load_scene(Scene& sc, const std::string& root, const std::string& pat
                 Shape shp;
                 (void)sv->at("id").as_string();
                 std::string geo = sv->at("geometry").as_string();
+                shp.geo = geo;
                 const json_min::Value& m = sv->at("material");
                 shp.mat.cs = vec3(m.at("Cs"));
                 shp.mat.ka = m.at("Ka").as_float();
@@ -270,6 +313,7 @@ static int load_scene(Scene& sc, const std::string& root, const std::string& pat
                 }
                 status |= load_mesh(sc, cache, root, geo, shp.mesh);
                 shp.model = model_matrix(shp);
+                if (shp.mesh >= 0 && sc.meshes[shp.mesh].type == 0) hoist_triangles(shp, sc.meshes[shp.mesh]);
                 sc.shapes.push_back(shp);
             }
         if (s.contains("camera")) {
@@ -412,22 +456,68 @@ struct Tracer {
         h.type = 1;
         return true;
     }
+    // The same test on the hoisted record (WTri): identical operations on
+    // identical values from `nd` on.
+    static bool wtri_hit(const Ray& r, const WTri& w, Hit& h) {
+        float nd = w.N.dot(r.d);
+        if (std::abs(nd - 0.0f) < kEPS) return false;
+        float t = -(w.N.dot(r.o) + w.D) / nd;
+        if (t <= kEPS) return false;
+        V3 P = r.o + r.d * t;
+        float a = CalcArea(P, w.v1, w.v2, w.N) / w.area;
+        float b = CalcArea(w.v0, P, w.v2, w.N) / w.area;
+        float g = CalcArea(w.v0, w.v1, P, w.N) / w.area;
+        if (a < 0 || b < 0 || g < 0) return false;
+        h.p = P; h.type = 0; h.n = w.hn; h.t = t; h.a = a; h.b = b; h.g = g;
+        return true;
+    }
     // IntersectScene, Raytracer.cpp:473-526
     bool intersect(const Ray& r, Hit& out) const {
+        if (g_faithful) return intersect_faithful(r, out);
         Hit best;
         bool found = false;
         for (const Shape& s : sc->shapes) {
             const Mesh& m = sc->meshes[s.mesh];
             if (m.type == 0) {
-                for (const Tri& t : m.tris) {
+                for (size_t i = 0; i < s.wtris.size(); i++) {
                     Hit h;
-                    if (tri_hit(r, t, s.model, h) && (!found || h.t < best.t)) {
-                        found = true; best = h; best.tri = &t; best.mat = &s.mat;
+                    if (wtri_hit(r, s.wtris[i], h) && (!found || h.t < best.t)) {
+                        found = true; best = h; best.tri = &m.tris[i]; best.mat = &s.mat;
                     }
                 }
             } else {
                 Hit h;
                 if (sph_hit(r, m.radius, s.model, h) && (!found || h.t < best.t)) {
+                    found = true; best = h; best.mat = &s.mat;
+                }
+            }
+        }
+        if (found) out = best;
+        return found;
+    }
+    // Ref-faithful mode (CPU-baseline timing only; same results): the work the
+    // reference does per IntersectScene call as written — meshMap lookup by
+    // string (:477), ComputeModelMatrix per shape (:480), and per triangle test
+    // the unused Matrix::Inverse (:350-351) and three TransformPoint (:353-355).
+    bool intersect_faithful(const Ray& r, Hit& out) const {
+        Hit best;
+        bool found = false;
+        for (const Shape& s : sc->shapes) {
+            const Mesh& m = sc->meshes[sc->mesh_by_name.at(s.geo)];
+            const M4 model = model_matrix(s);
+            if (m.type == 0) {
+                for (const Tri& t : m.tris) {
+                    M4 inv;
+                    M4::inverse(model, inv);
+                    g_sink = inv.m[0][0];  // computed, as in the reference, unused
+                    Hit h;
+                    if (tri_hit(r, t, model, h) && (!found || h.t < best.t)) {
+                        found = true; best = h; best.tri = &t; best.mat = &s.mat;
+                    }
+                }
+            } else {
+                Hit h;
+                if (sph_hit(r, m.radius, model, h) && (!found || h.t < best.t)) {
                     found = true; best = h; best.mat = &s.mat;
                 }
             }
@@ -627,6 +717,22 @@ static Ray generate_ray(const Camera2& c, int x, int y) {  // GenerateRay, Raytr
 
 using namespace ora;
 
+// Worker threads: $OMP_NUM_THREADS when set (the GPU box caps a job's CPU share
+// there), else every hardware thread.
+static int default_threads() {
+    if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+        int n = std::atoi(e);
+        if (n > 0) return n;
+    }
+    int n = (int)std::thread::hardware_concurrency();
+    return n > 0 ? n : 1;
+}
+
+extern "C" int oracle_set_mode(int faithful) {
+    g_faithful = faithful ? 1 : 0;
+    return 0;
+}
+
 extern "C" int oracle_render(const char* assets_root, const char* scene, int w, int h, int depth,
                              int ao_samples, int ao_enabled, int engine, int threads, int row_begin,
                              int row_end, int16_t* fb, uint64_t* counters, uint64_t* rays_per_row) {
@@ -645,23 +751,22 @@ extern "C" int oracle_render(const char* assets_root, const char* scene, int w, 
     tr.ao_bmax = (float)(2 * kPI);
     tr.n_amb = 0;
     for (auto& l : sc.lights) tr.n_amb += l.type == LAMB;
-    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
-    if (threads <= 0) threads = 1;
+    if (threads <= 0) threads = default_threads();
 
     // Pass 1: AO calls per pixel for every pixel in [0, row_end) (raster prefix).
     const int nrows_all = row_end;
     std::vector<uint32_t> calls((size_t)nrows_all * w);
     {
-        std::atomic<int> next{0};
+        // work items are pixels (not rows): tiny frames at high AO counts still use every core
+        std::atomic<int64_t> next{0};
+        const int64_t npix = (int64_t)nrows_all * w;
         auto work = [&] {
             for (;;) {
-                int y = next.fetch_add(1);
-                if (y >= nrows_all) break;
-                for (int x = 0; x < w; x++) {
-                    Counters c;
-                    tr.raycast(generate_ray(cam, x, y), depth, nullptr, c, true);
-                    calls[(size_t)y * w + x] = (uint32_t)c.ao_calls;
-                }
+                int64_t i = next.fetch_add(1);
+                if (i >= npix) break;
+                Counters c;
+                tr.raycast(generate_ray(cam, (int)(i % w), (int)(i / w)), depth, nullptr, c, true);
+                calls[(size_t)i] = (uint32_t)c.ao_calls;
             }
         };
         std::vector<std::thread> th;
@@ -680,32 +785,39 @@ extern "C" int oracle_render(const char* assets_root, const char* scene, int w, 
         for (uint64_t i = 0; i < total; i++) src.stream[i] = (uint32_t)g();
     }
     // Pass 2: render rows [row_begin, row_end).
-    std::vector<Counters> rowc((size_t)(row_end - row_begin));
+    const int64_t nsel = (int64_t)(row_end - row_begin) * w;
+    std::vector<Counters> pixc((size_t)nsel);
     {
-        std::atomic<int> next{row_begin};
+        std::atomic<int64_t> next{0};
         auto work = [&] {
             RngCursor rng;
             rng.src = &src;
             for (;;) {
-                int y = next.fetch_add(1);
-                if (y >= row_end) break;
-                Counters& c = rowc[y - row_begin];
-                for (int x = 0; x < w; x++) {
-                    size_t pi = (size_t)y * w + x;
-                    rng.seek(ao_enabled ? base[pi] * per_call : 0);
-                    Ray r = generate_ray(cam, x, y);
-                    c.primary++;
-                    Pix p = tr.raycast(r, depth, &rng, c, fb == nullptr);
-                    if (fb) {
-                        int16_t* o = fb + ((size_t)(y - row_begin) * w + x) * 3;
-                        o[0] = p.r; o[1] = p.g; o[2] = p.b;
-                    }
+                int64_t i = next.fetch_add(1);
+                if (i >= nsel) break;
+                const int y = row_begin + (int)(i / w), x = (int)(i % w);
+                Counters& c = pixc[(size_t)i];
+                size_t pi = (size_t)y * w + x;
+                rng.seek(ao_enabled ? base[pi] * per_call : 0);
+                Ray r = generate_ray(cam, x, y);
+                c.primary++;
+                Pix p = tr.raycast(r, depth, &rng, c, fb == nullptr);
+                if (fb) {
+                    int16_t* o = fb + (size_t)i * 3;
+                    o[0] = p.r; o[1] = p.g; o[2] = p.b;
                 }
             }
         };
         std::vector<std::thread> th;
         for (int t = 0; t < threads; t++) th.emplace_back(work);
         for (auto& t : th) t.join();
+    }
+    std::vector<Counters> rowc((size_t)(row_end - row_begin));
+    for (int64_t i = 0; i < nsel; i++) {
+        Counters& r = rowc[(size_t)(i / w)];
+        const Counters& c = pixc[(size_t)i];
+        r.primary += c.primary; r.secondary += c.secondary; r.shadow += c.shadow;
+        r.ao += c.ao; r.ao_calls += c.ao_calls;
     }
     Counters tot;
     for (size_t i = 0; i < rowc.size(); i++) {

@@ -9,10 +9,15 @@
 // Reference: /root/reference/580 Raytracer/Raytracer.{h,cpp} (MSVC C++, single
 // threaded). Restated here, function by function (file:line in each definition),
 // with two changes that do not alter a single output bit:
-//   * the model matrix of each shape (ComputeModelMatrix, Raytracer.cpp:528-586)
-//     is computed once per shape instead of once per shape per IntersectScene
-//     call (Raytracer.cpp:480), and the unused Matrix::Inverse per triangle test
-//     (Raytracer.cpp:350-351) and per pixel (:850) is computed once;
+//   * by default ("hoisted") the model matrix of each shape (ComputeModelMatrix,
+//     Raytracer.cpp:528-586) and the ray-invariant part of each triangle test
+//     (world vertices, normal, plane offset, signed area, :353-389) are computed
+//     once at load with the same float operations, instead of per IntersectScene
+//     call (:480) / per test; the unused Matrix::Inverse per triangle test
+//     (:350-351) is skipped. oracle_set_mode(1) ("ref-faithful") restores that
+//     per-call work (string meshMap lookup, ComputeModelMatrix per shape per
+//     call, Inverse + TransformPoint per test) so the restatement costs what the
+//     reference costs -- the CPU baseline of bench.py; results are identical;
 //   * rows may be rendered on several threads: the single serial RNG stream
 //     (member mGenerator, Raytracer.h:592) is addressed by absolute draw index,
 //     found with a count pass + prefix sum over the raster order.
@@ -40,6 +45,9 @@ int oracle_count_rows(const char* assets_root, const char* scene, int w, int h, 
 int oracle_shade_rows(const char* assets_root, const char* scene, int w, int h, int depth, int ao_samples,
                       int ao_enabled, int row_begin, int row_step, int n_rows, const uint64_t* row_base,
                       int16_t* fb);
+
+// 0 = hoisted (default), 1 = ref-faithful cost model (see above). Process-global.
+int oracle_set_mode(int faithful);
 
 // Writes the reference's P6 output (FlushFrameBufferToPPM, Raytracer.cpp:796-830).
 int oracle_write_ppm(const char* path, int w, int h, const int16_t* fb);

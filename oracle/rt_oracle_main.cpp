@@ -1,6 +1,6 @@
 // rt_oracle CLI (TEST INFRASTRUCTURE ONLY): renders with the CPU restatement.
 // usage: rt_oracle <dir containing Assets/> <scene.json> <w> <h> <depth> <out.ppm|->
-//                  [--ao N] [--ao-off] [--mt] [--threads T] [--rows a b]
+//                  [--ao N] [--ao-off] [--mt] [--threads T] [--rows a b] [--faithful]
 // Prints one JSON line with timing and ray counters on stdout.
 #include "rt_oracle.h"
 #include <chrono>
@@ -11,7 +11,7 @@
 
 int main(int argc, char** argv) {
     if (argc < 7) {
-        std::fprintf(stderr, "usage: %s <root> <scene> <w> <h> <depth> <out.ppm|-> [--ao N] [--ao-off] [--mt] [--threads T] [--rows a b]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <root> <scene> <w> <h> <depth> <out.ppm|-> [--ao N] [--ao-off] [--mt] [--threads T] [--rows a b] [--faithful]\n", argv[0]);
         return 2;
     }
     int w = std::atoi(argv[3]), h = std::atoi(argv[4]), depth = std::atoi(argv[5]);
@@ -20,6 +20,7 @@ int main(int argc, char** argv) {
         if (!std::strcmp(argv[i], "--ao") && i + 1 < argc) ao = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--ao-off")) ao_on = 0;
         else if (!std::strcmp(argv[i], "--mt")) engine = 1;
+        else if (!std::strcmp(argv[i], "--faithful")) oracle_set_mode(1);
         else if (!std::strcmp(argv[i], "--threads") && i + 1 < argc) threads = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rows") && i + 2 < argc) { r0 = std::atoi(argv[++i]); r1 = std::atoi(argv[++i]); }
         else { std::fprintf(stderr, "bad arg %s\n", argv[i]); return 2; }

@@ -54,6 +54,9 @@ SYNTH = [
     ("cornell10k_d6_aooff", "cornell10k.json", 24, 16, 6, 128, 0, "minstd"),
     ("field100k_d4_ao4", "field100k.json", 16, 9, 4, 4, 1, "minstd"),
     ("field1m_d2_ao2", "field1m.json", 8, 5, 2, 2, 1, "minstd"),
+    # configs 4 and 5 at their own depth and AO count (reference: ~30 min / ~1.5 h of CPU)
+    ("field100k_d6_ao256", "field100k.json", 16, 9, 6, 256, 1, "minstd"),
+    ("field1m_d8_ao256", "field1m.json", 6, 4, 8, 256, 1, "minstd"),
 ]
 SYNTH_ROOT = os.path.join(REF, "synth")
 
@@ -115,8 +118,22 @@ def run(entry, keep_ppm, root=ROOT, extra=None):
     return rec
 
 
+def merge_entry(man_path, rec):
+    """Add one record to the manifest under a file lock (several --only runs may
+    finish concurrently)."""
+    import fcntl
+    with open(man_path + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        man = json.load(open(man_path)) if os.path.exists(man_path) else {"entries": []}
+        have = {e["name"]: e for e in man["entries"]}
+        have[rec["name"]] = rec
+        man["entries"] = sorted(have.values(), key=lambda r: r["name"])
+        json.dump(man, open(man_path, "w"), indent=1)
+
+
 def main():
     big = "--big" in sys.argv
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     os.makedirs(os.path.join(HERE, "ppm"), exist_ok=True)
     man_path = os.path.join(HERE, "manifest.json")
     man = json.load(open(man_path)) if os.path.exists(man_path) else {"entries": []}
@@ -124,6 +141,8 @@ def main():
     todo = [(e, True, False) for e in SMALL] + [(e, True, True) for e in SYNTH] + \
         ([(e, False, False) for e in BIG] if big else [])
     for e, keep, synth in todo:
+        if only is not None and e[0] != only:
+            continue
         if e[0] in have and (not keep or os.path.exists(os.path.join(HERE, have[e[0]].get("ppm", "-")))):
             continue
         if synth:
@@ -131,8 +150,10 @@ def main():
             have[e[0]] = run(e, keep, SYNTH_ROOT, {"assets": "synthetic", "asset_sha256": files})
         else:
             have[e[0]] = run(e, keep)
-        man["entries"] = sorted(have.values(), key=lambda r: r["name"])
-        json.dump(man, open(man_path, "w"), indent=1)
+        merge_entry(man_path, have[e[0]])
+    if only is not None:
+        return
+    man = json.load(open(man_path))
     # The reference's own committed render (mt19937, depth 0, AO 128, 500x500;
     # provenance established in SURVEY.md §4) — kept gzipped as a data fixture.
     if os.path.exists(REF_OUTPUT_PPM):

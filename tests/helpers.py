@@ -109,19 +109,23 @@ def oracle_lib():
     lib.oracle_render.restype = ctypes.c_int
     lib.oracle_render.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 9 + \
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.oracle_set_mode.argtypes = [ctypes.c_int]
     return lib
 
 
 def oracle_render(scene, w, h, depth, ao_samples=128, ao_enabled=True, engine=0, threads=0,
-                  rows=None, root=ASSETS_ROOT):
-    """CPU restatement render -> (int16 (nrows, w, 3) framebuffer, counters dict)."""
+                  rows=None, root=ASSETS_ROOT, faithful=False):
+    """CPU restatement render -> (int16 (nrows, w, 3) framebuffer, counters dict).
+    faithful=True: the ref-faithful cost model (same results, reference's cost)."""
     lib = oracle_lib()
+    lib.oracle_set_mode(1 if faithful else 0)
     r0, r1 = rows if rows else (0, h)
     fb = np.zeros((r1 - r0, w, 3), dtype=np.int16)
     cnt = np.zeros(6, dtype=np.uint64)
     st = lib.oracle_render(os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples,
                            int(ao_enabled), engine, threads, r0, r1,
                            fb.ctypes.data, cnt.ctypes.data, None)
+    lib.oracle_set_mode(0)
     assert st == 0, "oracle_render failed"
     keys = ["rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"]
     return fb, dict(zip(keys, (int(x) for x in cnt)))

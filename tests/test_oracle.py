@@ -46,6 +46,19 @@ def test_oracle_row_subsets_and_threads_agree():
     assert np.array_equal(part, full[13:29])
 
 
+@pytest.mark.parametrize("name", ["teapots_d2_ao4", "cornell10k_d4_ao4", "sss_d4_ao16"])
+def test_oracle_faithful_mode_matches_golden(name):
+    """The ref-faithful cost model (per-call model matrix, unused Inverse and
+    TransformPoint per test; the CPU baseline) gives the golden bytes too."""
+    e = next(x for x in helpers.golden_entries(True) if x["name"] == name)
+    fb, c_f = helpers.oracle_render(e["scene"], e["width"], e["height"], e["depth"], e["ao_samples"],
+                                    e["ao_enabled"], root=helpers.entry_root(e), faithful=True)
+    assert helpers.rt580().ppm_bytes(fb) == helpers.golden_ppm(e)
+    _, c_h = helpers.oracle_render(e["scene"], e["width"], e["height"], e["depth"], e["ao_samples"],
+                                   e["ao_enabled"], root=helpers.entry_root(e))
+    assert c_f == c_h
+
+
 @pytest.mark.skipif(not os.path.isdir(helpers.REFERENCE), reason="reference not mounted")
 def test_scene_fixtures_are_the_reference_assets():
     ref = os.path.join(helpers.REFERENCE, "Assets")
