@@ -18,7 +18,7 @@ Raytracer::~Raytracer() {}
 int Raytracer::LoadSceneJSON(const std::string scenePath) {
     std::string err;
     mSceneValid = false;
-    mUploaded = false;
+    mUploadedScene = 0;
     int st = rt580::load_scene_json(mAssetsRoot, scenePath, mScene, err);
     if (st != RT_SUCCESS) {
         std::cerr << err << "\n";
@@ -28,7 +28,7 @@ int Raytracer::LoadSceneJSON(const std::string scenePath) {
         if (s.mesh < 0) return RT_FAILURE;
     rt580::pack_scene(mScene, mPacked);
     mSceneValid = true;
-    std::cerr << "Scene parsing completed!\n";  // Raytracer.cpp:772 (stderr: keep stdout for results)
+    std::cout << "Scene parsing completed!" << std::endl;  // Raytracer.cpp:772
     return RT_SUCCESS;
 }
 
@@ -78,7 +78,9 @@ int Raytracer::InitializeRenderer() {
 int Raytracer::Render(const std::string outputName) {
     if (mWidth <= 0 || mHeight <= 0) return RT_INVALID_ARG;
     if (InitializeRenderer() != RT_SUCCESS) return RT_FAILURE;
-    if (!mUploaded) {
+    // The device scene is process-wide: upload again when another instance (or
+    // rt_gpu_shutdown) replaced the one this instance uploaded.
+    if (mUploadedScene == 0 || rt_gpu_scene_id() != mUploadedScene) {
         if (rt_gpu_init(-1) != RT_SUCCESS) return RT_FAILURE;
         rt_scene_soa s;
         std::memset(&s, 0, sizeof s);
@@ -91,7 +93,7 @@ int Raytracer::Render(const std::string outputName) {
         s.n_lights = (int32_t)mPacked.lights.size();
         s.lights = mPacked.lights.data();
         if (rt_gpu_upload_scene(&s) != RT_SUCCESS) return RT_FAILURE;
-        mUploaded = true;
+        mUploadedScene = rt_gpu_scene_id();
     }
     // Selected rows land in their frame positions; other rows keep their contents.
     const int nsel = (mParams.row_end - mParams.row_begin + mParams.row_step - 1) / mParams.row_step;

@@ -46,7 +46,7 @@ class Raytracer {
     rt580::Scene mScene;
     rt580::PackedScene mPacked;
     bool mSceneValid = false;
-    bool mUploaded = false;
+    uint64_t mUploadedScene = 0;  // rt_gpu_scene_id() of this instance's upload (0: none)
     bool mWriteOutput = true;
     rt_render_params mParams;
     int mDepth = 4, mAoSamples = 128, mAoOn = 1, mEngine = RT_RNG_MINSTD_RAND0;

@@ -102,7 +102,7 @@ struct DevWork {
     uint32_t aofix_cap;
 };
 
-void upload_minstd_table(hipStream_t s);
+hipError_t upload_minstd_table(hipStream_t s);
 // Breadth-first trace of all levels: nodes, shading except AO, per-pixel counters.
 hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s);
 // Per-row AO-call totals + in-row prefixes, then the local row scan.
@@ -118,7 +118,7 @@ size_t far_sort_tmp_bytes(uint32_t cap);
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s);
 hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* out,
                             hipStream_t s);
-void upload_gamma_lut(const uint8_t* lut, hipStream_t s);
+hipError_t upload_gamma_lut(const uint8_t* lut, hipStream_t s);
 hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_math_selftest(uint64_t seed, uint64_t n, unsigned long long* bad, hipStream_t s);
 hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows,

@@ -32,6 +32,7 @@
 #include <hipcub/hipcub.hpp>
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "../../include/rt580.h"
@@ -816,15 +817,23 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                 v = v3(vx, vy, z);
             } else {
                 double sa, ca;
-                if (VARIANT & 64) { sa = ang; ca = z; }  // DIAGNOSTIC ablation only (wrong output)
-                else rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
+#ifdef RT580_DIAGNOSTICS
+                if (VARIANT & 64) { sa = ang; ca = z; }  // DIAGNOSTIC build only (wrong output)
+                else
+#endif
+                rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
                 v = v3((float)((double)r * ca), (float)((double)r * sa), z);
             }
-            if (!(VARIANT & 128)) v = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
+#ifdef RT580_DIAGNOSTICS
+            constexpr bool skip_norm = (VARIANT & 128) != 0;  // DIAGNOSTIC build only (wrong output)
+#else
+            constexpr bool skip_norm = false;
+#endif
+            if (!skip_norm) v = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
             if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
             o = v3_add(hp, v3_scale(v, 0.2f));
             // Ray constructor (Raytracer.h:431-433)
-            d = (VARIANT & 128) ? v : ((VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v));
+            d = skip_norm ? v : ((VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v));
             if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o);
         }
         if (VARIANT & 4096) {
@@ -842,8 +851,11 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                 }
             }
         }
-        const bool hit = (VARIANT & 32) ? (d.x > 2.0f)  // DIAGNOSTIC ablation only
-                       : (VARIANT & 512) ? (active && !ao_brute && bvh_any(S.bv, o, d, /*with_far=*/false))
+        const bool hit =
+#ifdef RT580_DIAGNOSTICS
+                         (VARIANT & 32) ? (d.x > 2.0f) :  // DIAGNOSTIC build only (wrong output)
+#endif
+                         (VARIANT & 512) ? (active && !ao_brute && bvh_any(S.bv, o, d, /*with_far=*/false))
                        : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
                                        : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
         if (VARIANT & 512) {
@@ -1459,8 +1471,8 @@ __global__ void gamma_u8_kernel(const int16_t* __restrict__ fb, uint64_t n, uint
     }
 }
 
-void upload_gamma_lut(const uint8_t* lut, hipStream_t s) {
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_gamma_lut), lut, 256, 0, hipMemcpyHostToDevice, s);
+hipError_t upload_gamma_lut(const uint8_t* lut, hipStream_t s) {
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_gamma_lut), lut, 256, 0, hipMemcpyHostToDevice, s);
 }
 
 hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s) {
@@ -1547,7 +1559,7 @@ __global__ void copy_rows_kernel(const int16_t* __restrict__ src, int width, int
 
 // ---------------------------------------------------------------- launchers
 
-void upload_minstd_table(hipStream_t s) {
+hipError_t upload_minstd_table(hipStream_t s) {
     uint32_t pw[32];
     uint64_t a = 16807;
     for (int i = 0; i < 32; i++) { pw[i] = (uint32_t)a; a = (a * a) % 2147483647ull; }
@@ -1558,8 +1570,13 @@ void upload_minstd_table(hipStream_t s) {
         x = (x * 16807ull) % 2147483647ull;
         x = (x * 16807ull) % 2147483647ull;
     }
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_pow2), pw, sizeof pw, 0, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
+    static uint32_t pw_keep[32];  // async copies read host memory later: keep it alive
+    std::memcpy(pw_keep, pw, sizeof pw);
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_pow2), pw_keep, sizeof pw_keep, 0,
+                                          hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
+    return e;
 }
 
 // Which launcher step failed last (error messages of the shim).
@@ -1659,7 +1676,8 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                     nq -= nb;
                 }
-                if (const char* dump = getenv("RT580_DUMP_FAR")) {  // DIAGNOSTIC: queued rays per level
+#ifdef RT580_DIAGNOSTICS
+                if (const char* dump = getenv("RT580_DUMP_FAR")) {  // DIAGNOSTIC build: queued rays per level
                     std::vector<float4> host((size_t)nq * 2);
                     if (nq) (void)hipMemcpy(host.data(), W.far_rays, (size_t)nq * 32, hipMemcpyDeviceToHost);
                     if (FILE* f = fopen(dump, "ab")) {
@@ -1670,6 +1688,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         fclose(f);
                     }
                 }
+#endif
                 if (nq) {
                     RT_STEP("trace far pass");
                     const int fm = far_mode(nq);
@@ -1824,10 +1843,12 @@ hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& 
         }
         return hipGetLastError();
     }
-    if (v >= 32) {  // diagnostic ablations (timing only)
+    if (v >= 32) {  // A/B variants; 32/64 (timing ablations with wrong output) only in diagnostic builds
         switch (v) {
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
-            RT_AO_CASE(41) RT_AO_CASE(73) RT_AO_CASE(137) RT_AO_CASE(105) RT_AO_CASE(233)
+#ifdef RT580_DIAGNOSTICS
+            RT_AO_CASE(41) RT_AO_CASE(73) RT_AO_CASE(105) RT_AO_CASE(137) RT_AO_CASE(233)
+#endif
             RT_AO_CASE(1032) RT_AO_CASE(3080) RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(7180) RT_AO_CASE(7182)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;

@@ -60,7 +60,8 @@ struct State {
     // two streams (frame pipelining, see begin_slot)
     Slot slot[2];
     int cur = 0;               // slot of the frame being enqueued
-    uint64_t frames = 0;       // frames begun (selects the slot)
+    int last_slot = -1;        // slot of the previous frame call
+    uint64_t frames = 0;       // frames begun
     hipEvent_t user_mark[2] = {nullptr, nullptr};  // the caller's stream at the start of a frame call
     bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
     // BVH far-queue buffers (BVH frames always run serialized on slot 0)
@@ -73,6 +74,8 @@ struct State {
     // capacity verification: a (params, scene) already rendered without overflow
     rt_render_params verified{};
     uint64_t verified_gen = ~0ull;
+    int verified_rows[3] = {0, 0, 0};  // the rows that frame traced: begin, step, count
+    int traced_rows[3] = {0, 0, 0};    // the rows the current frame traces
     bool verified_valid = false;
     // stats of the last traced rows
     int last_rows = 0, last_width = 0, last_ao_samples = 0, last_ao_enabled = 0;
@@ -84,6 +87,7 @@ struct State {
 
 State g;
 char g_err[512] = "";
+uint64_t g_scene_counter = 0;  // process-wide upload counter (survives rt_gpu_shutdown)
 #define SL (g.slot[g.cur])
 
 // Stream of the frame being enqueued.
@@ -105,24 +109,30 @@ int fail(const char* fmt, ...) {
         if (e_ != hipSuccess) return fail("%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
-// Frame pipelining. Frame k runs on slot k & 1 (its own stream and workspace),
-// so frame k+1's latency-bound trace overlaps frame k's AO kernel. Ordering:
-//  - frame k waits on the caller's stream as it was at the START of call k-1
-//    (user_mark): that covers whatever the caller queued against frame k-2's
-//    framebuffer (same slot, overwritten now) before it asked for frame k-1;
+// Frame pipelining. Consecutive frame calls alternate between two slots (own
+// stream and workspace), so frame k+1's latency-bound trace overlaps frame k's
+// AO kernel. Ordering:
+//  - a frame on the slot the PREVIOUS call did not use waits on the caller's
+//    stream as it was at the start of the previous call (user_mark): that
+//    covers whatever the caller queued against this slot's last framebuffer
+//    before it made that call;
+//  - a frame on the same slot as the previous call (a BVH frame after a slot-0
+//    frame; see below) waits on the caller's stream as it is now, so work the
+//    caller queued against the previous frame's framebuffer completes first;
 //  - the caller's stream waits for the frame (end_slot), so work the caller
 //    queues after the call sees its results ("asynchronous on the shim's stream").
-// BVH frames (host syncs inside, shared far-queue buffers) run on slot 0 after
-// everything the caller's stream holds, i.e. serialized.
+// BVH frames (host syncs inside, shared far-queue buffers) always run on slot 0.
 int begin_slot(bool serialize) {
     if (!g.pipeline) {
         g.cur = 0;
         return RT_SUCCESS;
     }
     const int k = (int)(g.frames & 1);
-    HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));
-    g.cur = serialize ? 0 : k;
-    const hipEvent_t wait = (g.frames == 0 || serialize) ? g.user_mark[k] : g.user_mark[k ^ 1];
+    HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));  // this call's start
+    const int slot = serialize ? 0 : (g.last_slot < 0 ? 0 : g.last_slot ^ 1);
+    const hipEvent_t wait = (g.frames == 0 || slot == g.last_slot) ? g.user_mark[k] : g.user_mark[k ^ 1];
+    g.cur = slot;
+    g.last_slot = slot;
     HIP_TRY(hipStreamWaitEvent(SL.stream, wait, 0));
     g.frames++;
     return RT_SUCCESS;
@@ -216,7 +226,8 @@ DevScene dev_scene(const rt_render_params* p) {
     v.dhi_median = g.bvh.dhi_median;
     v.has_tree = !g.bvh.nodes.empty();
     v.has_far = !g.bvh.far_nodes.empty();
-    {   // DIAGNOSTIC (timing ablation only, wrong results): RT580_BVH_DIAG=1 skips the far search
+#ifdef RT580_DIAGNOSTICS
+    {   // DIAGNOSTIC build only (timing ablation, wrong results): RT580_BVH_DIAG=1 skips the far search
         static int diag = -1;
         if (diag < 0) {
             const char* e = std::getenv("RT580_BVH_DIAG");
@@ -224,6 +235,7 @@ DevScene dev_scene(const rt_render_params* p) {
         }
         if (diag & 1) v.has_far = 0;
     }
+#endif
     v.scale = g.bvh.scale;
     v.grid_start = (const uint32_t*)g.grid_start.p;
     v.grid_items = (const uint32_t*)g.grid_items.p;
@@ -359,6 +371,9 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
     const DevScene sc = dev_scene(p);
     g.last_accel = sc.use_bvh != 0;
+    g.traced_rows[0] = row_begin;
+    g.traced_rows[1] = row_step;
+    g.traced_rows[2] = n_rows;
     {
         const hipError_t e = launch_trace(sc, f, dev_work(), fs());
         if (e != hipSuccess) return fail("launch_trace (%s): %s", launch_where(), hipGetErrorString(e));
@@ -406,12 +421,15 @@ int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     return RT_SUCCESS;
 }
 
-// Node-capacity check. A (params, scene) pair that already rendered without
-// overflow never overflows again (the frame is deterministic); otherwise wait
-// for the frame and read the highest node id it requested.
+// Node-capacity check. A (params, scene, traced rows) triple that already
+// rendered without overflow never overflows again (the frame is deterministic);
+// otherwise wait for the frame and read the highest node id it requested. The
+// traced rows are part of the key: rt_gpu_count_rows traces the selected rows
+// and rt_gpu_render_device the prefix [0, row_end) for the same params.
 int check_capacity(const rt_render_params* p, bool& retry) {
     retry = false;
-    if (g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0)
+    if (g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0 &&
+        std::memcmp(g.verified_rows, g.traced_rows, sizeof g.traced_rows) == 0)
         return RT_SUCCESS;
     HIP_TRY(hipMemcpyAsync(g.needed_host, SL.needed.p, 4, hipMemcpyDeviceToHost, fs()));
     HIP_TRY(hipStreamSynchronize(fs()));
@@ -424,6 +442,7 @@ int check_capacity(const rt_render_params* p, bool& retry) {
     }
     g.verified = *p;
     g.verified_gen = g.scene_gen;
+    std::memcpy(g.verified_rows, g.traced_rows, sizeof g.traced_rows);
     g.verified_valid = true;
     return RT_SUCCESS;
 }
@@ -459,13 +478,13 @@ int rt_gpu_init(int device) {
     g.ev = g.ev_default.data();
     HIP_TRY(hipHostMalloc((void**)&g.needed_host, 64, hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&g.far_count_host, 64, hipHostMallocDefault));
-    upload_minstd_table(g.stream);
+    HIP_TRY(upload_minstd_table(g.stream));
     {   // FlushFrameBufferToPPM's mapping, with this host's glibc powf (Raytracer.cpp:816-818);
         // called through a volatile pointer so no compiler constant-folds it
         float (*volatile pf)(float, float) = ::powf;
         static uint8_t lut[256];
         for (int c = 0; c < 256; c++) lut[c] = static_cast<unsigned char>(pf(c / 255.0f, 1.0f / 2.2f) * 255.0f);
-        upload_gamma_lut(lut, g.stream);
+        HIP_TRY(upload_gamma_lut(lut, g.stream));
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(g.stream));
@@ -546,9 +565,11 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         else g.n_nonambient++;
     }
     g.have_scene = true;
-    g.scene_gen++;
+    g.scene_gen = ++g_scene_counter;
     return RT_SUCCESS;
 }
+
+uint64_t rt_gpu_scene_id(void) { return g.inited && g.have_scene ? g.scene_gen : 0; }
 
 int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     if (check_params(p)) return RT_FAILURE;

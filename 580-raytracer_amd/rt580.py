@@ -56,6 +56,7 @@ class SceneSoa(ctypes.Structure):
 SIGNATURES = [
     ("rt_gpu_init", ctypes.c_int, [ctypes.c_int]),
     ("rt_gpu_upload_scene", ctypes.c_int, [ctypes.POINTER(SceneSoa)]),
+    ("rt_gpu_scene_id", ctypes.c_uint64, []),
     ("rt_gpu_set_stream", ctypes.c_int, [ctypes.c_void_p]),
     ("rt_gpu_own_stream", ctypes.c_void_p, []),
     ("rt_gpu_render", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),

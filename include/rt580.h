@@ -147,6 +147,10 @@ typedef struct rt_render_stats {
 int rt_gpu_init(int device);
 /* Upload (replace) the flattened scene; buffers stay resident in HBM. */
 int rt_gpu_upload_scene(const rt_scene_soa* scene);
+/* Identity of the resident scene: a process-wide counter value assigned by
+ * each successful upload (never reused, also across rt_gpu_shutdown); 0 when
+ * no scene is resident. The class surface re-uploads when it changed. */
+uint64_t rt_gpu_scene_id(void);
 /* Queue all further work on this HIP stream (hipStream_t); NULL is the HIP null
  * stream (PyTorch's default stream). Initially: the shim's own non-blocking
  * stream, whose handle rt_gpu_own_stream() returns. */

@@ -1,0 +1,115 @@
+"""Shim state across calls: frame pipelining's slot/stream ordering, the
+process-wide device scene shared by several Raytracer instances, and
+re-initialisation after rt_gpu_shutdown."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import helpers
+from test_gpu_parity import render_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(scene, w, h, depth, ao, root):
+    rt580 = helpers.rt580()
+    rt = rt580.Raytracer(w, h, root)
+    assert rt.LoadSceneJSON(scene) == 0
+    rt.set_depth(depth)
+    rt.set_ao(ao, True)
+    assert rt.InitializeRenderer() == 0
+    return rt, rt.render_params()
+
+
+def test_pipelined_frames_alternating_accel_keep_each_framebuffer():
+    """BVH frames run on slot 0; a brute-force frame after one must not
+    overwrite slot 0's framebuffer while work the caller queued against it (a
+    delayed read on the caller's stream) is still pending (rt_shim.cpp
+    begin_slot)."""
+    import torch
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    root = helpers.synthetic_root("cornell10k")
+    w, h = 40, 24
+    cfg = [(2, 4), (3, 8)]  # (depth, AO): the two alternating frames differ
+    want = [render_gpu("cornell10k.json", w, h, d, a, True, root=root)[0] for d, a in cfg]
+    rts = [_params("cornell10k.json", w, h, d, a, root) for d, a in cfg]
+    s = rts[0][0].scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    rt580.check(lib.rt_gpu_set_stream(ctypes.c_void_p(stream.cuda_stream)), "stream")
+    n = w * h * 3
+    outs = []
+    try:
+        for i in range(8):
+            k = i % 2
+            assert lib.rt_gpu_set_accel(1 if k == 0 else 0) == 0  # BVH (slot 0) / brute (pipelined)
+            fbp = ctypes.c_void_p()
+            rt580.check(lib.rt_gpu_render_device(ctypes.byref(rts[k][1]), ctypes.byref(fbp)), "render_device")
+            torch.cuda._sleep(2_000_000)  # the caller's read of this frame's fb is late
+            o = torch.empty(n, dtype=torch.uint8, device=dev)
+            rt580.check(lib.rt_gpu_gamma_u8(fbp, n, o.data_ptr()), "gamma_u8")
+            outs.append((k, o))
+        torch.cuda.synchronize()
+    finally:
+        lib.rt_gpu_set_accel(1)
+        lib.rt_gpu_set_stream(lib.rt_gpu_own_stream())
+    for i, (k, o) in enumerate(outs):
+        body = rt580.ppm_bytes(want[k]).split(b"\n", 3)[3]
+        assert o.cpu().numpy().tobytes() == body, "frame %d (config %d) was overwritten" % (i, k)
+
+
+def test_two_instances_with_different_scenes_interleave():
+    """The device scene is process-wide: instance A must re-upload its scene
+    after instance B rendered another one (raytracer.cpp Render)."""
+    rt580 = helpers.rt580()
+    a = rt580.Raytracer(48, 36, helpers.ASSETS_ROOT)
+    b = rt580.Raytracer(48, 36, helpers.ASSETS_ROOT)
+    assert a.LoadSceneJSON("simpleSphereScene.json") == 0 and b.LoadSceneJSON("scene.json") == 0
+    for r in (a, b):
+        r.set_depth(2)
+        r.set_ao(4, True)
+    assert a.Render("") == 0
+    fa = a.framebuffer()
+    assert b.Render("") == 0
+    fb = b.framebuffer()
+    assert a.Render("") == 0
+    assert np.array_equal(a.framebuffer(), fa)
+    assert b.Render("") == 0
+    assert np.array_equal(b.framebuffer(), fb)
+    assert not np.array_equal(fa, fb)
+    # after a shutdown the next Render initialises and uploads again
+    rt580.load().rt_gpu_shutdown()
+    assert a.Render("") == 0
+    assert np.array_equal(a.framebuffer(), fa)
+    ref, _ = helpers.oracle_render("simpleSphereScene.json", 48, 36, 2, 4, True)
+    assert np.array_equal(fa, ref)
+    a.close()
+    b.close()
+
+
+def test_count_rows_then_full_render_same_params():
+    """rt_gpu_count_rows traces only the selected rows, rt_gpu_render the
+    prefix; the node-capacity verification must not carry over between them
+    (rt_shim.cpp check_capacity keys on the traced rows)."""
+    import torch
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    d = helpers.rt580_dist()
+    scene, w, h, depth, ao = "simpleSphereSceneAO.json", 64, 48, 8, 4
+    rt, params = _params(scene, w, h, depth, ao, helpers.ASSETS_ROOT)
+    s = rt.scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    dev = torch.device("cuda", 0)
+    rt580.check(lib.rt_gpu_set_stream(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "stream")
+    try:
+        d.GpuRows(rt580, params, torch, dev).count(0, 4)
+        torch.cuda.synchronize()
+        host = np.zeros(w * h * 3, dtype=np.int16)
+        rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "render")
+    finally:
+        lib.rt_gpu_set_stream(lib.rt_gpu_own_stream())
+    ref, _ = helpers.oracle_render(scene, w, h, depth, ao, True)
+    assert np.array_equal(host.reshape(h, w, 3), ref)
