@@ -21,6 +21,10 @@ struct DevScene {
     int n_lights;
     int n_ambient;
     int use_bvh;   // triangle scenes: exact BVH queries (rt_isect.h) instead of brute force
+    // The primitives in a fixed pseudo-random order: the any-hit scan of
+    // far-origin rays reads them this way (any order gives the same boolean;
+    // accepted primitives come clustered by mesh in scene order, see far_scan_kernel).
+    const rt_prim* scan_prims;
     BvhView bv;
 };
 

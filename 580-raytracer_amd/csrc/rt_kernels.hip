@@ -1149,12 +1149,14 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
             if (brute) {
                 // BRUTE_ANY_U records per lane in flight per step, then one
                 // ballot; any order gives the same boolean
+                // in the shuffled order (DevScene::scan_prims): the first acceptor
+                // is then ~N / (acceptors + 1) records in instead of up to N
                 for (int k0 = 0; k0 < n_scan; k0 += BRUTE_ANY_U * 64) {
                     rt_prim p[BRUTE_ANY_U];
 #pragma unroll
                     for (int u = 0; u < BRUTE_ANY_U; u++) {
                         const int k = k0 + u * 64 + lane;
-                        if (k < n_scan) p[u] = S.prims[k];
+                        if (k < n_scan) p[u] = S.scan_prims[k];
                     }
 #pragma unroll
                     for (int u = 0; u < BRUTE_ANY_U; u++)

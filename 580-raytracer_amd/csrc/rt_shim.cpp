@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <random>
 #include <vector>
 
@@ -49,7 +50,7 @@ struct State {
     int n_prims = 0, n_lights = 0, n_ambient = 0, n_nonambient = 0;
     bool have_scene = false;
     // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
-    DevBuf bvh_nodes, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always;
+    DevBuf bvh_nodes, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always, scan_prims;
     BvhBuild bvh;
     bool bvh_ok = false;
     int grid_log2 = 0, grid_n_always = 0;  // far-search direction grid (uploaded; host copy dropped)
@@ -213,6 +214,7 @@ DevScene dev_scene(const rt_render_params* p) {
     s.n_lights = g.n_lights;
     s.n_ambient = g.n_ambient;
     s.use_bvh = g.accel == RT_ACCEL_AUTO && g.bvh_ok && bvh_usable(g.bvh, p->cam_from);
+    s.scan_prims = g.scan_prims.p ? (const rt_prim*)g.scan_prims.p : s.prims;
     BvhView& v = s.bv;
     v.all = s.prims;
     v.nodes = (const BvhNode*)g.bvh_nodes.p;
@@ -531,6 +533,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     // exact BVH for triangle scenes that do not fit one LDS tile (rt_bvh.h)
     g.bvh = BvhBuild();
     g.bvh_ok = false;
+    release(g.scan_prims);
     g.grid_log2 = g.grid_n_always = 0;
     if (s->n_prims > 64) {
         g.bvh_ok = build_bvh(s->prims, s->n_prims, g.bvh);
@@ -544,6 +547,18 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
                          upload_vec(g.grid_start, g.bvh.grid_start) || upload_vec(g.grid_items, g.bvh.grid_items) ||
                          upload_vec(g.grid_always, g.bvh.grid_always)))
             return RT_FAILURE;
+        if (g.bvh_ok && !g.bvh.far_nodes.empty()) {
+            // The any-hit scan order of far-origin rays (far_scan_kernel): a fixed
+            // shuffle of the scene. Such a ray (origin ~1e6 out, from one of the
+            // reference's far hits) is accepted by hundreds to thousands of
+            // primitives, but often only by one mesh's: in scene order the first
+            // acceptor can be ~75k records in (field100k), in shuffled order it
+            // is ~N / (acceptors + 1) in. The boolean does not depend on the order.
+            std::vector<rt_prim> perm(s->prims, s->prims + s->n_prims);
+            std::mt19937 rng(580u);
+            std::shuffle(perm.begin(), perm.end(), rng);
+            if (upload_vec(g.scan_prims, perm)) return RT_FAILURE;
+        }
         g.grid_log2 = g.bvh.grid_start.empty() ? 0 : g.bvh.grid_log2;
         g.grid_n_always = (int)g.bvh.grid_always.size();
         // the device needs only the arrays; keep the host copy small
@@ -767,7 +782,7 @@ void rt_gpu_shutdown(void) {
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
                       &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
-                      &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights})
+                      &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims})
         release(*b);
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
