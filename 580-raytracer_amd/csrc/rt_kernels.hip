@@ -407,13 +407,16 @@ __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { retu
 // PHASE 0: the whole level in one pass (brute force, or BVH without sorted far
 // pass). BVH scenes with a plane tree split it: PHASE 1 = near closest hit,
 // provisional hit stored per node and rays that may still have a far hit
-// queued (sorted far_closest_kernel in between); PHASE 2 = shading from the
-// stored hit. Items [i0, i1) of the level.
+// queued (sorted far_closest_kernel in between); PHASE 3 = the shadow ray of
+// directional light `light` (its index among the directional lights: `dl`):
+// near any-hit, the undecided rays queued for the sorted far pass, flags in
+// W.shadow; PHASE 2 = shading from the stored hit and shadow flags. Items
+// [i0, i1) of the level.
 // SCALAR (small brute-force scenes): wave-uniform scalar scene loads and the
 // division-free sign rejections (tri_test<SIGN>) instead of the LDS tile.
 template <bool BVH, int PHASE, bool SCALAR = false>
 __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
-                                                   uint32_t i1) {
+                                                   uint32_t i1, int light = 0, int dl = 0) {
     __shared__ rt_prim tile[TILE];
     const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
     const uint32_t base_id = level == 0 ? 0u : W.lvl[LVL_BASE + level];
@@ -476,6 +479,41 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             }
             continue;
         }
+        if (PHASE == 3) {
+            // the shadow ray of the shading phase (Raytracer.cpp:59-75), same
+            // float operations as below: hit point o + d t, origin hp + L * 0.2
+            bool q = false, brute = false;
+            uint8_t flag = 0;
+            rv3 so = v3(0, 0, 0), L2 = v3(0, 0, 0);
+            if (active && W.hit_prim[node] >= 0) {
+                const float t = W.hit4[node].x;
+                const rt_light l = S.lights[light];
+                const rv3 hp = v3_add(o, v3_scale(d, t));
+                L2 = ld3(l.L2);
+                so = v3_add(hp, v3_scale(ld3(l.L), 0.2f));
+                brute = far_origin(S, so);
+                if (!brute && bvh_any(S.bv, so, L2, /*with_far=*/false)) flag = 1;
+                else q = brute || !dir_zero(L2);
+            }
+            if (active) W.shadow[(size_t)dl * W.far_cap + (item - i0)] = flag;
+            const uint64_t bm = __ballot(brute);
+            if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
+            const uint64_t qm = __ballot(q);
+            if (qm) {
+                const int leader = __ffsll((unsigned long long)qm) - 1;
+                uint32_t qb = 0;
+                if ((threadIdx.x & 63) == leader) qb = atomicAdd(W.far_count, (uint32_t)__popcll(qm));
+                qb = __shfl(qb, leader);
+                if (q) {
+                    const uint32_t slot = qb + (uint32_t)__popcll(qm & lanemask_lt());
+                    W.far_rays[2 * (size_t)slot] = make_float4(so.x, so.y, so.z, __uint_as_float(item - i0));
+                    W.far_rays[2 * (size_t)slot + 1] = make_float4(L2.x, L2.y, L2.z, 0.0f);
+                    W.far_keys[slot] = brute ? RT_KEY_BRUTE : dir_key(L2);
+                    W.far_vals[slot] = slot;
+                }
+            }
+            continue;
+        }
         bool hit;
         if (PHASE == 2) {
             hit = false;
@@ -507,6 +545,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
         // (those need AO; int16 wrap-around addition commutes, so they are added
         // in resolve_kernel).
         rpix local = px(0, 0, 0);
+        int dli = 0;  // index among the directional lights
         for (int li = 0; li < S.n_lights; li++) {
             const rt_light l = S.lights[li];
             if (l.kind == RT_LIGHT_AMBIENT) continue;
@@ -525,7 +564,10 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                 so = v3_add(hi.p, v3_scale(L, 0.2f));
             }
             bool occluded;
-            if (l.kind == RT_LIGHT_DIRECTIONAL) {
+            if (PHASE == 2 && l.kind == RT_LIGHT_DIRECTIONAL && W.shadow) {
+                occluded = hit && W.shadow[(size_t)dli * W.far_cap + (item - i0)] != 0;  // decided by PHASE 3
+                dli++;
+            } else if (l.kind == RT_LIGHT_DIRECTIONAL) {
                 occluded = BVH ? (hit && bvh_any(S.bv, so, L2))
                                : SCALAR ? any_hit_scalar<true>(S, hit, so, L2)
                                         : any_hit(S, tile, resident, hit, so, L2);
@@ -1040,7 +1082,15 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
 #ifndef FAR_ANY_WPE
 #define FAR_ANY_WPE 8
 #endif
-__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE))) far_any_kernel(DevScene S, DevWork W, uint32_t n) {
+// flag != null: shadow rays (tag = flag index, the flag is set on a hit);
+// else AO rays (tag = AO call, its occlusion count is incremented).
+__device__ __forceinline__ void any_hit_out(const DevWork& W, uint8_t* flag, uint32_t tag) {
+    if (flag) flag[tag] = 1;
+    else atomicAdd(&W.occ[tag], 1u);
+}
+
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
+far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * TB;
@@ -1090,17 +1140,17 @@ __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY
                 }
             }
         }
-        if (hit) atomicAdd(&W.occ[call], 1u);
+        if (hit) any_hit_out(W, flag, call);
     }
 }
 
 // Per-lane variants (each lane walks its own path): better than the wave union
 // when the queue is too sparse for sorted waves to share a direction.
-__global__ void __launch_bounds__(TB) far_any_lane_kernel(DevScene S, DevWork W, uint32_t n) {
+__global__ void __launch_bounds__(TB) far_any_lane_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
         const uint32_t r = W.far_vals_alt[i];
         const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
-        if (far_any(S.bv, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z))) atomicAdd(&W.occ[__float_as_uint(a.w)], 1u);
+        if (far_any(S.bv, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z))) any_hit_out(W, flag, __float_as_uint(a.w));
     }
 }
 
@@ -1134,7 +1184,7 @@ __global__ void __launch_bounds__(TB) far_closest_lane_kernel(DevScene S, DevWor
 #define BRUTE_ANY_U 2  // far_scan_kernel brute any-hit: records per lane per ballot step
 #endif
 __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uint32_t first, uint32_t n, int closest,
-                                                      int n_far, int brute) {
+                                                      int n_far, int brute, uint8_t* flag) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_scan = brute ? S.n_prims : n_far;
     for (uint32_t i = first + blockIdx.x * (TB / 64) + wave; i < n; i += gridDim.x * (TB / 64)) {
@@ -1174,7 +1224,7 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
                 }
                 if (__ballot(hit)) break;
             }
-            if (__ballot(hit) && lane == 0) atomicAdd(&W.occ[tag], 1u);
+            if (__ballot(hit) && lane == 0) any_hit_out(W, flag, tag);
             continue;
         }
         Hit h;
@@ -1674,7 +1724,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 if (nb) {
                     RT_STEP("trace brute scan");
                     hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W,
-                                       nq - nb, nq, 1, (int)S.bv.n_far, 1);
+                                       nq - nb, nq, 1, (int)S.bv.n_far, 1, (uint8_t*)nullptr);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                     nq -= nb;
                 }
@@ -1700,8 +1750,35 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         hipLaunchKernelGGL(far_closest_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
                     else
                         hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nq * 64, 16384)), dim3(TB), 0, s, S,
-                                           W, 0u, nq, 1, (int)S.bv.n_far, 0);
+                                           W, 0u, nq, 1, (int)S.bv.n_far, 0, (uint8_t*)nullptr);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
+                }
+                // shadow rays of the directional lights: near any-hit, then the
+                // sorted far pass (brute scan for far-origin rays), like AO rays
+                if (W.shadow) {
+                    for (int dl = 0; dl < S.n_dir; dl++) {
+                        const int li = S.dir_light[dl];
+                        if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
+                        RT_STEP("trace shadow near pass");
+                        hipLaunchKernelGGL((trace_kernel<true, 3>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1,
+                                           li, dl);
+                        if ((e = hipGetLastError()) != hipSuccess) return e;
+                        uint32_t sq = 0, sb = 0;
+                        if ((e = sort_far_queue(W, s, sq, sb)) != hipSuccess) return e;
+                        uint8_t* flags = W.shadow + (size_t)dl * W.far_cap;
+                        if (sb) {
+                            RT_STEP("trace shadow brute scan");
+                            hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)sb * 64, 16384)), dim3(TB), 0, s,
+                                               S, W, sq - sb, sq, 0, (int)S.bv.n_far, 1, flags);
+                            if ((e = hipGetLastError()) != hipSuccess) return e;
+                            sq -= sb;
+                        }
+                        if (sq) {
+                            RT_STEP("trace shadow far pass");
+                            hipLaunchKernelGGL(far_any_kernel, dim3(grid_for(sq, 16384)), dim3(TB), 0, s, S, W, sq, flags);
+                            if ((e = hipGetLastError()) != hipSuccess) return e;
+                        }
+                    }
                 }
                 RT_STEP("trace shade phase");
                 hipLaunchKernelGGL((trace_kernel<true, 2>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
@@ -1801,7 +1878,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
             if (nb) {
                 hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W,
-                                   nq - nb, nq, 0, (int)S.bv.n_far, 1);
+                                   nq - nb, nq, 0, (int)S.bv.n_far, 1, (uint8_t*)nullptr);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 nq -= nb;
             }
@@ -1810,12 +1887,13 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if (nq == 0) continue;
             const int fm = far_mode(nq);
             if (fm == 1)
-                hipLaunchKernelGGL(far_any_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                hipLaunchKernelGGL(far_any_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq, (uint8_t*)nullptr);
             else if (fm == 2)
-                hipLaunchKernelGGL(far_any_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                hipLaunchKernelGGL(far_any_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq,
+                                   (uint8_t*)nullptr);
             else
                 hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nq * 64, 16384)), dim3(TB), 0, s, S, W,
-                                   0u, nq, 0, (int)S.bv.n_far, 0);
+                                   0u, nq, 0, (int)S.bv.n_far, 0, (uint8_t*)nullptr);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         return hipSuccess;

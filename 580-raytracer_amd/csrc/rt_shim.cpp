@@ -48,6 +48,7 @@ struct State {
     // scene
     DevBuf prims, shade, mats, lights;
     int n_prims = 0, n_lights = 0, n_ambient = 0, n_nonambient = 0;
+    std::vector<int> dir_lights;  // scene indices of the directional lights
     bool have_scene = false;
     // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
     DevBuf bvh_nodes, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always, scan_prims;
@@ -66,7 +67,7 @@ struct State {
     hipEvent_t user_mark[2] = {nullptr, nullptr};  // the caller's stream at the start of a frame call
     bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
     // BVH far-queue buffers (BVH frames always run serialized on slot 0)
-    DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim;
+    DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim, shadow;
     uint32_t* far_count_host = nullptr;  // pinned
     uint32_t far_cap = 0;
     uint32_t node_cap = 0, call_cap = 0;
@@ -215,6 +216,9 @@ DevScene dev_scene(const rt_render_params* p) {
     s.n_ambient = g.n_ambient;
     s.use_bvh = g.accel == RT_ACCEL_AUTO && g.bvh_ok && bvh_usable(g.bvh, p->cam_from);
     s.scan_prims = g.scan_prims.p ? (const rt_prim*)g.scan_prims.p : s.prims;
+    s.n_dir = 0;
+    if ((int)g.dir_lights.size() <= 8)
+        for (int li : g.dir_lights) s.dir_light[s.n_dir++] = li;
     BvhView& v = s.bv;
     v.all = s.prims;
     v.nodes = (const BvhNode*)g.bvh_nodes.p;
@@ -310,6 +314,9 @@ DevWork dev_work() {
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
     w.hit4 = split ? (float4*)g.hit4.p : nullptr;
     w.hit_prim = split ? (int32_t*)g.hit_prim.p : nullptr;
+    // shadow flags of the split trace's directional lights (more than 8: decided in the shading phase)
+    w.shadow = (split && g.shadow.p && !g.dir_lights.empty() && g.dir_lights.size() <= 8) ? (uint8_t*)g.shadow.p
+                                                                                              : nullptr;
     w.aofix_items = (uint64_t*)SL.aofix_items.p;
     w.aofix_count = (uint32_t*)SL.aofix_count.p;
     w.aofix_cap = (uint32_t)(SL.aofix_items.bytes / 8);
@@ -363,6 +370,9 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     }
     if (g.bvh_ok && !g.bvh.far_nodes.empty() &&
         (ensure(g.hit4, (size_t)cap * 16) || ensure(g.hit_prim, (size_t)cap * 4)))
+        return RT_FAILURE;
+    if (g.bvh_ok && !g.bvh.far_nodes.empty() && !g.dir_lights.empty() && g.dir_lights.size() <= 8 &&
+        ensure(g.shadow, g.dir_lights.size() * (size_t)g.far_cap))
         return RT_FAILURE;
     return RT_SUCCESS;
 }
@@ -575,9 +585,11 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     g.n_lights = s->n_lights;
     g.n_ambient = 0;
     g.n_nonambient = 0;
+    g.dir_lights.clear();
     for (int i = 0; i < s->n_lights; i++) {
         if (s->lights[i].kind == RT_LIGHT_AMBIENT) g.n_ambient++;
         else g.n_nonambient++;
+        if (s->lights[i].kind == RT_LIGHT_DIRECTIONAL) g.dir_lights.push_back(i);
     }
     g.have_scene = true;
     g.scene_gen = ++g_scene_counter;
@@ -782,7 +794,7 @@ void rt_gpu_shutdown(void) {
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
                       &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
-                      &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims})
+                      &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.shadow})
         release(*b);
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
