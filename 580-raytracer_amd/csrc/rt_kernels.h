@@ -132,6 +132,10 @@ hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int h
 hipError_t upload_gamma_lut(const uint8_t* lut, hipStream_t s);
 hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_math_selftest(uint64_t seed, uint64_t n, unsigned long long* bad, hipStream_t s);
+// Per-launch HIP-event timing of the AO ray kernel (profiling; see rt_kernels.hip).
+void kernel_timer_enable(bool on);
+hipError_t kernel_timer_read(double* ms, int* launches, uint64_t* units);
+void kernel_timer_release();
 hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows,
                             int16_t* dst, hipStream_t s);
 

@@ -401,6 +401,106 @@ __device__ __forceinline__ FarTri load_far_tri(const FarTri* tris, int j) {
     return t;
 }
 
+// ---------------------------------------------------------------- wave-cooperative near any-hit
+// bvh_any's near part (brute list + spatial BVH, rt_isect.h) for the 64 rays
+// of a wave at once: the wave walks one node sequence with wave-uniform scalar
+// node loads; a child is entered if the fat-ray slab test of any lane that is
+// still undecided meets its box, and only those lanes (a 64-bit mask kept with
+// the stack entry) continue below it. Each lane runs the unchanged per-ray slab
+// and triangle tests, so a lane's set of tested triangles contains everything
+// its own per-lane traversal would test (the culling is conservative for every
+// lane), and its boolean is the same. Suited to coherent waves: the samples of
+// one AO call (common origin), the shadow rays of neighbouring pixels toward
+// one directional light (common direction).
+// Every lane of the wave must call it (convergent); `active` selects the rays.
+struct WaveEntry {
+    int32_t c, n;
+    uint32_t m_lo, m_hi;
+};
+#define RT_WAVE_STACK RT_BVH_STACK
+
+__device__ __forceinline__ BvhNode load_bvh_node_scalar(const BvhNode* nodes, int j) {
+    const cu32_ptr src = (cu32_ptr)(nodes + j);
+    BvhNode nd;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&nd);
+#pragma unroll
+    for (int k = 0; k < 16; k++) dst[k] = src[k];
+    return nd;
+}
+
+__device__ bool bvh_any_near_wave(const BvhView& V, bool active, rv3 o, rv3 d, WaveEntry* stk) {
+    const int lane = threadIdx.x & 63;
+    bool hit = false;
+    for (int k = 0; k < V.n_brute; k++) {  // spheres + unanalysable triangles, every ray
+        if (__ballot(active && !hit) == 0) break;
+        const int j = (int)__builtin_amdgcn_readfirstlane(V.brute[k]);
+        const rt_prim P = load_prim_scalar(V.all, j);
+        if (active && !hit) hit = prim_test_any(P, o, d);
+    }
+    if (!V.has_tree) return hit;
+    bool live = active && !hit && !dir_zero(d);
+    if (__ballot(live) == 0) return hit;
+    const SlabRay sr = slab_ray(V, o, d);
+    int sp = 0;
+    int32_t c = 0, n = 0;  // root (internal)
+    for (;;) {
+        if (n == 0) {
+            const BvhNode nd = load_bvh_node_scalar(V.nodes, c);
+            float t0, t1;
+            const bool h0 = live && nd.n0 >= 0 && slab(nd.lo0, nd.hi0, sr, t0);
+            const bool h1 = live && nd.n1 >= 0 && slab(nd.lo1, nd.hi1, sr, t1);
+            const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
+            if (b0 && b1) {
+                // the child more lanes need first (any order gives the same booleans)
+                const bool first0 = __popcll(b0) >= __popcll(b1);
+                const uint64_t mp = first0 ? b1 : b0;
+                WaveEntry e;
+                e.c = first0 ? nd.c1 : nd.c0;
+                e.n = first0 ? nd.n1 : nd.n0;
+                e.m_lo = (uint32_t)mp;
+                e.m_hi = (uint32_t)(mp >> 32);
+                stk[sp] = e;  // every lane writes the same value
+                sp++;
+                c = first0 ? nd.c0 : nd.c1;
+                n = first0 ? nd.n0 : nd.n1;
+                live = ((first0 ? b0 : b1) >> lane) & 1ull;
+                continue;
+            }
+            if (b0 || b1) {
+                c = b0 ? nd.c0 : nd.c1;
+                n = b0 ? nd.n0 : nd.n1;
+                live = ((b0 ? b0 : b1) >> lane) & 1ull;
+                continue;
+            }
+        } else {
+            for (int k = c; k < c + n; k++) {
+                const rt_prim P = load_prim_scalar(V.prims, k);
+                float t, a, b, g;
+                if (live && tri_test<false, true>(P, o, d, t, a, b, g)) {
+                    hit = true;
+                    live = false;
+                }
+                if (__ballot(live) == 0) break;
+            }
+        }
+        bool resumed = false;
+        while (sp > 0) {
+            sp--;
+            const WaveEntry e = stk[sp];
+            const uint64_t m = ((uint64_t)e.m_hi << 32) | e.m_lo;
+            live = ((m >> lane) & 1ull) && !hit;
+            if (__ballot(live)) {
+                c = __builtin_amdgcn_readfirstlane(e.c);
+                n = __builtin_amdgcn_readfirstlane(e.n);
+                resumed = true;
+                break;
+            }
+        }
+        if (!resumed) break;
+    }
+    return hit;
+}
+
 // ---------------------------------------------------------------- trace (one tree level)
 __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { return F.row_begin + lr * F.row_step; }
 
@@ -416,8 +516,9 @@ __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { retu
 // division-free sign rejections (tri_test<SIGN>) instead of the LDS tile.
 template <bool BVH, int PHASE, bool SCALAR = false>
 __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
-                                                   uint32_t i1, int light = 0, int dl = 0) {
+                                                   uint32_t i1, int light = 0, int dl = 0, int wave_near = 0) {
     __shared__ rt_prim tile[TILE];
+    __shared__ WaveEntry wstk[PHASE == 3 ? TB / 64 : 1][RT_WAVE_STACK];
     const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
     const uint32_t base_id = level == 0 ? 0u : W.lvl[LVL_BASE + level];
     // Children beyond the node capacity were not stored (the frame is re-rendered
@@ -482,9 +583,9 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
         if (PHASE == 3) {
             // the shadow ray of the shading phase (Raytracer.cpp:59-75), same
             // float operations as below: hit point o + d t, origin hp + L * 0.2
-            bool q = false, brute = false;
+            bool q = false, brute = false, lit = false;
             uint8_t flag = 0;
-            rv3 so = v3(0, 0, 0), L2 = v3(0, 0, 0);
+            rv3 so = v3(0, 0, 0), L2 = v3(1, 0, 0);
             if (active && W.hit_prim[node] >= 0) {
                 const float t = W.hit4[node].x;
                 const rt_light l = S.lights[light];
@@ -492,9 +593,14 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                 L2 = ld3(l.L2);
                 so = v3_add(hp, v3_scale(ld3(l.L), 0.2f));
                 brute = far_origin(S, so);
-                if (!brute && bvh_any(S.bv, so, L2, /*with_far=*/false)) flag = 1;
-                else q = brute || !dir_zero(L2);
+                lit = true;
             }
+            // per lane, or (wave_near, A/B) one wave-cooperative near traversal:
+            // neighbouring pixels' shadow rays share the light's direction
+            const bool nh = wave_near ? bvh_any_near_wave(S.bv, lit && !brute, so, L2, wstk[threadIdx.x >> 6])
+                                      : (lit && !brute && bvh_any(S.bv, so, L2, /*with_far=*/false));
+            if (nh) flag = 1;
+            else q = lit && (brute || !dir_zero(L2));
             if (active) W.shadow[(size_t)dl * W.far_cap + (item - i0)] = flag;
             const uint64_t bm = __ballot(brute);
             if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
@@ -790,6 +896,7 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                                         uint64_t item_begin = 0, uint64_t item_end = ~0ull) {
     __shared__ rt_prim tile[TILE];
     __shared__ double sct_lds[440];  // glibc __sincostab, staged once per workgroup
+    __shared__ WaveEntry ao_wstk[(VARIANT & 8192) ? TB / 64 : 1][RT_WAVE_STACK];
     const double* sct = rt_dev::rt_sincostab;
     if (VARIANT & 1) {
         for (int i = threadIdx.x; i < 440; i += TB) sct_lds[i] = rt_dev::rt_sincostab[i];
@@ -897,7 +1004,8 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
 #ifdef RT580_DIAGNOSTICS
                          (VARIANT & 32) ? (d.x > 2.0f) :  // DIAGNOSTIC build only (wrong output)
 #endif
-                         (VARIANT & 512) ? (active && !ao_brute && bvh_any(S.bv, o, d, /*with_far=*/false))
+                         (VARIANT & 8192) ? bvh_any_near_wave(S.bv, active && !ao_brute, o, d, ao_wstk[threadIdx.x >> 6])
+                       : (VARIANT & 512) ? (active && !ao_brute && bvh_any(S.bv, o, d, /*with_far=*/false))
                        : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
                                        : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
         if (VARIANT & 512) {
@@ -1012,10 +1120,24 @@ __global__ void __launch_bounds__(TB) ao_near_kernel(DevScene S, DevFrame F, Dev
 // Occupancy-capped flavours of ao_near_kernel (RT580_NEAR_WPE=0|5|6|8 for A/B;
 // 100k 1080p AO time: uncapped 169 ms (103 VGPRs, 4 waves/SIMD), 5: 161 ms, 6: 158 ms,
 // 8: 149 ms; the spills of the capped builds cost less than the latency they hide).
-template <int WPE>
+template <int WPE, int V = 512 | 1024 | 2048 | 4096>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
-    ao_body<512 | 1024 | 2048 | 4096>(S, F, W, b, e);
+    ao_body<V>(S, F, W, b, e);
+}
+
+// RT580_NEAR_WAVE=1 (A/B): the wave-cooperative near traversal
+// (bvh_any_near_wave, VARIANT 8192) for AO and shadow rays instead of the
+// per-lane bvh_any. Measured on 100k 1080p: AO 139 ms vs 85 ms per lane (the
+// union of 64 hemisphere directions' paths is far longer than one path),
+// shadow passes 14.5 vs 13.9 ms of trace. Off by default.
+static bool near_wave() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_NEAR_WAVE");
+        v = e ? atoi(e) : 0;
+    }
+    return v != 0;
 }
 
 static int near_wpe() {
@@ -1631,6 +1753,64 @@ hipError_t upload_minstd_table(hipStream_t s) {
     return e;
 }
 
+// ---------------------------------------------------------------- kernel timer
+// HIP events around each launch of the AO ray kernel (the scene query of every
+// AO sample: ao_kernel for small scenes, ao_near_kernel for BVH scenes), on the
+// stream it runs on, while rt_gpu_profile is on: bench.py's roofline divides
+// the kernel's work by these per-launch durations.
+namespace {
+struct KernelTimer {
+    bool on = false;
+    std::vector<hipEvent_t> pool;  // begin/end pairs
+    size_t used = 0;
+    uint64_t units = 0;            // AO samples covered by the timed launches
+};
+KernelTimer g_kt;
+}  // namespace
+
+static void kt_begin(hipStream_t s) {
+    if (!g_kt.on) return;
+    if (g_kt.pool.size() < g_kt.used + 2) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess) return;
+        if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); return; }
+        g_kt.pool.push_back(a);
+        g_kt.pool.push_back(b);
+    }
+    (void)hipEventRecord(g_kt.pool[g_kt.used], s);
+}
+static void kt_end(hipStream_t s, uint64_t units) {
+    if (!g_kt.on || g_kt.pool.size() < g_kt.used + 2) return;
+    (void)hipEventRecord(g_kt.pool[g_kt.used + 1], s);
+    g_kt.used += 2;
+    g_kt.units += units;
+}
+
+void kernel_timer_enable(bool on) {
+    g_kt.on = on;
+    g_kt.used = 0;
+    g_kt.units = 0;
+}
+
+hipError_t kernel_timer_read(double* ms, int* launches, uint64_t* units) {
+    double t = 0;
+    for (size_t i = 0; i + 1 < g_kt.used; i += 2) {
+        float x = 0;
+        const hipError_t e = hipEventElapsedTime(&x, g_kt.pool[i], g_kt.pool[i + 1]);
+        if (e != hipSuccess) return e;
+        t += x;
+    }
+    *ms = t;
+    *launches = (int)(g_kt.used / 2);
+    *units = g_kt.units;
+    return hipSuccess;
+}
+
+void kernel_timer_release() {
+    for (hipEvent_t e : g_kt.pool) (void)hipEventDestroy(e);
+    g_kt = KernelTimer();
+}
+
 // Which launcher step failed last (error messages of the shim).
 static const char* g_where = "";
 const char* launch_where() { return g_where; }
@@ -1761,7 +1941,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
                         RT_STEP("trace shadow near pass");
                         hipLaunchKernelGGL((trace_kernel<true, 3>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1,
-                                           li, dl);
+                                           li, dl, near_wave() ? 1 : 0);
                         if ((e = hipGetLastError()) != hipSuccess) return e;
                         uint32_t sq = 0, sb = 0;
                         if ((e = sort_far_queue(W, s, sq, sb)) != hipSuccess) return e;
@@ -1862,7 +2042,11 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(W.aofix_count, 0, 4, s)) != hipSuccess) return e;
             const int wpe = near_wpe();
-            if (wpe == 5)
+            kt_begin(s);
+            if (near_wave())
+                hipLaunchKernelGGL((ao_near_kernel_w<8, 512 | 1024 | 2048 | 4096 | 8192>), dim3(grid_for(e1 - b, 8192)),
+                                   dim3(TB), 0, s, S, F, W, b, e1);
+            else if (wpe == 5)
                 hipLaunchKernelGGL(ao_near_kernel_w<5>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
             else if (wpe == 6)
                 hipLaunchKernelGGL(ao_near_kernel_w<6>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
@@ -1870,6 +2054,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 hipLaunchKernelGGL(ao_near_kernel_w<8>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
             else
                 hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+            kt_end(s, e1 - b);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             // exact recompute of the fast pass's failing samples; their misses join the far queue
             if ((e = launch_ao_fix(S, F, W, b, e1, s)) != hipSuccess) return e;
@@ -1899,7 +2084,16 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         return hipSuccess;
     }
     const int v = ao_variant();  // (frame_init_kernel zeroed W.aofix_count)
+    uint64_t items = 0;
+    if (g_kt.on) {  // the AO sample count of this launch (profiling only: a D2H read)
+        uint64_t calls = 0;
+        if (hipMemcpyAsync(&calls, W.totals, 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess)
+            items = calls * (uint64_t)F.ao_samples;
+    }
+    kt_begin(s);
     const hipError_t e = launch_ao_small(S, F, W, s, v);
+    kt_end(s, items);
     if (e != hipSuccess || !(v & 4096)) return e;
     return launch_ao_fix(S, F, W, 0, ~0ull, s);
 }

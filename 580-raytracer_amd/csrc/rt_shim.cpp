@@ -43,6 +43,7 @@ struct State {
     std::array<hipEvent_t, EV_N> ev_default{};
     hipEvent_t* ev = nullptr;  // events of the frame being enqueued
     bool profiling = false;
+    bool kt_keep = false;
     int prof_frames = 0;
     std::vector<std::array<hipEvent_t, EV_N>> prof_pool;
     // scene
@@ -324,6 +325,10 @@ DevWork dev_work() {
 }
 
 int begin_frame() {
+    if (!g.profiling && g.kt_keep) {  // the first frame after profiling ends its kernel timing
+        kernel_timer_enable(false);
+        g.kt_keep = false;
+    }
     if (!g.profiling) {
         g.ev = g.ev_default.data();
         return RT_SUCCESS;
@@ -762,6 +767,16 @@ int rt_gpu_profile(int enable) {
     if (enable || g.prof_frames == 0) g.ev = g.ev_default.data();
     g.profiling = enable != 0;
     g.prof_frames = 0;
+    if (enable) kernel_timer_enable(true);
+    else g.kt_keep = true;  // keep the last profiled launches readable
+    return RT_SUCCESS;
+}
+
+int rt_gpu_profile_ao_kernel(double* ms_total, int* launches, uint64_t* ao_rays) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (!ms_total || !launches || !ao_rays) return fail("rt_gpu_profile_ao_kernel: NULL output");
+    if (sync_all()) return RT_FAILURE;
+    HIP_TRY(kernel_timer_read(ms_total, launches, ao_rays));
     return RT_SUCCESS;
 }
 
@@ -813,6 +828,7 @@ void rt_gpu_shutdown(void) {
     if (g.needed_host) (void)hipHostFree(g.needed_host);
     if (g.far_count_host) (void)hipHostFree(g.far_count_host);
     if (g.own_stream) (void)hipStreamDestroy(g.own_stream);
+    kernel_timer_release();
     g = State();
 }
 

@@ -66,6 +66,8 @@ SIGNATURES = [
     ("rt_gpu_last_stats", ctypes.c_int, [ctypes.POINTER(RenderStats)]),
     ("rt_gpu_profile", ctypes.c_int, [ctypes.c_int]),
     ("rt_gpu_profile_read", ctypes.c_int, [ctypes.POINTER(ctypes.c_double)] * 4 + [ctypes.POINTER(ctypes.c_int)]),
+    ("rt_gpu_profile_ao_kernel", ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_gpu_set_accel", ctypes.c_int, [ctypes.c_int]),
     ("rt_gpu_gamma_u8", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     ("rt_gpu_row_bases", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

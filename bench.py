@@ -3,10 +3,12 @@
 "Mrays/sec + ms/frame at 1920x1080, depth=4, 64 AO samples; 1/2/4/8 GPU").
 
 A step = one frame of BASELINE config 2 (simpleSphereScene.json, 1920x1080,
-depth 4, 64 AO samples; the reference's scene file, synthetic = none needed)
-rendered from scratch: count pass + RNG-offset scan + shading kernel (+ for
-N > 1 the all-gather of per-row AO counts and the RCCL gather of the row tiles
-to rank 0). The scene is resident in HBM; the framebuffer stays in HBM.
+depth 4, 64 AO samples; the reference's own scene file) rendered from scratch:
+trace of the recursion tree, AO-call count + RNG-offset scan, AO kernel,
+resolve (+ for N > 1 the all-gather of per-row AO counts and the RCCL gather of
+the row tiles to rank 0). The scene is resident in HBM; the framebuffer stays
+in HBM (device throughput, frames pipelined on two streams). The blocking
+Render() latency (framebuffer copied to the host) is reported beside it.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
                     [--workload config2|cornell10k|field100k_1080p|field100k|field1m]
@@ -16,37 +18,41 @@ to rank 0). The scene is resident in HBM; the framebuffer stays in HBM.
 tools/gen_scenes.py, generated on first use under tests/_scenes); config2 is
 the headline. Synthetic workloads default to 2 steps after 1 warm-up.
 
-Rank 0 prints ONE JSON line (metric, value = whole-job Mrays/s, ms_per_step,
-roofline of the shading kernel, cpu_baseline = the reference itself timed on
-this host's cores on a bounded sample).
+Rank 0 prints ONE JSON line on stdout (metric, value = whole-job Mrays/s,
+ms_per_step, roofline of the AO ray kernel, cpu_baseline = the repository's
+CPU restatement in ref-faithful mode on this host, 1 core and all cores).
 """
 import argparse
+import contextlib
 import ctypes
 import json
 import os
-import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD
+# every 2 cycles, 2.4 GHz; HBM3E 8.0 TB/s.
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0   # 1228.8 G wave-instructions/s
+HBM_PEAK_GBS = 8000.0
 
-# name -> (scene, synthetic?, width, height, depth, AO samples, CPU-baseline sample (w, h, depth, ao), label)
-# The CPU sample is a downscaled frame of the same scene rendered by the reference
-# binary on one core (~10-30 s); the reference is O(primitives) per ray, so the
-# triangle scenes get tiny samples (and, for 1M triangles, fewer AO samples).
+# name -> (scene, synthetic?, width, height, depth, AO samples,
+#          CPU-baseline sample (w, h, depth, ao), label)
+# The CPU sample is a downscaled frame of the same scene (~10-30 s for the
+# ref-faithful restatement on one core); the reference is O(primitives) per ray,
+# so the triangle scenes get tiny samples.
 WORKLOADS = {
     "config2": ("simpleSphereScene.json", False, 1920, 1080, 4, 64, (480, 270, 4, 64),
                 "BASELINE config 2: simpleSphereScene.json 1920x1080 depth=4 AO=64"),
     "cornell10k": ("cornell10k.json", True, 1920, 1080, 4, 64, (6, 4, 4, 64),
                    "BASELINE config 3: 10k-triangle Cornell box 1920x1080 depth=4 AO=64"),
-    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64, (4, 3, 4, 64),
+    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64, (2, 2, 4, 64),
                         "north_star target: 100k-triangle field 1920x1080 depth=4 AO=64"),
-    "field100k": ("field100k.json", True, 3840, 2160, 6, 256, (4, 3, 6, 64),
+    "field100k": ("field100k.json", True, 3840, 2160, 6, 256, (2, 1, 6, 64),
                   "BASELINE config 4: 100k-triangle field 3840x2160 depth=6 AO=256"),
-    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, (2, 2, 8, 2),
+    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, (1, 1, 8, 2),
                 "BASELINE config 5: 1M-triangle field 7680x4320 depth=8 AO=256"),
 }
 
@@ -56,6 +62,22 @@ def env_int(k, d):
         return int(os.environ.get(k, d))
     except ValueError:
         return d
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """The reference prints "Scene parsing completed!" on stdout
+    (Raytracer.cpp:772) and so does the drop-in; keep bench.py's stdout to the
+    one JSON line by pointing fd 1 at stderr around such calls."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def main():
@@ -103,7 +125,8 @@ def main():
 
     root = helpers.synthetic_root(SCENE[:-5]) if SYNTH else helpers.ASSETS_ROOT
     rt = rt580.Raytracer(WIDTH, HEIGHT, root)
-    assert rt.LoadSceneJSON(SCENE) == 0, "LoadSceneJSON failed"
+    with stdout_to_stderr():
+        assert rt.LoadSceneJSON(SCENE) == 0, "LoadSceneJSON failed"
     rt.set_depth(DEPTH)
     rt.set_ao(AO, True)
     assert rt.InitializeRenderer() == 0
@@ -112,7 +135,6 @@ def main():
     rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(scene)), "rt_gpu_upload_scene")
     prims = [scene.prims[i] for i in range(scene.n_prims)]
     n_tri = sum(1 for p in prims if p.kind == 0)
-    n_sph = len(prims) - n_tri
 
     fbp = ctypes.c_void_p()
     K = max(args.row_sample, 1) if world == 1 else 1
@@ -197,6 +219,9 @@ def main():
     rt580.check(lib.rt_gpu_profile_read(*[ctypes.byref(m) for m in ms], ctypes.byref(frames)), "rt_gpu_profile_read")
     per_frame = [m.value / max(frames.value, 1) for m in ms]  # trace, rank, ao, resolve
     rt580.check(lib.rt_gpu_profile(0), "rt_gpu_profile")
+    k_ms, k_launches, k_rays = ctypes.c_double(), ctypes.c_int(), ctypes.c_uint64()
+    rt580.check(lib.rt_gpu_profile_ao_kernel(ctypes.byref(k_ms), ctypes.byref(k_launches), ctypes.byref(k_rays)),
+                "rt_gpu_profile_ao_kernel")
     # rays of one frame (this rank's rows), from the count pass of the last frame
     st = rt580.RenderStats()
     rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "rt_gpu_last_stats")
@@ -215,19 +240,6 @@ def main():
 
     if rank == 0:
         value = rays_frame * args.steps / dt / 1e6
-        bytes_per_ray = 56 * n_tri + 16 * n_sph  # SoA primitive records, no reuse
-        # dominant kernel: ao_kernel (one launch = this rank's AO rays of a frame)
-        # or, when it takes clearly longer, trace_kernel (camera, reflection/refraction
-        # and shadow rays of all levels; per-level launches summed). With frame
-        # pipelining the trace events of frame k+1 span time shared with frame k's
-        # AO kernel, so they overstate trace's own GPU time (config 2: 1.36 ms by
-        # events vs 0.65 ms by rocprofv3); trace counts as dominant only above 2x.
-        if per_frame[0] > 2.0 * per_frame[2]:
-            kname, kms = "trace_kernel", per_frame[0]
-            krays = int(local["rays_primary"]) + int(local["rays_secondary"]) + int(local["rays_shadow"])
-        else:
-            kname, kms, krays = "ao_kernel", per_frame[2], int(local["rays_ao"])
-        achieved = krays * bytes_per_ray / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
         out = {
             "metric": "Mrays/sec (+ ms/frame) at %dx%d, depth=%d, %d AO samples" % (WIDTH, HEIGHT, DEPTH, AO),
             "value": round(value, 3),
@@ -260,24 +272,12 @@ def main():
                 "ao": round(per_frame[2], 4),
                 "resolve": round(per_frame[3], 4),
             },
-            "roofline": {
-                "kernel": kname,
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": measured_traffic(args.workload, kname),
-                "bytes_per_ray": bytes_per_ray,
-                "rays_per_launch": krays,
-                "note": "algorithmic scene-stream bytes (56*T + 16*S per ray, SURVEY §8d) x rays of one "
-                        "%s launch / its mean duration (HIP events on its stream); the kernel itself "
-                        "is VALU-bound (the %d-primitive scene is re-read from LDS/scalar cache, not HBM)"
-                        % (kname, len(prims)),
-            },
         }
         if check_ok is not None:
             out["frame_matches_reference"] = check_ok
+        out["roofline"] = roofline(args.workload, k_ms.value, k_launches.value, k_rays.value, int(local["rays_ao"]))
+        if world == 1 and K == 1:
+            out["render_call_ms"] = render_latency(lib, rt580, params, torch)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(lib, rt580, helpers, root)
         print(json.dumps(out), flush=True)
@@ -290,56 +290,86 @@ def log(msg):
     print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
 
 
-def measured_traffic(workload, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
-    summary (profiles/), corrected per MI355X_MICROARCH.md §HBM; None if absent."""
-    name = "pmc_ao_kernel.json" if workload == "config2" and kernel == "ao_kernel" else \
-        "pmc_%s_%s.json" % (workload, kernel)
-    path = os.path.join(REPO, "profiles", name)
+def roofline(workload, k_ms, k_launches, k_rays, rays_ao_frame):
+    """Roofline of the AO ray kernel (the scene query of every AO sample; 95 %
+    of the frame's rays). Neither MFMA nor HBM bounds it (no dense
+    contraction; the scene is re-read from L2/MALL, see `traffic`): it is
+    bound by VALU instruction issue. achieved = VALU wave-instructions per AO
+    ray (rocprofv3 SQ_INSTS_VALU per dispatch / AO rays per dispatch, from the
+    committed profile summary profiles/r02/roofline_<workload>.json) x the AO
+    rays of one launch / that launch's mean duration, measured here with HIP
+    events around every launch on its own stream (rt_gpu_profile_ao_kernel).
+    peak = 1024 SIMDs x one wave64 VALU instruction per 2 cycles x 2.4 GHz."""
+    res = {"kernel": "ao_kernel (AO ray scene query)", "bound": "valu", "unit": "Ginst/s",
+           "peak": VALU_PEAK_GINST, "achieved": None, "frac": None, "traffic": None}
+    if k_launches <= 0 or k_ms <= 0:
+        res["note"] = "no AO kernel launch was timed"
+        return res
+    launch_s = k_ms / k_launches * 1e-3
+    rays_launch = k_rays / k_launches
+    res["launch_ms"] = round(launch_s * 1e3, 4)
+    res["ao_rays_per_launch"] = int(rays_launch)
+    path = os.path.join(REPO, "profiles", "r02", "roofline_%s.json" % workload)
+    prof = None
     if os.path.exists(path):
         try:
-            return json.load(open(path)).get("hbm_bytes_per_launch")
+            prof = json.load(open(path))
         except (ValueError, OSError):
-            return None
-    return None
+            prof = None
+    if not prof or not prof.get("valu_per_ao_ray"):
+        res["note"] = "no committed counter profile for this workload (%s)" % os.path.relpath(path, REPO)
+        return res
+    res["kernel"] = prof["kernel"]
+    achieved = prof["valu_per_ao_ray"] * rays_launch / launch_s / 1e9
+    res["achieved"] = round(achieved, 2)
+    res["frac"] = round(achieved / VALU_PEAK_GINST, 4)
+    if prof.get("hbm_bytes_per_ao_ray") is not None:
+        traffic = prof["hbm_bytes_per_ao_ray"] * rays_launch
+        res["traffic"] = round(traffic)
+        res["hbm"] = {"achieved": round(traffic / launch_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(traffic / launch_s / 1e9 / HBM_PEAK_GBS, 4)}
+    res["per_ray"] = {"valu_wave_insts": round(prof["valu_per_ao_ray"], 4),
+                      "hbm_bytes": prof.get("hbm_bytes_per_ao_ray")}
+    res["profile"] = {"file": os.path.relpath(path, REPO), "launch_ms_rocprof": prof.get("avg_ms"),
+                      "valu_issue_frac_rocprof": prof.get("valu_issue_frac"),
+                      "frame_share_rocprof": prof.get("frame_share"), "top_kernels": prof.get("top_kernels")}
+    res["note"] = ("VALU-issue roofline: counter-measured VALU wave-instructions per AO ray x AO rays per launch "
+                   "/ live launch time; traffic = FETCH_SIZE+WRITE_SIZE (x1 KiB) per AO ray x rays per launch "
+                   "(HBM is not the bound: see hbm.frac)")
+    return res
+
+
+def render_latency(lib, rt580, params, torch, n=3):
+    """Blocking rt_gpu_render (what Render() calls): first launch -> int16
+    framebuffer on the host (SURVEY §8d ms/frame), excluding scene load/upload
+    and the PPM write. Mean of n calls after the timed region."""
+    import numpy as np
+    host = np.zeros(params.width * params.height * 3, dtype=np.int16)
+    times = []
+    for _ in range(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
+        times.append((time.perf_counter() - t0) * 1e3)
+    return round(sum(times) / len(times), 4)
 
 
 def cpu_baseline(lib, rt580, helpers, root):
-    """The reference binary (oracle/_ref, built from /root/reference's own
-    sources) on one core, on a bounded sample of the same workload."""
+    """The repository's CPU restatement (oracle/) in ref-faithful mode (the
+    reference's per-call work: string mesh lookup and ComputeModelMatrix per
+    shape per IntersectScene call, the unused Matrix::Inverse + TransformPoint
+    per triangle test; oracle_set_mode(1)) on a bounded sample of the same
+    workload, on 1 core and on all of this host's cores (threads), rows of the
+    same RNG stream. The reference itself does not travel to this box."""
     w, h, depth, ao = CPU_SAMPLE
-    exe = os.path.join(REPO, "oracle", "_ref", "rt_ref_param")
-    ref_root = root if SYNTH else os.path.join(REPO, "oracle", "_ref", "root")
-    # rays of the sample frame: the GPU count pass of the same configuration
-    rt = rt580.Raytracer(w, h, root)
-    assert rt.LoadSceneJSON(SCENE) == 0
-    rt.set_depth(depth)
-    rt.set_ao(ao, True)
-    assert rt.InitializeRenderer() == 0
-    p = rt.render_params()
-    fb = (ctypes.c_int16 * (w * h * 3))()
-    rt580.check(lib.rt_gpu_render(ctypes.byref(p), fb), "rt_gpu_render (sample)")
-    st = rt580.RenderStats()
-    rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "stats")
-    rays = int(st.rays_total)
-    kind = "reference"
-    if os.path.exists(exe):
-        t0 = time.perf_counter()
-        pr = subprocess.run(["taskset", "-c", "0", exe, ref_root, SCENE, str(w), str(h), str(depth), "/dev/null",
-                             str(ao), "0"], capture_output=True, text=True)
-        wall = time.perf_counter() - t0
-        secs = wall
-        for line in pr.stderr.splitlines():
-            if line.startswith("render_seconds="):
-                secs = float(line.split()[0].split("=")[1])
-        if pr.returncode != 0:
-            return {"value": None, "error": pr.stderr[-300:]}
-    else:
-        kind = "port"
-        t0 = time.perf_counter()
-        _, cnt = helpers.oracle_render(SCENE, w, h, depth, ao, True, threads=1, root=root)
-        secs = time.perf_counter() - t0
-        rays = cnt["rays_total"]
+    threads = env_int("OMP_NUM_THREADS", os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    _, cnt = helpers.oracle_render(SCENE, w, h, depth, ao, True, threads=1, root=root, faithful=True)
+    secs1 = time.perf_counter() - t0
+    rays = cnt["rays_total"]
+    t0 = time.perf_counter()
+    helpers.oracle_render(SCENE, w, h, depth, ao, True, threads=threads, root=root, faithful=True)
+    secsn = time.perf_counter() - t0
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -349,16 +379,18 @@ def cpu_baseline(lib, rt580, helpers, root):
     except OSError:
         pass
     return {
-        "value": float("%.4g" % (rays / secs / 1e6)),
+        "value": float("%.4g" % (rays / secs1 / 1e6)),
         "unit": "Mrays/s",
         "cores": 1,
-        "kind": kind,
-        "seconds": round(secs, 3),
+        "kind": "port",
+        "seconds": round(secs1, 3),
         "rays": rays,
+        "all_cores": {"value": float("%.4g" % (rays / secsn / 1e6)), "cores": threads, "seconds": round(secsn, 3)},
         "cpu": cpu,
         "sample": "%s %dx%d depth=%d AO=%d (a downscaled frame of the workload, %.4g%% of its pixels), "
-                  "single thread, oracle/_ref/rt_ref_param = reference Raytracer.cpp with the AO count as a "
-                  "parameter" % (SCENE, w, h, depth, ao, 100.0 * w * h / (WIDTH * HEIGHT)),
+                  "oracle/rt_oracle.cpp in ref-faithful mode (same bytes as the reference; its cost model "
+                  "checked against the reference binary in the build container, DESIGN.md)"
+                  % (SCENE, w, h, depth, ao, 100.0 * w * h / (WIDTH * HEIGHT)),
     }
 
 

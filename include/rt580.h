@@ -211,6 +211,11 @@ int rt_gpu_last_stats(rt_render_stats* stats);
  * resolve (int16 blend) kernel. */
 int rt_gpu_profile(int enable);
 int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double* ms_resolve, int* frames);
+/* While profiling: HIP events around every launch of the AO ray kernel (the
+ * scene query of each AO sample: ao_kernel, or ao_near_kernel for BVH scenes),
+ * on the stream it runs on. Sum of their durations, number of launches and the
+ * AO rays they covered, since rt_gpu_profile(1). Synchronizes. */
+int rt_gpu_profile_ao_kernel(double* ms_total, int* launches, uint64_t* ao_rays);
 /* Last error message (static storage). */
 const char* rt_gpu_last_error(void);
 void rt_gpu_shutdown(void);
