@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -98,7 +99,18 @@ int Raytracer::Render(const std::string outputName) {
     // Selected rows land in their frame positions; other rows keep their contents.
     const int nsel = (mParams.row_end - mParams.row_begin + mParams.row_step - 1) / mParams.row_step;
     std::vector<int16_t> rows((size_t)(nsel > 0 ? nsel : 0) * mWidth * 3);
-    if (rt_gpu_render(&mParams, rows.data()) != RT_SUCCESS) return RT_FAILURE;
+    // Whole frames shard across the node's GPUs (interleaved rows, RCCL
+    // exchange + gather, rt_gpu_render_multi); SetGpuCount / $RT580_GPUS
+    // choose how many (default: every visible device).
+    int gpus = mGpus;
+    if (gpus <= 0) {
+        const char* e = std::getenv("RT580_GPUS");
+        gpus = e ? std::atoi(e) : rt_gpu_device_count();
+    }
+    const bool whole = mParams.row_begin == 0 && mParams.row_step == 1 && mParams.row_end == mHeight;
+    const int st = (gpus > 1 && whole) ? rt_gpu_render_multi(&mParams, rows.data(), gpus, nullptr)
+                                       : rt_gpu_render(&mParams, rows.data());
+    if (st != RT_SUCCESS) return RT_FAILURE;
     for (int k = 0; k < nsel; k++) {
         int y = mParams.row_begin + k * mParams.row_step;
         std::memcpy(&mFrameBuffer[(size_t)y * mWidth], &rows[(size_t)k * mWidth * 3], (size_t)mWidth * 6);
@@ -203,6 +215,7 @@ int rt580_set_depth(rt580_raytracer* h, int d) { return h ? h->rt.SetDepth(d) : 
 int rt580_set_ao(rt580_raytracer* h, int n, int on) { return h ? h->rt.SetAmbientOcclusion(n, on != 0) : RT_INVALID_ARG; }
 int rt580_set_rng(rt580_raytracer* h, int e) { return h ? h->rt.SetRngEngine(e) : RT_INVALID_ARG; }
 int rt580_set_rows(rt580_raytracer* h, int a, int b) { return h ? h->rt.SetRows(a, b, 1) : RT_INVALID_ARG; }
+int rt580_set_gpus(rt580_raytracer* h, int n) { return h ? h->rt.SetGpuCount(n) : RT_INVALID_ARG; }
 
 const int16_t* rt580_framebuffer(rt580_raytracer* h) {
     return h ? reinterpret_cast<const int16_t*>(h->rt.FrameBuffer()) : nullptr;

@@ -32,6 +32,12 @@ class Raytracer {
     int SetRngEngine(int engine);                    // Raytracer.h:592 (minstd_rand0)
     int SetRows(int row_begin, int row_end, int row_step = 1);
     int SetWriteOutput(bool on) { mWriteOutput = on; return RT_SUCCESS; }
+    // GPUs Render() shards a whole frame across (0: $RT580_GPUS, else every visible device).
+    int SetGpuCount(int n) {
+        if (n < 0 || n > 16) return RT_INVALID_ARG;
+        mGpus = n;
+        return RT_SUCCESS;
+    }
 
     const Pixel* FrameBuffer() const { return mFrameBuffer.data(); }
     const rt_render_params& Params() const { return mParams; }
@@ -51,4 +57,5 @@ class Raytracer {
     rt_render_params mParams;
     int mDepth = 4, mAoSamples = 128, mAoOn = 1, mEngine = RT_RNG_MINSTD_RAND0;
     int mRowBegin = 0, mRowEnd = -1, mRowStep = 1;
+    int mGpus = 0;
 };

@@ -136,6 +136,10 @@ hipError_t launch_math_selftest(uint64_t seed, uint64_t n, unsigned long long* b
 void kernel_timer_enable(bool on);
 hipError_t kernel_timer_read(double* ms, int* launches, uint64_t* units);
 void kernel_timer_release();
+// Multi-GPU frame: tiles[k] holds rows k, k+world, ... (n_max rows each) -> out
+// in raster order.
+hipError_t launch_deinterleave(const int16_t* tiles, int world, int n_max, int width, int height, int16_t* out,
+                               hipStream_t s);
 hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows,
                             int16_t* dst, hipStream_t s);
 

@@ -1731,6 +1731,26 @@ __global__ void copy_rows_kernel(const int16_t* __restrict__ src, int width, int
     dst[i] = src[(size_t)(row_begin + k * row_step) * per_row + e];
 }
 
+__global__ void deinterleave_kernel(const int16_t* __restrict__ tiles, int world, int n_max, int width, int height,
+                                    int16_t* __restrict__ out) {
+    const size_t per_row = (size_t)width * 3;
+    const size_t total = per_row * (size_t)height;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t y = i / per_row, e = i - y * per_row;
+        const size_t r = y % (size_t)world, j = y / (size_t)world;
+        out[i] = tiles[(r * (size_t)n_max + j) * per_row + e];
+    }
+}
+
+hipError_t launch_deinterleave(const int16_t* tiles, int world, int n_max, int width, int height, int16_t* out,
+                               hipStream_t s) {
+    const uint64_t n = (uint64_t)width * 3 * height;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(deinterleave_kernel, dim3(grid_for(n, 16384)), dim3(256), 0, s, tiles, world, n_max, width,
+                       height, out);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- launchers
 
 hipError_t upload_minstd_table(hipStream_t s) {

@@ -1,7 +1,13 @@
 // rt_shim.cpp — the extern "C" rt_gpu_* boundary (include/rt580.h): device
 // buffers resident in HBM, one HIP stream, HIP-event timings, error mapping to
 // the reference's status codes (Raytracer.h:8-10). No exception crosses it.
+//
+// State lives in per-device contexts. The public entry points act on context 0
+// (the device of rt_gpu_init); rt_gpu_render_multi drives contexts 0..G-1, one
+// per GPU of the node, and exchanges over RCCL (loaded on first use).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <array>
 #include <cmath>
@@ -88,9 +94,33 @@ struct State {
     bool split_ready = false;
 };
 
-State g;
+constexpr int kMaxCtx = 16;
+State g_ctx[kMaxCtx];
+int g_cur = 0;  // context the entry points act on (0 outside rt_gpu_render_multi)
+#define g (g_ctx[g_cur])
 char g_err[512] = "";
 uint64_t g_scene_counter = 0;  // process-wide upload counter (survives rt_gpu_shutdown)
+
+// The scene last uploaded to context 0, kept on the host for the other devices.
+struct HostScene {
+    std::vector<rt_prim> prims;
+    std::vector<rt_prim_shade> shade;
+    std::vector<rt_material> mats;
+    std::vector<rt_light> lights;
+    rt_scene_soa view() const {
+        rt_scene_soa v;
+        std::memset(&v, 0, sizeof v);
+        v.abi_version = RT580_ABI_VERSION;
+        v.n_prims = (int32_t)prims.size();
+        v.prims = prims.data();
+        v.shade = shade.data();
+        v.n_materials = (int32_t)mats.size();
+        v.materials = mats.data();
+        v.n_lights = (int32_t)lights.size();
+        v.lights = lights.data();
+        return v;
+    }
+} g_host_scene;
 #define SL (g.slot[g.cur])
 
 // Stream of the frame being enqueued.
@@ -406,12 +436,23 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
 }
 
 // mt19937: the reference's serial stream is generated on the host up to the
-// last draw this frame needs (no jump-ahead), then uploaded.
-int prepare_mt_stream(const rt_render_params* p) {
+// last draw these rows need, then uploaded (draws are addressed by absolute
+// index). Single call: the local total; multi-rank rows: max over the rows of
+// (global row base + the row's AO calls).
+int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global, int n_rows) {
     if (p->rng_engine != RT_RNG_MT19937 || !p->ao_enabled || g.n_ambient == 0) return RT_SUCCESS;
     uint64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, SL.totals.p, 8, hipMemcpyDeviceToHost, fs()));
-    HIP_TRY(hipStreamSynchronize(fs()));
+    if (!row_base_global) {
+        HIP_TRY(hipMemcpyAsync(&total, SL.totals.p, 8, hipMemcpyDeviceToHost, fs()));
+        HIP_TRY(hipStreamSynchronize(fs()));
+    } else if (n_rows > 0) {
+        std::vector<uint64_t> base((size_t)n_rows);
+        std::vector<uint32_t> calls((size_t)n_rows);
+        HIP_TRY(hipMemcpyAsync(base.data(), row_base_global, (size_t)n_rows * 8, hipMemcpyDeviceToHost, fs()));
+        HIP_TRY(hipMemcpyAsync(calls.data(), SL.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToHost, fs()));
+        HIP_TRY(hipStreamSynchronize(fs()));
+        for (int i = 0; i < n_rows; i++) total = std::max(total, base[i] + calls[i]);
+    }
     const uint64_t n = total * 2ull * (uint64_t)p->ao_samples;
     if (ensure(SL.mt_stream, n * 4 + 8)) return RT_FAILURE;
     std::vector<uint32_t> host(n);
@@ -429,7 +470,7 @@ int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     const DevScene sc = dev_scene(p);
     HIP_TRY(launch_rank(sc, f, dev_work(), row_base_global, fs()));
     HIP_TRY(hipEventRecord(g.ev[EV_RANK], fs()));
-    if (prepare_mt_stream(p)) return RT_FAILURE;
+    if (prepare_mt_stream(p, row_base_global, n_rows)) return RT_FAILURE;
     DevWork w = dev_work();
     HIP_TRY(launch_ao(sc, f, w, fs()));
     HIP_TRY(hipEventRecord(g.ev[EV_AO], fs()));
@@ -598,6 +639,12 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     }
     g.have_scene = true;
     g.scene_gen = ++g_scene_counter;
+    if (g_cur == 0) {
+        g_host_scene.prims.assign(s->prims, s->prims + s->n_prims);
+        g_host_scene.shade.assign(s->shade, s->shade + s->n_prims);
+        g_host_scene.mats.assign(s->materials, s->materials + s->n_materials);
+        g_host_scene.lights.assign(s->lights, s->lights + s->n_lights);
+    }
     return RT_SUCCESS;
 }
 
@@ -678,8 +725,6 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
 int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device, int16_t* fb_device) {
     if (check_params(p)) return RT_FAILURE;
     if (!row_base_device || !fb_device) return fail("row_base_device / fb_device is NULL");
-    if (p->rng_engine == RT_RNG_MT19937 && p->ao_enabled)
-        return fail("mt19937 is not supported by the multi-rank split (no jump-ahead)");
     if (!g.split_ready || std::memcmp(&g.split_params, p, sizeof *p) != 0)
         return fail("rt_gpu_shade_rows must follow rt_gpu_count_rows with the same params");
     HIP_TRY(hipSetDevice(g.device));
@@ -801,7 +846,13 @@ int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double
 
 const char* rt_gpu_last_error(void) { return g_err; }
 
-void rt_gpu_shutdown(void) {
+}  // extern "C"
+
+namespace {
+void destroy_comms();
+void release_multi();
+
+void shutdown_ctx() {
     if (!g.inited) return;
     (void)hipSetDevice(g.device);
     (void)sync_all();
@@ -828,8 +879,291 @@ void rt_gpu_shutdown(void) {
     if (g.needed_host) (void)hipHostFree(g.needed_host);
     if (g.far_count_host) (void)hipHostFree(g.far_count_host);
     if (g.own_stream) (void)hipStreamDestroy(g.own_stream);
-    kernel_timer_release();
     g = State();
+}
+}  // namespace
+
+extern "C" {
+
+void rt_gpu_shutdown(void) {
+    const int cur = g_cur;
+    release_multi();
+    for (int k = kMaxCtx - 1; k >= 0; k--) {
+        g_cur = k;
+        shutdown_ctx();
+    }
+    g_cur = cur;
+    kernel_timer_release();
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- multi-GPU Render
+namespace {
+
+// RCCL, loaded on the first multi-GPU frame (single-GPU use never needs it;
+// under PyTorch the already loaded librccl.so.1 is reused by its SONAME).
+struct Rccl {
+    bool tried = false;
+    void* h = nullptr;
+    decltype(&ncclCommInitAll) CommInitAll = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclAllGather) AllGather = nullptr;
+    decltype(&ncclSend) Send = nullptr;
+    decltype(&ncclRecv) Recv = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+} g_rccl;
+
+bool rccl_load() {
+    if (g_rccl.tried) return g_rccl.h != nullptr;
+    g_rccl.tried = true;
+    for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+        g_rccl.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+        if (g_rccl.h) break;
+    }
+    if (!g_rccl.h) return false;
+#define RT_RCCL_SYM(f) g_rccl.f = (decltype(g_rccl.f))dlsym(g_rccl.h, "nccl" #f)
+    RT_RCCL_SYM(CommInitAll);
+    RT_RCCL_SYM(CommDestroy);
+    RT_RCCL_SYM(AllGather);
+    RT_RCCL_SYM(Send);
+    RT_RCCL_SYM(Recv);
+    RT_RCCL_SYM(GroupStart);
+    RT_RCCL_SYM(GroupEnd);
+    RT_RCCL_SYM(GetErrorString);
+#undef RT_RCCL_SYM
+    if (!g_rccl.CommInitAll || !g_rccl.CommDestroy || !g_rccl.AllGather || !g_rccl.Send || !g_rccl.Recv ||
+        !g_rccl.GroupStart || !g_rccl.GroupEnd || !g_rccl.GetErrorString) {
+        dlclose(g_rccl.h);
+        g_rccl.h = nullptr;
+        return false;
+    }
+    return true;
+}
+
+#define RCCL_TRY(expr)                                                                          \
+    do {                                                                                        \
+        ncclResult_t r_ = (expr);                                                               \
+        if (r_ != ncclSuccess) return fail("%s: %s", #expr, g_rccl.GetErrorString(r_));         \
+    } while (0)
+
+// One split of the frame over n contexts (devices), with its RCCL communicator.
+struct Multi {
+    int n = 0;
+    int devs[kMaxCtx] = {};
+    bool rccl = false;
+    ncclComm_t comms[kMaxCtx] = {};
+    uint64_t scene_of[kMaxCtx] = {};  // context 0's scene id last uploaded to context k
+    DevBuf row_calls[kMaxCtx], gathered[kMaxCtx], base[kMaxCtx], tile[kMaxCtx];  // on device k
+    DevBuf root_tiles, frame;                                                     // on device 0
+    hipEvent_t ready[kMaxCtx] = {};                                               // local transport
+} g_multi;
+
+void destroy_comms() {
+    if (g_multi.rccl)
+        for (int k = 0; k < g_multi.n; k++)
+            if (g_multi.comms[k]) (void)g_rccl.CommDestroy(g_multi.comms[k]);
+    for (auto& c : g_multi.comms) c = nullptr;
+    g_multi.rccl = false;
+    g_multi.n = 0;
+}
+
+void release_multi() {
+    destroy_comms();
+    for (int k = 0; k < kMaxCtx; k++) {
+        if (!g_ctx[k].inited) continue;
+        (void)hipSetDevice(g_ctx[k].device);
+        for (DevBuf* b : {&g_multi.row_calls[k], &g_multi.gathered[k], &g_multi.base[k], &g_multi.tile[k]}) release(*b);
+        if (g_multi.ready[k]) (void)hipEventDestroy(g_multi.ready[k]);
+        g_multi.ready[k] = nullptr;
+        g_multi.scene_of[k] = 0;
+    }
+    if (g_ctx[0].inited) {
+        (void)hipSetDevice(g_ctx[0].device);
+        release(g_multi.root_tiles);
+        release(g_multi.frame);
+    }
+}
+
+// RT580_MULTI_TRANSPORT: "rccl" (default for distinct devices), "local"
+// (device copies; the only choice when a device appears twice, e.g. the
+// split rehearsed on one GPU by the tests).
+int transport_env() {
+    const char* e = std::getenv("RT580_MULTI_TRANSPORT");
+    if (!e) return 0;
+    if (!std::strcmp(e, "rccl")) return 1;
+    if (!std::strcmp(e, "local")) return 2;
+    return 0;
+}
+
+// The rest of the frame once every context has counted its rows (phase 2 +
+// gather + de-interleave + D2H); g_cur is restored by the caller.
+int multi_finish(const rt_render_params* p, int n, int n_max, int16_t* fb_out) {
+    const int H = p->height, W = p->width;
+    const size_t tile_bytes = (size_t)n_max * W * 6;
+    // exchange of the per-row AO-call counts (H int32 in all; the one step the
+    // serial RNG stream needs, Raytracer.h:592)
+    if (g_multi.rccl) {
+        RCCL_TRY(g_rccl.GroupStart());
+        for (int k = 0; k < n; k++) {
+            g_cur = k;
+            RCCL_TRY(g_rccl.AllGather(g_multi.row_calls[k].p, g_multi.gathered[k].p, (size_t)n_max, ncclInt32,
+                                      g_multi.comms[k], g.stream));
+        }
+        RCCL_TRY(g_rccl.GroupEnd());
+    } else {
+        for (int k = 0; k < n; k++) {
+            g_cur = k;
+            HIP_TRY(hipSetDevice(g.device));
+            HIP_TRY(hipEventRecord(g_multi.ready[k], g.stream));
+        }
+        for (int k = 0; k < n; k++) {
+            g_cur = k;
+            HIP_TRY(hipSetDevice(g.device));
+            for (int j = 0; j < n; j++) {
+                HIP_TRY(hipStreamWaitEvent(g.stream, g_multi.ready[j], 0));
+                HIP_TRY(hipMemcpyPeerAsync((char*)g_multi.gathered[k].p + (size_t)j * n_max * 4, g.device,
+                                           g_multi.row_calls[j].p, g_ctx[j].device, (size_t)n_max * 4, g.stream));
+            }
+        }
+    }
+    // phase 2 on every device: its rows' RNG bases, then shading
+    for (int k = 0; k < n; k++) {
+        g_cur = k;
+        HIP_TRY(hipSetDevice(g.device));
+        rt_render_params pk = *p;
+        pk.row_begin = k;
+        pk.row_step = n;
+        pk.row_end = H;
+        if (rt_gpu_row_bases((const int32_t*)g_multi.gathered[k].p, n, n_max, H, k, (uint64_t*)g_multi.base[k].p) ||
+            rt_gpu_shade_rows(&pk, (const uint64_t*)g_multi.base[k].p, (int16_t*)g_multi.tile[k].p))
+            return RT_FAILURE;
+    }
+    // the int16 row tiles to device 0
+    g_cur = 0;
+    HIP_TRY(hipSetDevice(g.device));
+    if (ensure(g_multi.root_tiles, tile_bytes * n) || ensure(g_multi.frame, (size_t)H * W * 6)) return RT_FAILURE;
+    HIP_TRY(hipMemcpyAsync(g_multi.root_tiles.p, g_multi.tile[0].p, tile_bytes, hipMemcpyDeviceToDevice, g.stream));
+    if (g_multi.rccl) {
+        RCCL_TRY(g_rccl.GroupStart());
+        for (int k = 1; k < n; k++) {
+            RCCL_TRY(g_rccl.Send(g_multi.tile[k].p, tile_bytes, ncclUint8, 0, g_multi.comms[k], g_ctx[k].stream));
+            RCCL_TRY(g_rccl.Recv((char*)g_multi.root_tiles.p + (size_t)k * tile_bytes, tile_bytes, ncclUint8, k,
+                                 g_multi.comms[0], g_ctx[0].stream));
+        }
+        RCCL_TRY(g_rccl.GroupEnd());
+    } else {
+        for (int k = 1; k < n; k++) {
+            g_cur = k;
+            HIP_TRY(hipSetDevice(g.device));
+            HIP_TRY(hipEventRecord(g_multi.ready[k], g.stream));
+        }
+        g_cur = 0;
+        HIP_TRY(hipSetDevice(g.device));
+        for (int k = 1; k < n; k++) {
+            HIP_TRY(hipStreamWaitEvent(g.stream, g_multi.ready[k], 0));
+            HIP_TRY(hipMemcpyPeerAsync((char*)g_multi.root_tiles.p + (size_t)k * tile_bytes, g.device,
+                                       g_multi.tile[k].p, g_ctx[k].device, tile_bytes, g.stream));
+        }
+    }
+    HIP_TRY(launch_deinterleave((const int16_t*)g_multi.root_tiles.p, n, n_max, W, H, (int16_t*)g_multi.frame.p,
+                                g.stream));
+    HIP_TRY(hipMemcpyAsync(fb_out, g_multi.frame.p, (size_t)H * W * 6, hipMemcpyDeviceToHost, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    for (int k = 1; k < n; k++) {  // the other devices' streams are idle again before the next frame
+        g_cur = k;
+        HIP_TRY(hipSetDevice(g.device));
+        HIP_TRY(hipStreamSynchronize(g.stream));
+    }
+    g_cur = 0;
+    HIP_TRY(hipSetDevice(g.device));
+    return RT_SUCCESS;
+}
+
+int multi_render(const rt_render_params* p, int16_t* fb_out, int n, const int* devices) {
+    if (check_params(p)) return RT_FAILURE;  // context 0: inited, scene resident
+    if (n < 1 || n > kMaxCtx) return fail("rt_gpu_render_multi: %d devices outside [1, %d]", n, kMaxCtx);
+    if (!fb_out) return fail("rt_gpu_render_multi: fb_out is NULL");
+    if (p->row_begin != 0 || p->row_step != 1 || p->row_end != p->height)
+        return fail("rt_gpu_render_multi renders whole frames (row_begin 0, row_step 1, row_end height)");
+    int devs[kMaxCtx];
+    int n_dev = 0;
+    HIP_TRY(hipGetDeviceCount(&n_dev));
+    for (int k = 0; k < n; k++) {
+        devs[k] = devices ? devices[k] : (g.device + k) % (n_dev > 0 ? n_dev : 1);
+        if (devs[k] < 0 || devs[k] >= n_dev) return fail("rt_gpu_render_multi: device %d out of range", devs[k]);
+    }
+    if (devs[0] != g.device) return fail("rt_gpu_render_multi: devices[0] must be rt_gpu_init's device");
+    const int tr = transport_env();
+    bool dup = false;
+    for (int a = 0; a < n; a++)
+        for (int b = a + 1; b < n; b++) dup = dup || devs[a] == devs[b];
+    if (n == 1 && tr != 1) return rt_gpu_render(p, fb_out);
+    const bool use_rccl = tr == 1 || (tr == 0 && !dup);
+    if (use_rccl && dup) return fail("rt_gpu_render_multi: RCCL needs distinct devices");
+    if (use_rccl && !rccl_load()) return fail("rt_gpu_render_multi: librccl.so.1 could not be loaded");
+    // contexts 1..n-1: one per device, same scene and acceleration mode as context 0
+    const State& c0 = g_ctx[0];
+    for (int k = 1; k < n; k++) {
+        g_cur = k;
+        if (g.inited && g.device != devs[k]) {
+            shutdown_ctx();
+            g_multi.scene_of[k] = 0;
+        }
+        if (!g.inited && rt_gpu_init(devs[k])) return RT_FAILURE;
+        g.accel = c0.accel;
+        g.pipeline = c0.pipeline;
+        if (g_multi.scene_of[k] != c0.scene_gen) {
+            const rt_scene_soa v = g_host_scene.view();
+            if (rt_gpu_upload_scene(&v)) return RT_FAILURE;
+            g_multi.scene_of[k] = c0.scene_gen;
+        }
+    }
+    g_cur = 0;
+    // the communicator of this device set
+    bool same = g_multi.n == n && g_multi.rccl == use_rccl;
+    for (int k = 0; same && k < n; k++) same = g_multi.devs[k] == devs[k];
+    if (!same) {
+        destroy_comms();
+        if (use_rccl) RCCL_TRY(g_rccl.CommInitAll(g_multi.comms, n, devs));
+        g_multi.n = n;
+        g_multi.rccl = use_rccl;
+        for (int k = 0; k < n; k++) g_multi.devs[k] = devs[k];
+    }
+    // phase 1 on every device: trace its interleaved rows, count their AO calls
+    const int H = p->height, W = p->width;
+    const int n_max = (H + n - 1) / n;
+    for (int k = 0; k < n; k++) {
+        g_cur = k;
+        HIP_TRY(hipSetDevice(g.device));
+        if (!g_multi.ready[k]) HIP_TRY(hipEventCreateWithFlags(&g_multi.ready[k], hipEventDisableTiming));
+        if (ensure(g_multi.row_calls[k], (size_t)n_max * 4) || ensure(g_multi.gathered[k], (size_t)n * n_max * 4) ||
+            ensure(g_multi.base[k], (size_t)n_max * 8) || ensure(g_multi.tile[k], (size_t)n_max * W * 6))
+            return RT_FAILURE;
+        HIP_TRY(hipMemsetAsync(g_multi.row_calls[k].p, 0, (size_t)n_max * 4, g.stream));  // padding rows count 0
+        rt_render_params pk = *p;
+        pk.row_begin = k;
+        pk.row_step = n;
+        pk.row_end = H;
+        if (rt_gpu_count_rows(&pk, (uint32_t*)g_multi.row_calls[k].p)) return RT_FAILURE;
+    }
+    return multi_finish(p, n, n_max, fb_out);
+}
+
+}  // namespace
+
+extern "C" int rt_gpu_render_multi(const rt_render_params* p, int16_t* fb_out, int n_devices, const int* devices) {
+    if (g_cur != 0) return fail("rt_gpu_render_multi: re-entered");
+    const int st = multi_render(p, fb_out, n_devices, devices);
+    g_cur = 0;
+    if (g.inited) (void)hipSetDevice(g.device);
+    return st;
+}
+
+extern "C" int rt_gpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}

@@ -69,6 +69,9 @@ SIGNATURES = [
     ("rt_gpu_profile_ao_kernel", ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_gpu_set_accel", ctypes.c_int, [ctypes.c_int]),
+    ("rt_gpu_render_multi", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p]),
+    ("rt_gpu_device_count", ctypes.c_int, []),
     ("rt_gpu_gamma_u8", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     ("rt_gpu_row_bases", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p]),
@@ -87,6 +90,7 @@ SIGNATURES = [
     ("rt580_set_ao", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     ("rt580_set_rng", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("rt580_set_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    ("rt580_set_gpus", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("rt580_framebuffer", ctypes.POINTER(ctypes.c_int16), [ctypes.c_void_p]),
     ("rt580_get_render_params", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(RenderParams)]),
     ("rt580_get_scene", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SceneSoa)]),
@@ -179,6 +183,9 @@ class Raytracer:
 
     def set_rows(self, row_begin, row_end):
         check(self.lib.rt580_set_rows(self.h, row_begin, row_end), "set_rows")
+
+    def set_gpus(self, n):
+        check(self.lib.rt580_set_gpus(self.h, n), "set_gpus")
 
     def framebuffer(self):
         """Pixel[w*h] as a (h, w, 3) int16 numpy array (copy)."""

@@ -181,6 +181,21 @@ int rt_gpu_shade_rows(const rt_render_params* params, const uint64_t* row_base_d
  * -> row_base_device (uint64[n_max], zero padded). One kernel on the shim's stream. */
 int rt_gpu_row_bases(const int32_t* gathered_device, int world, int n_max, int height, int rank,
                      uint64_t* row_base_device);
+/* Multi-GPU rt_gpu_render inside the library: one process drives
+ * n_devices GPUs (devices: their ids, devices[0] = rt_gpu_init's device; NULL =
+ * consecutive ids from it). Device k renders rows k, k+G, ... (interleaved rows
+ * balance sky and geometry); the per-row AO-call counts are all-gathered
+ * (ncclAllGather), each device scans them into its rows' RNG bases and shades
+ * them, the int16 row tiles go to device 0 (ncclSend/ncclRecv) and are
+ * de-interleaved there, then copied into fb_out (Pixel[w*h], whole frames only).
+ * The scene of context 0 is uploaded to every device on first use. RCCL
+ * (librccl.so.1) is loaded on the first call with distinct devices; a device
+ * listed twice selects device-to-device copies instead (the split rehearsed on
+ * one GPU; RT580_MULTI_TRANSPORT=rccl|local forces either). n_devices == 1 is
+ * rt_gpu_render. Blocking. The image is byte-identical for every G. */
+int rt_gpu_render_multi(const rt_render_params* params, int16_t* fb_out, int n_devices, const int* devices);
+/* Visible HIP devices (0 without a GPU). */
+int rt_gpu_device_count(void);
 /* FlushFrameBufferToPPM's pixel mapping on the device (Raytracer.cpp:812-818):
  * (unsigned char)(powf(c / 255.0f, 1.0f / 2.2f) * 255.0f) per int16 channel,
  * through a 256-entry table built with the host's glibc powf (frame values are
@@ -237,6 +252,9 @@ int rt580_set_depth(rt580_raytracer* rt, int depth);
 int rt580_set_ao(rt580_raytracer* rt, int samples, int enabled);
 int rt580_set_rng(rt580_raytracer* rt, int engine);
 int rt580_set_rows(rt580_raytracer* rt, int row_begin, int row_end);
+/* GPUs Render() shards whole frames across (rt_gpu_render_multi); 0 (default):
+ * $RT580_GPUS if set, else every visible device. */
+int rt580_set_gpus(rt580_raytracer* rt, int n);
 const int16_t* rt580_framebuffer(rt580_raytracer* rt); /* Pixel[w*h] */
 int rt580_get_render_params(rt580_raytracer* rt, rt_render_params* out);
 int rt580_get_scene(rt580_raytracer* rt, rt_scene_soa* out); /* views valid until next load */

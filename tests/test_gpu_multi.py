@@ -1,0 +1,107 @@
+"""Multi-GPU Render inside lib580rt.so (rt_gpu_render_multi):
+interleaved rows per device, the per-row AO-count exchange, RNG bases, shading,
+gather of the row tiles to device 0 and de-interleave. The GPU box has one
+MI355X, so the G-way split runs with every context on device 0 and device
+copies as the transport (a device listed twice selects it); the RCCL transport
+itself runs here with one rank (RT580_MULTI_TRANSPORT=rccl) and on the 8-GPU
+node only in the driver's scaling runs. The frame must be byte-identical to the
+single-GPU render for every G."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import helpers
+from test_gpu_parity import render_gpu
+from test_dropin import assets_dir, build_ref_main
+
+pytestmark = pytest.mark.gpu
+
+
+def _multi(scene, w, h, depth, ao, G, rng=0, root=helpers.ASSETS_ROOT, transport=None):
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    rt = rt580.Raytracer(w, h, root)
+    assert rt.LoadSceneJSON(scene) == 0
+    rt.set_depth(depth)
+    rt.set_ao(ao, True)
+    rt.set_rng(rng)
+    assert rt.InitializeRenderer() == 0
+    params = rt.render_params()
+    s = rt.scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    devs = (ctypes.c_int * G)(*([0] * G))
+    out = np.zeros(w * h * 3, dtype=np.int16)
+    old = os.environ.get("RT580_MULTI_TRANSPORT")
+    if transport:
+        os.environ["RT580_MULTI_TRANSPORT"] = transport
+    try:
+        rt580.check(lib.rt_gpu_render_multi(ctypes.byref(params), out.ctypes.data, G, devs), "rt_gpu_render_multi")
+    finally:
+        if transport:
+            if old is None:
+                del os.environ["RT580_MULTI_TRANSPORT"]
+            else:
+                os.environ["RT580_MULTI_TRANSPORT"] = old
+    rt.close()
+    return out.reshape(h, w, 3)
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_render_multi_matches_single(G):
+    scene, w, h, depth, ao = "simpleSphereScene.json", 97, 61, 4, 64
+    full, _ = render_gpu(scene, w, h, depth, ao, True)
+    got = _multi(scene, w, h, depth, ao, G)
+    assert np.array_equal(got, full), "%d pixels differ" % int((got != full).any(axis=2).sum())
+
+
+def test_render_multi_rccl_transport_one_rank():
+    """The RCCL code path (ncclCommInitAll, ncclAllGather of the row counts) with
+    a single rank on the one GPU of the box."""
+    scene, w, h, depth, ao = "simpleSphereScene.json", 64, 40, 3, 16
+    full, _ = render_gpu(scene, w, h, depth, ao, True)
+    got = _multi(scene, w, h, depth, ao, 1, transport="rccl")
+    assert np.array_equal(got, full)
+
+
+def test_render_multi_bvh_scene():
+    root = helpers.synthetic_root("cornell10k")
+    scene, w, h, depth, ao = "cornell10k.json", 48, 27, 4, 8
+    full, _ = render_gpu(scene, w, h, depth, ao, True, root=root)
+    got = _multi(scene, w, h, depth, ao, 3, root=root)
+    assert np.array_equal(got, full)
+
+
+def test_render_multi_mt19937():
+    """MSVC's engine across ranks: each rank addresses the serial mt19937 stream
+    by absolute draw index (generated up to its rows' last draw)."""
+    entry = next(e for e in helpers.golden_entries(True) if e["name"] == "sss_d2_ao16_mt")
+    got = _multi(entry["scene"], entry["width"], entry["height"], entry["depth"], entry["ao_samples"], 3, rng=1)
+    assert helpers.rt580().ppm_bytes(got) == helpers.golden_ppm(entry)
+
+
+def test_class_render_shards_across_gpus():
+    """Render() of the class surface with set_gpus(4) (four contexts on the
+    box's one device) writes the golden image."""
+    entry = next(e for e in helpers.golden_entries(True) if e["name"] == "teapots_d2_ao4")
+    rt = helpers.rt580().Raytracer(entry["width"], entry["height"], helpers.ASSETS_ROOT)
+    assert rt.LoadSceneJSON(entry["scene"]) == 0
+    rt.set_depth(entry["depth"])
+    rt.set_ao(entry["ao_samples"], entry["ao_enabled"])
+    rt.set_gpus(4)
+    assert rt.Render("") == 0
+    assert helpers.rt580().ppm_bytes(rt.framebuffer()) == helpers.golden_ppm(entry)
+    rt.close()
+
+
+def test_reference_main_with_two_gpus(tmp_path):
+    """The reference's main() through the drop-in with RT580_GPUS=2."""
+    exe = build_ref_main(str(tmp_path))
+    cwd = assets_dir(tmp_path)
+    env = dict(os.environ, RT580_GPUS="2")
+    p = subprocess.run([exe], cwd=cwd, capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr
+    want = next(e for e in helpers.golden_entries(False) if e["name"] == "main_500_d4_ao128")["sha256"]
+    assert helpers.sha256(open(os.path.join(cwd, "output.ppm"), "rb").read()) == want
