@@ -4,10 +4,13 @@
 // 3.11.3 (ExternalPlugins/json.hpp): a token without '.', 'e' or 'E' is an
 // integer (strtoll/strtoull, json.hpp lexer), anything else goes through
 // std::strtod (json.hpp:8290-8292); the scene code then narrows to float with
-// static_cast (json.hpp:4694). Objects keep the last value of a duplicated key
-// and iterate in key order (nlohmann's std::map). Parse errors throw
-// json_min::error, which the loaders turn into RT_FAILURE like the reference's
-// try/catch (Raytracer.cpp:657-663, :775-778).
+// static_cast (json.hpp:4694); a boolean converts to 1/0 like nlohmann's
+// from_json for arithmetic types. Numbers follow the JSON grammar exactly as
+// nlohmann's lexer does (no leading zeros, '+', leading or trailing '.'). A
+// UTF-8 byte-order mark before the document is skipped. Objects keep the last
+// value of a duplicated key and iterate in key order (nlohmann's std::map).
+// Parse errors throw json_min::error, which the loaders turn into RT_FAILURE
+// like the reference's try/catch (Raytracer.cpp:657-663, :775-778).
 #pragma once
 #include <cerrno>
 #include <cstdint>
@@ -47,7 +50,7 @@ struct Value {
             case Int: return static_cast<float>(i);
             case UInt: return static_cast<float>(u);
             case Float: return static_cast<float>(f);
-            case Bool: throw error("type_error: number expected, got boolean");
+            case Bool: return b ? 1.0f : 0.0f;
             default: throw error("type_error: number expected");
         }
     }
@@ -56,6 +59,7 @@ struct Value {
             case Int: return static_cast<int>(i);
             case UInt: return static_cast<int>(u);
             case Float: return static_cast<int>(f);
+            case Bool: return b ? 1 : 0;
             default: throw error("type_error: number expected");
         }
     }
@@ -93,6 +97,9 @@ class Parser {
   public:
     explicit Parser(const std::string& text) : p_(text.c_str()), end_(text.c_str() + text.size()) {}
     Value parse_document() {
+        if (end_ - p_ >= 3 && (unsigned char)p_[0] == 0xEF && (unsigned char)p_[1] == 0xBB &&
+            (unsigned char)p_[2] == 0xBF)
+            p_ += 3;  // UTF-8 BOM (nlohmann's lexer skips it)
         ws();
         Value v = value();
         ws();
@@ -170,6 +177,7 @@ class Parser {
         p_++;  // opening quote
         while (p_ < end_ && *p_ != '"') {
             char c = *p_++;
+            if ((unsigned char)c < 0x20) fail("control character in string");  // must be escaped (nlohmann)
             if (c == '\\') {
                 if (p_ >= end_) fail("bad escape");
                 char e = *p_++;
@@ -201,14 +209,30 @@ class Parser {
         p_++;
         return out;
     }
+    bool digit() const { return p_ < end_ && *p_ >= '0' && *p_ <= '9'; }
+    // -? (0 | [1-9][0-9]*) (. [0-9]+)? ([eE] [+-]? [0-9]+)?  (RFC 8259; what
+    // nlohmann's lexer accepts; a digit right after a leading 0 ends the
+    // number there and the parser then rejects the next token)
     void number(Value& v) {
         const char* s = p_;
         if (*p_ == '-') p_++;
-        if (p_ >= end_ || !(*p_ >= '0' && *p_ <= '9')) fail("bad number");
+        if (!digit()) fail("bad number");
+        if (*p_ == '0') p_++;
+        else
+            while (digit()) p_++;
         bool is_float = false;
-        while (p_ < end_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' || *p_ == '+' || *p_ == '-')) {
-            if (*p_ == '.' || *p_ == 'e' || *p_ == 'E') is_float = true;
+        if (p_ < end_ && *p_ == '.') {
+            is_float = true;
             p_++;
+            if (!digit()) fail("bad number: digit expected after '.'");
+            while (digit()) p_++;
+        }
+        if (p_ < end_ && (*p_ == 'e' || *p_ == 'E')) {
+            is_float = true;
+            p_++;
+            if (p_ < end_ && (*p_ == '+' || *p_ == '-')) p_++;
+            if (!digit()) fail("bad number: digit expected in exponent");
+            while (digit()) p_++;
         }
         std::string tok(s, p_);
         char* e = nullptr;

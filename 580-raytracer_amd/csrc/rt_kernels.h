@@ -131,6 +131,7 @@ hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int h
                             hipStream_t s);
 hipError_t upload_gamma_lut(const uint8_t* lut, hipStream_t s);
 hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
+hipError_t launch_powf_eval(const float* x, float y, float* out, uint64_t n, hipStream_t s);
 hipError_t launch_math_selftest(uint64_t seed, uint64_t n, unsigned long long* bad, hipStream_t s);
 // Per-launch HIP-event timing of the AO ray kernel (profiling; see rt_kernels.hip).
 void kernel_timer_enable(bool on);

@@ -1717,6 +1717,20 @@ __global__ void math_selftest_kernel(uint64_t seed, uint64_t n, unsigned long lo
         if (b[k]) atomicAdd(bad + k, b[k]);
 }
 
+// The device restatement of glibc powf (rt_libm.h), as CalculateLocalColor
+// calls it (Raytracer.cpp:253), over caller-given inputs: checked against the
+// host's glibc by tests/test_gpu_libm.py.
+__global__ void powf_eval_kernel(const float* __restrict__ x, float y, float* __restrict__ out, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = rt_glibc_powf(x[i], y);
+}
+
+hipError_t launch_powf_eval(const float* x, float y, float* out, uint64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(powf_eval_kernel, dim3(grid_for(n, 16384)), dim3(TB), 0, s, x, y, out, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_math_selftest(uint64_t seed, uint64_t n, unsigned long long* bad, hipStream_t s) {
     hipLaunchKernelGGL(math_selftest_kernel, dim3(16384), dim3(TB), 0, s, seed, n, bad);
     return hipGetLastError();

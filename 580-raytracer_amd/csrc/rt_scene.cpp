@@ -76,12 +76,18 @@ int load_scene_json(const std::string& root, const std::string& scene_path, Scen
     int status = RT_SUCCESS;
     try {
         json_min::Value j = json_min::parse(text);
-        const json_min::Value& s = j.at("scene");
+        // jsonData["scene"] (Raytracer.cpp:667): a document without "scene"
+        // (or with a non-object there) has no shapes, camera or lights and
+        // still loads; a document that is not an object is a type error.
+        if (!j.is_object()) throw json_min::error("type_error: cannot use operator[] with a string argument");
+        static const json_min::Value kNull;
+        const json_min::Value& s = j.contains("scene") ? j.at("scene") : kNull;
         if (s.contains("shapes")) {
             for (const json_min::Value* sv : s.at("shapes").items()) {
                 Shape shp;
                 shp.id = sv->at("id").as_string();
                 shp.geometry = sv->at("geometry").as_string();
+                if (sv->contains("notes")) (void)sv->at("notes").as_string();  // get<std::string>() (:673-675)
                 const json_min::Value& m = sv->at("material");
                 shp.material.cs = json_vec3(m.at("Cs"));
                 shp.material.ka = m.at("Ka").as_float();

@@ -757,6 +757,14 @@ int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches) {
     return RT_SUCCESS;
 }
 
+int rt580_eval_powf(const float* x_device, float y, float* out_device, uint64_t n) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (n && (!x_device || !out_device)) return fail("rt580_eval_powf: NULL buffer");
+    HIP_TRY(hipSetDevice(g.device));
+    HIP_TRY(launch_powf_eval(x_device, y, out_device, n, g.stream));
+    return RT_SUCCESS;
+}
+
 int rt_gpu_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* row_base) {
     if (!g.inited) return fail("rt_gpu_init not called");
     if (!gathered || !row_base) return fail("rt_gpu_row_bases: NULL buffer");

@@ -208,6 +208,10 @@ int rt_gpu_gamma_u8(const int16_t* fb_device, uint64_t n_values, uint8_t* out_de
  * (fast sincos + exact fallback), the last three on n seeded random inputs.
  * Blocking. Test hook; not part of the reference's surface. */
 int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches);
+/* The device's glibc-powf restatement (specular term, Raytracer.cpp:253) on n
+ * device inputs x with exponent y -> out (device), on the shim's stream. Test
+ * hook (compared with the host's glibc powf); not part of the reference. */
+int rt580_eval_powf(const float* x_device, float y, float* out_device, uint64_t n);
 /* Scene-query acceleration. RT_ACCEL_BRUTE tests every primitive per ray, as
  * the reference's IntersectScene does (Raytracer.cpp:473-526); RT_ACCEL_AUTO
  * (default) uses the exact-semantics BVH for triangle scenes larger than one

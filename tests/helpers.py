@@ -58,6 +58,24 @@ def synthetic_root(*names):
     return SCENES_ROOT
 
 
+def scene_exponents():
+    """Every specular exponent ("n", the powf exponent of CalculateLocalColor,
+    Raytracer.cpp:253) of the scenes the tests and BASELINE configs render: the
+    reference's Assets/ and the synthetic scenes of configs 3-5."""
+    import glob
+    exps = set()
+    for root in (ASSETS_ROOT, synthetic_root("cornell10k", "field100k", "field1m")):
+        for f in sorted(glob.glob(os.path.join(root, "Assets", "*.json"))):
+            with open(f) as fh:
+                head = fh.read(64)
+            if '"scene"' not in head:
+                continue  # meshes
+            j = json.load(open(f))
+            for sh in j["scene"].get("shapes", []):
+                exps.add(float(np.float32(sh["material"]["n"])))
+    return sorted(exps)
+
+
 def entry_root(entry):
     if entry.get("assets") == "synthetic":
         return synthetic_root(entry["scene"][:-5])

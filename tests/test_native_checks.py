@@ -45,9 +45,13 @@ def test_ao_direction_fast_sincos_bound_and_samples():
 
 
 def test_powf_exhaustive_over_scene_exponents():
-    """Every float x in [0, 1.0001] for each specular exponent in the scene assets
-    (Raytracer.cpp:253; fmax(dot(V,R),0) of unit vectors)."""
-    _run(_build("libm_check"), "powf", "2", "5", "10", "20", "700", "900")
+    """Every float x in [0, 1.0001] for each specular exponent of every scene the
+    path renders: the reference's Assets/ and the synthetic scenes of configs
+    3-5 (Raytracer.cpp:253; fmax(dot(V,R),0) of unit vectors)."""
+    exps = helpers.scene_exponents()
+    assert {2.0, 5.0, 64.0, 120.0, 900.0} <= set(exps) and len(exps) >= 20
+    out = _run(_build("libm_check"), "powf", *["%r" % e for e in exps])
+    assert "checked=%d" % (len(exps) * (0x3f800347 + 1)) in out, out
 
 
 def test_powf_random_pairs():
