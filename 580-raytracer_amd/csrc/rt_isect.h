@@ -430,10 +430,21 @@ RTM_HD bool far_any(const BvhView& V, rv3 o, rv3 d) {
 
 // with_far = false: brute list + spatial BVH only (the caller runs the far
 // search itself, e.g. the sorted wave-cooperative pass of rt_kernels.hip).
-RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true) {
+// tmax (near part only, with_far = false): count a hit only if !(t > tmax) --
+// the reference's point-light shadow test, occluded iff the closest hit has
+// !(t > |light - hit|) (Raytracer.cpp:75), is "some hit with !(t > dist)" for
+// finite t; boxes entered beyond tmax are skipped (the fat box of a hit at t
+// is entered at or before t).
+RTM_HD bool prim_hit_within(const rt_prim& P, rv3 o, rv3 d, float tmax) {
+    float t, a, b, g;
+    const bool h = P.kind == RT_PRIM_TRIANGLE ? tri_test<false, true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+    return h && !(t > tmax);
+}
+
+RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true, float tmax = INFINITY) {
     RT_CNT(brute_tests, V.n_brute);
     for (int k = 0; k < V.n_brute; k++)
-        if (prim_test_any(V.all[V.brute[k]], o, d)) return true;
+        if (prim_hit_within(V.all[V.brute[k]], o, d, tmax)) return true;
     if (!V.has_tree || dir_zero(d)) return false;
     const SlabRay sr = slab_ray(V, o, d);
     uint32_t stk[RT_BVH_STACK];
@@ -444,8 +455,8 @@ RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true) {
             RT_CNT(nodes, 1);
             const BvhNode& nd = V.nodes[c];
             float t0, t1;
-            const bool h0 = nd.n0 >= 0 && slab(nd.lo0, nd.hi0, sr, t0);
-            const bool h1 = nd.n1 >= 0 && slab(nd.lo1, nd.hi1, sr, t1);
+            const bool h0 = nd.n0 >= 0 && slab(nd.lo0, nd.hi0, sr, t0) && !(t0 > tmax);
+            const bool h1 = nd.n1 >= 0 && slab(nd.lo1, nd.hi1, sr, t1) && !(t1 > tmax);
             if (h0 && h1) {
                 const bool first0 = t0 <= t1;
                 stk[sp++] = first0 ? (((uint32_t)nd.n1 << 27) | (uint32_t)nd.c1)
@@ -463,7 +474,7 @@ RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true) {
             RT_CNT(leaf_tris, n);
             for (int k = c; k < c + n; k++) {
                 float t, a, b, g;
-                if (tri_test<false, true>(V.prims[k], o, d, t, a, b, g)) return true;
+                if (tri_test<false, true>(V.prims[k], o, d, t, a, b, g) && !(t > tmax)) return true;
             }
         }
         if (sp == 0) break;

@@ -25,9 +25,10 @@ struct DevScene {
     // far-origin rays reads them this way (any order gives the same boolean;
     // accepted primitives come clustered by mesh in scene order, see far_scan_kernel).
     const rt_prim* scan_prims;
-    // scene indices of the directional lights (host-side launch loop), <= 8
-    int n_dir;
-    int dir_light[8];
+    // scene indices of the shadow-casting (directional and point) lights, in
+    // JSON order, for the host-side launch loop of the shadow passes; <= 8
+    int n_shadow;
+    int shadow_light[8];
     BvhView bv;
 };
 
@@ -102,10 +103,10 @@ struct DevWork {
     // far phases of a BVH trace level: (t, alpha, beta, gamma), prim (-1: none)
     float4* hit4;          // [node_cap]
     int32_t* hit_prim;     // [node_cap]
-    // directional-light shadow rays of a BVH trace level, decided before the
-    // shading phase: [directional light k][item - chunk start] occluded flags
-    // (near any-hit pass + the sorted far pass), far_cap entries per light
-    uint8_t* shadow;       // [n_directional * far_cap] or null
+    // shadow rays of a BVH trace level, decided before the shading phase:
+    // [shadow light k][item - chunk start] occluded flags (near pass + the
+    // sorted far pass / brute scan), far_cap entries per light
+    uint8_t* shadow;       // [n_shadow * far_cap] or null
     // AO samples whose fast sincos rounding test failed (rt_libm.h), recomputed
     // exactly by ao_fix_kernel: item ids, count (may exceed the capacity)
     uint64_t* aofix_items; // [aofix_cap]

@@ -582,25 +582,44 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
         }
         if (PHASE == 3) {
             // the shadow ray of the shading phase (Raytracer.cpp:59-75), same
-            // float operations as below: hit point o + d t, origin hp + L * 0.2
+            // float operations as below: hit point o + d t, origin hp + L * 0.2.
+            // Directional: occluded iff any hit. Point: iff the closest hit has
+            // !(t > dist), i.e. some hit has !(t > dist) (tmax); a far hit
+            // (t >= T, rt_bvh.h) cannot have t <= dist unless dist >= T, and
+            // those rare rays go to the brute scan, which applies the bound.
             bool q = false, brute = false, lit = false;
             uint8_t flag = 0;
             rv3 so = v3(0, 0, 0), L2 = v3(1, 0, 0);
+            float tmax = INFINITY;
             if (active && W.hit_prim[node] >= 0) {
                 const float t = W.hit4[node].x;
                 const rt_light l = S.lights[light];
                 const rv3 hp = v3_add(o, v3_scale(d, t));
-                L2 = ld3(l.L2);
-                so = v3_add(hp, v3_scale(ld3(l.L), 0.2f));
+                rv3 L;
+                if (l.kind == RT_LIGHT_DIRECTIONAL) {
+                    L = ld3(l.L);
+                    L2 = ld3(l.L2);
+                } else {
+                    const rv3 tl = v3_sub(ld3(l.position), hp);
+                    L = v3_normalize(tl);
+                    L2 = v3_normalize(L);
+                    tmax = v3_length(tl);
+                }
+                so = v3_add(hp, v3_scale(L, 0.2f));
                 brute = far_origin(S, so);
+                if (!brute && l.kind != RT_LIGHT_DIRECTIONAL) {
+                    const FarNode root = load_far_node(S.bv.far_nodes, 0);
+                    brute = !(tmax < far_T(far_ray(S.bv, so), root.min_dhi));
+                }
                 lit = true;
             }
             // per lane, or (wave_near, A/B) one wave-cooperative near traversal:
-            // neighbouring pixels' shadow rays share the light's direction
-            const bool nh = wave_near ? bvh_any_near_wave(S.bv, lit && !brute, so, L2, wstk[threadIdx.x >> 6])
-                                      : (lit && !brute && bvh_any(S.bv, so, L2, /*with_far=*/false));
+            // neighbouring pixels' shadow rays share a directional light's direction
+            const bool nh = (wave_near && isinf(tmax))
+                                ? bvh_any_near_wave(S.bv, lit && !brute, so, L2, wstk[threadIdx.x >> 6])
+                                : (lit && !brute && bvh_any(S.bv, so, L2, /*with_far=*/false, tmax));
             if (nh) flag = 1;
-            else q = lit && (brute || !dir_zero(L2));
+            else q = lit && (brute || (!dir_zero(L2) && isinf(tmax)));
             if (active) W.shadow[(size_t)dl * W.far_cap + (item - i0)] = flag;
             const uint64_t bm = __ballot(brute);
             if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
@@ -613,7 +632,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                 if (q) {
                     const uint32_t slot = qb + (uint32_t)__popcll(qm & lanemask_lt());
                     W.far_rays[2 * (size_t)slot] = make_float4(so.x, so.y, so.z, __uint_as_float(item - i0));
-                    W.far_rays[2 * (size_t)slot + 1] = make_float4(L2.x, L2.y, L2.z, 0.0f);
+                    W.far_rays[2 * (size_t)slot + 1] = make_float4(L2.x, L2.y, L2.z, tmax);
                     W.far_keys[slot] = brute ? RT_KEY_BRUTE : dir_key(L2);
                     W.far_vals[slot] = slot;
                 }
@@ -651,7 +670,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
         // (those need AO; int16 wrap-around addition commutes, so they are added
         // in resolve_kernel).
         rpix local = px(0, 0, 0);
-        int dli = 0;  // index among the directional lights
+        int dli = 0;  // index among the shadow-casting lights
         for (int li = 0; li < S.n_lights; li++) {
             const rt_light l = S.lights[li];
             if (l.kind == RT_LIGHT_AMBIENT) continue;
@@ -670,7 +689,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                 so = v3_add(hi.p, v3_scale(L, 0.2f));
             }
             bool occluded;
-            if (PHASE == 2 && l.kind == RT_LIGHT_DIRECTIONAL && W.shadow) {
+            if (PHASE == 2 && W.shadow) {
                 occluded = hit && W.shadow[(size_t)dli * W.far_cap + (item - i0)] != 0;  // decided by PHASE 3
                 dli++;
             } else if (l.kind == RT_LIGHT_DIRECTIONAL) {
@@ -1022,7 +1041,7 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                 if (q) {
                     const uint32_t slot = base + (uint32_t)__popcll(qm & lanemask_lt());
                     W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
-                    W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+                    W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, INFINITY);  // .w: t bound
                     W.far_keys[slot] = ao_brute ? RT_KEY_BRUTE : dir_key(d);
                     W.far_vals[slot] = slot;
                 }
@@ -1073,7 +1092,7 @@ __device__ void ao_fix_item(const DevScene& S, const DevFrame& F, const DevWork&
             if (brute) atomicAdd(W.far_count + 1, 1u);
             const uint32_t slot = atomicAdd(W.far_count, 1u);
             W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
-            W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+            W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, INFINITY);
             W.far_keys[slot] = brute ? RT_KEY_BRUTE : dir_key(d);
             W.far_vals[slot] = slot;
             return;
@@ -1313,7 +1332,8 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
         const uint32_t r = W.far_vals_alt[i];
         const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
         const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
-        const uint32_t tag = __float_as_uint(a.w);  // AO call (any) or tree node (closest)
+        const uint32_t tag = __float_as_uint(a.w);  // AO call / shadow flag (any) or tree node (closest)
+        const float tmax = b.w;                     // any-hit: count a hit only if !(t > tmax)
         if (!brute && dir_zero(d)) continue;
         const FarRay fr = far_ray(S.bv, o);
         if (!closest) {
@@ -1332,7 +1352,7 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
                     }
 #pragma unroll
                     for (int u = 0; u < BRUTE_ANY_U; u++)
-                        if (k0 + u * 64 + lane < n_scan && prim_test_any(p[u], o, d)) hit = true;
+                        if (k0 + u * 64 + lane < n_scan && prim_hit_within(p[u], o, d, tmax)) hit = true;
                     if (__ballot(hit)) break;
                 }
             }
@@ -1970,8 +1990,8 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 // shadow rays of the directional lights: near any-hit, then the
                 // sorted far pass (brute scan for far-origin rays), like AO rays
                 if (W.shadow) {
-                    for (int dl = 0; dl < S.n_dir; dl++) {
-                        const int li = S.dir_light[dl];
+                    for (int dl = 0; dl < S.n_shadow; dl++) {
+                        const int li = S.shadow_light[dl];
                         if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
                         RT_STEP("trace shadow near pass");
                         hipLaunchKernelGGL((trace_kernel<true, 3>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1,
@@ -2118,16 +2138,9 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         return hipSuccess;
     }
     const int v = ao_variant();  // (frame_init_kernel zeroed W.aofix_count)
-    uint64_t items = 0;
-    if (g_kt.on) {  // the AO sample count of this launch (profiling only: a D2H read)
-        uint64_t calls = 0;
-        if (hipMemcpyAsync(&calls, W.totals, 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
-            hipStreamSynchronize(s) == hipSuccess)
-            items = calls * (uint64_t)F.ao_samples;
-    }
     kt_begin(s);
     const hipError_t e = launch_ao_small(S, F, W, s, v);
-    kt_end(s, items);
+    kt_end(s, 0);  // one launch per frame: its AO rays are the frame's (no host sync here)
     if (e != hipSuccess || !(v & 4096)) return e;
     return launch_ao_fix(S, F, W, 0, ~0ull, s);
 }

@@ -55,7 +55,7 @@ struct State {
     // scene
     DevBuf prims, shade, mats, lights;
     int n_prims = 0, n_lights = 0, n_ambient = 0, n_nonambient = 0;
-    std::vector<int> dir_lights;  // scene indices of the directional lights
+    std::vector<int> shadow_lights;  // scene indices of the directional and point lights
     bool have_scene = false;
     // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
     DevBuf bvh_nodes, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always, scan_prims;
@@ -247,9 +247,9 @@ DevScene dev_scene(const rt_render_params* p) {
     s.n_ambient = g.n_ambient;
     s.use_bvh = g.accel == RT_ACCEL_AUTO && g.bvh_ok && bvh_usable(g.bvh, p->cam_from);
     s.scan_prims = g.scan_prims.p ? (const rt_prim*)g.scan_prims.p : s.prims;
-    s.n_dir = 0;
-    if ((int)g.dir_lights.size() <= 8)
-        for (int li : g.dir_lights) s.dir_light[s.n_dir++] = li;
+    s.n_shadow = 0;
+    if ((int)g.shadow_lights.size() <= 8)
+        for (int li : g.shadow_lights) s.shadow_light[s.n_shadow++] = li;
     BvhView& v = s.bv;
     v.all = s.prims;
     v.nodes = (const BvhNode*)g.bvh_nodes.p;
@@ -345,9 +345,9 @@ DevWork dev_work() {
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
     w.hit4 = split ? (float4*)g.hit4.p : nullptr;
     w.hit_prim = split ? (int32_t*)g.hit_prim.p : nullptr;
-    // shadow flags of the split trace's directional lights (more than 8: decided in the shading phase)
-    w.shadow = (split && g.shadow.p && !g.dir_lights.empty() && g.dir_lights.size() <= 8) ? (uint8_t*)g.shadow.p
-                                                                                              : nullptr;
+    // shadow flags of the split trace's lights (more than 8: decided in the shading phase)
+    w.shadow = (split && g.shadow.p && !g.shadow_lights.empty() && g.shadow_lights.size() <= 8) ? (uint8_t*)g.shadow.p
+                                                                                                    : nullptr;
     w.aofix_items = (uint64_t*)SL.aofix_items.p;
     w.aofix_count = (uint32_t*)SL.aofix_count.p;
     w.aofix_cap = (uint32_t)(SL.aofix_items.bytes / 8);
@@ -406,8 +406,8 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     if (g.bvh_ok && !g.bvh.far_nodes.empty() &&
         (ensure(g.hit4, (size_t)cap * 16) || ensure(g.hit_prim, (size_t)cap * 4)))
         return RT_FAILURE;
-    if (g.bvh_ok && !g.bvh.far_nodes.empty() && !g.dir_lights.empty() && g.dir_lights.size() <= 8 &&
-        ensure(g.shadow, g.dir_lights.size() * (size_t)g.far_cap))
+    if (g.bvh_ok && !g.bvh.far_nodes.empty() && !g.shadow_lights.empty() && g.shadow_lights.size() <= 8 &&
+        ensure(g.shadow, g.shadow_lights.size() * (size_t)g.far_cap))
         return RT_FAILURE;
     return RT_SUCCESS;
 }
@@ -631,11 +631,11 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     g.n_lights = s->n_lights;
     g.n_ambient = 0;
     g.n_nonambient = 0;
-    g.dir_lights.clear();
+    g.shadow_lights.clear();
     for (int i = 0; i < s->n_lights; i++) {
         if (s->lights[i].kind == RT_LIGHT_AMBIENT) g.n_ambient++;
         else g.n_nonambient++;
-        if (s->lights[i].kind == RT_LIGHT_DIRECTIONAL) g.dir_lights.push_back(i);
+        if (s->lights[i].kind != RT_LIGHT_AMBIENT) g.shadow_lights.push_back(i);
     }
     g.have_scene = true;
     g.scene_gen = ++g_scene_counter;

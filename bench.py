@@ -275,7 +275,10 @@ def main():
         }
         if check_ok is not None:
             out["frame_matches_reference"] = check_ok
-        out["roofline"] = roofline(args.workload, k_ms.value, k_launches.value, k_rays.value, int(local["rays_ao"]))
+        # AO rays per timed launch: the chunked BVH launches report theirs; a
+        # small-scene frame is one launch over all of its AO rays
+        k_units = k_rays.value if k_rays.value else int(local["rays_ao"]) * max(frames.value, 1)
+        out["roofline"] = roofline(args.workload, k_ms.value, k_launches.value, k_units, int(local["rays_ao"]))
         if world == 1 and K == 1:
             out["render_call_ms"] = render_latency(lib, rt580, params, torch)
         if world == 1 and not args.no_cpu_baseline:

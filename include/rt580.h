@@ -233,7 +233,9 @@ int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double
 /* While profiling: HIP events around every launch of the AO ray kernel (the
  * scene query of each AO sample: ao_kernel, or ao_near_kernel for BVH scenes),
  * on the stream it runs on. Sum of their durations, number of launches and the
- * AO rays they covered, since rt_gpu_profile(1). Synchronizes. */
+ * AO rays they covered, since rt_gpu_profile(1) (ao_rays counts the chunked BVH
+ * launches only; a small-scene frame is one launch over all of its AO rays,
+ * rt_gpu_last_stats). Synchronizes. */
 int rt_gpu_profile_ao_kernel(double* ms_total, int* launches, uint64_t* ao_rays);
 /* Last error message (static storage). */
 const char* rt_gpu_last_error(void);

@@ -110,7 +110,7 @@ int main(int argc, char** argv) {
         if (P[j].kind == RT_PRIM_TRIANGLE) tris.push_back(j);
     BvhView Vnear = V;  // control: without the far search some results must differ
     Vnear.has_far = 0;
-    std::atomic<long> bad{0}, hits{0}, anyhits{0}, far_closest{0}, near_only_bad{0};
+    std::atomic<long> bad{0}, hits{0}, anyhits{0}, far_closest{0}, near_only_bad{0}, point_checks{0};
 #ifdef RT_BVH_COUNT
     std::atomic<long> cnt[2][6] = {};  // [closest, any][counter]
 #endif
@@ -166,7 +166,20 @@ int main(int argc, char** argv) {
                     for (int q = 0; q < 6; q++) cnt[1][q] += c[q];
                 }
 #endif
-                bool same = cb == cv && ab == av;
+                // point-light shadow form (Raytracer.cpp:75): occluded iff the
+                // closest hit has !(t > dist); near query with the t bound, valid
+                // when dist is below every far threshold (rt_kernels.hip PHASE 3)
+                bool point_ok = true;
+                if (V.has_far) {
+                    const float dist = std::ldexp(U(rng), (int)(rng() % 6)) ;  // (0, 32)
+                    const float Troot = far_T(far_ray(V, o), B.far_nodes[0].min_dhi);
+                    if (dist < Troot) {
+                        const bool want = cb && !(hb.t > dist);
+                        point_ok = bvh_any(V, o, d, /*with_far=*/false, dist) == want;
+                        point_checks++;
+                    }
+                }
+                bool same = cb == cv && ab == av && point_ok;
                 if (same && cb)
                     same = hb.prim == hv.prim && fbits(hb.t) == fbits(hv.t) && fbits(hb.a) == fbits(hv.a) &&
                            fbits(hb.b) == fbits(hv.b) && fbits(hb.g) == fbits(hv.g);
@@ -199,6 +212,7 @@ int main(int argc, char** argv) {
     }
 #endif
     std::printf("rays=%ld closest_hits=%ld any_hits=%ld far_closest_hits=%ld differ_without_far_search=%ld "
-                "mismatches=%ld\n", nrays, (long)hits, (long)anyhits, (long)far_closest, (long)near_only_bad, (long)bad);
+                "point_shadow_checks=%ld mismatches=%ld\n", nrays, (long)hits, (long)anyhits, (long)far_closest,
+                (long)near_only_bad, (long)point_checks, (long)bad);
     return bad ? 1 : 0;
 }
