@@ -9,6 +9,8 @@ for W in "$@"; do
   tools/profile.sh ${TAG}_$W --workload $W || exit 1
   python tools/roofline_from_profile.py gpurun_out/prof_${TAG}_$W $W > gpurun_out/roofline_$W.json || exit 1
   python tools/summarize_profile.py gpurun_out/prof_${TAG}_$W gpurun_out/prof_${TAG}_$W/summary.json || exit 1
+  # the raw per-dispatch CSVs are large (gpurun copies back <= 64 MiB): keep the summaries
+  rm -f gpurun_out/prof_${TAG}_$W/pmc*_counter_collection.csv gpurun_out/prof_${TAG}_$W/trace_kernel_trace.csv
 done
 for W in "$@"; do
   timeout -k 10 900 python bench.py --workload $W > gpurun_out/bench_${TAG}_$W.json 2> gpurun_out/bench_${TAG}_$W.err || { tail -5 gpurun_out/bench_${TAG}_$W.err; exit 1; }
