@@ -383,6 +383,64 @@ bool bvh_usable(const BvhBuild& b, const float cam_from[3]) {
     return max_abs3(cam_from) <= 1e6f * b.scale;
 }
 
+// ---------------------------------------------------------------- 4-wide collapse
+namespace {
+int32_t collapse4(const std::vector<BvhNode>& bin, int32_t b, std::vector<Bvh4Node>& out, int level, int& depth) {
+    depth = std::max(depth, level);
+    struct Entry {
+        int32_t c, n;
+        float lo[3], hi[3];
+    };
+    Entry e[4];
+    int ne = 0;
+    auto add = [&](int32_t c, int32_t n, const float* lo, const float* hi) {
+        if (n < 0) return;  // empty
+        Entry& x = e[ne++];
+        x.c = c;
+        x.n = n;
+        for (int k = 0; k < 3; k++) { x.lo[k] = lo[k]; x.hi[k] = hi[k]; }
+    };
+    const BvhNode& nd = bin[b];
+    for (int side = 0; side < 2; side++) {
+        const int32_t c = side ? nd.c1 : nd.c0, n = side ? nd.n1 : nd.n0;
+        const float* lo = side ? nd.lo1 : nd.lo0;
+        const float* hi = side ? nd.hi1 : nd.hi0;
+        if (n == 0) {  // internal: take its two children (their boxes as stored in it)
+            const BvhNode& m = bin[c];
+            add(m.c0, m.n0, m.lo0, m.hi0);
+            add(m.c1, m.n1, m.lo1, m.hi1);
+        } else {
+            add(c, n, lo, hi);
+        }
+    }
+    const int32_t id = (int32_t)out.size();
+    out.emplace_back();
+    Bvh4Node q;
+    for (int j = 0; j < 4; j++) {
+        for (int k = 0; k < 3; k++) { q.lo[k][j] = 0.0f; q.hi[k][j] = 0.0f; }
+        q.c[j] = 0;
+        q.n[j] = -1;
+    }
+    for (int j = 0; j < ne; j++) {
+        for (int k = 0; k < 3; k++) { q.lo[k][j] = e[j].lo[k]; q.hi[k][j] = e[j].hi[k]; }
+        q.n[j] = e[j].n;
+        q.c[j] = e[j].n == 0 ? collapse4(bin, e[j].c, out, level + 1, depth) : e[j].c;
+    }
+    out[id] = q;
+    return id;
+}
+}  // namespace
+
+void collapse_bvh4(BvhBuild& out) {
+    out.nodes4.clear();
+    if (out.nodes.empty()) return;
+    out.nodes4.reserve(out.nodes.size() / 2 + 8);
+    int depth = 0;
+    collapse4(out.nodes, 0, out.nodes4, 1, depth);
+    // a traversal stacks at most 3 entries per level
+    if (3 * depth + 1 > RT_BVH_STACK) out.nodes4.clear();
+}
+
 }  // namespace rt580
 
 namespace rt580 {

@@ -54,6 +54,19 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode is one 64-byte line");
 
+// 4-wide form of the same spatial BVH (collapse_bvh4: a node's children are
+// its binary node's children and grandchildren, with the boxes the binary tree
+// stores for them): the same boxes and leaves, half the depth. Boxes as
+// lo[axis][child] / hi[axis][child]; child link as BvhNode's (n == 0: node
+// `c` of this array; n > 0: leaf slots [c, c + n); n < 0: empty). 128 bytes.
+struct alignas(16) Bvh4Node {
+    float lo[3][4];
+    float hi[3][4];
+    int32_t c[4];
+    int32_t n[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node is two 64-byte lines");
+
 // Plane-tree node (own bounds): normals in [nlo, nhi], plane offsets D in
 // [dlo, dhi], and the subtree minima of D_hi and delta (for its T bound).
 // count > 0: leaf of far_tris [first, first + count); else children first, first + 1.
@@ -80,6 +93,7 @@ static_assert(sizeof(FarTri) == 32, "FarTri layout");
 
 struct BvhBuild {
     std::vector<BvhNode> nodes;     // node 0 is the root
+    std::vector<Bvh4Node> nodes4;   // the same tree 4-wide (collapse_bvh4); node 0 is the root
     std::vector<rt_prim> prims;     // near-set triangles in leaf order (copies of the scene records)
     std::vector<uint32_t> ids;      // scene index of each slot (tie-break + shading lookups)
     std::vector<FarNode> far_nodes; // node 0 is the root (empty when no far-set triangle)
@@ -107,6 +121,9 @@ struct BvhBuild {
 // Build over prims[0..n). Returns false if there are no triangles or a tree
 // would exceed the device stack (the caller then keeps brute force).
 bool build_bvh(const rt_prim* prims, int n, BvhBuild& out);
+
+// The 4-wide form of out.nodes (after build_bvh).
+void collapse_bvh4(BvhBuild& out);
 
 // Build the far-search direction grid over out.far_tris (after build_bvh; the
 // query side is rt_isect.h grid_cell / far_any / far_closest).

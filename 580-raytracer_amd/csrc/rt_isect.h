@@ -104,6 +104,7 @@ RTM_HD bool prim_test_any(const rt_prim& P, rv3 o, rv3 d) {
 struct BvhView {
     const rt_prim* all;         // scene primitives by index
     const BvhNode* nodes;
+    const Bvh4Node* nodes4;     // the same tree 4-wide (any-hit queries); null: binary only
     const rt_prim* prims;       // spatial leaf order
     const uint32_t* ids;
     const FarNode* far_nodes;
@@ -172,48 +173,67 @@ RTM_HD bool lex_better(float t, int id, bool found, const Hit& h) {
 // within D_lo + h of the triangle (rt_bvh.h), and the exact ray point o + d t
 // within u (2t + |o|) of Pp per component. So the exact ray meets the triangle's
 // box (inflated by delta_j >= D_lo) grown by alpha + beta t with
-// alpha = 32u (|o| + S) >= u |o| + h + rounding, beta = 16u >= 2u + slack for
-// the rounding of the slab arithmetic itself. Per axis:
-//   (d + beta) t >= lo - alpha - o   and   (d - beta) t <= hi + alpha - o
-// with the three sign cases of d +- beta; the culling is then conservative for
-// every t, with no bound on the ray length.
+// alpha >= u |o| + h + rounding, beta = 16u >= 2u + slack for the rounding of
+// the slab arithmetic itself. Per axis, for t >= 0:
+//   c_lo t >= lo - alpha - o   and   c_hi t <= hi + alpha - o
+// with c_lo = d + beta, c_hi = d - beta. Raising c_lo or lowering c_hi only
+// weakens a constraint at t >= 0, so for |d| <= beta (where c_lo, c_hi may be
+// 0) c_lo = max(d + beta, beta), c_hi = min(d - beta, -beta): every reciprocal
+// is finite. Each bound is one FMA, lo * (1/c_lo) - (o + alpha) / c_lo; the
+// rounding of the hoisted product (o + alpha) / c_lo and of o + alpha moves
+// the plane by at most 2u (|o| + alpha), which alpha = 40u (|o| + S) covers
+// on top of the 32u the bound itself needs. The culling is then conservative
+// for every t >= 0, with no bound on the ray length.
+//   Per axis the two plane distances t1 (lo), t2 (hi) give, for d > beta, the
+// interval [t1, t2]; for d < -beta [t2, t1]; for |d| <= beta [max(t1, t2),
+// inf). With k = -inf (|d| > beta) or +inf (|d| <= beta): low =
+// med3(t1, t2, k), high = max(t1, t2, k) -- for |d| > beta the min/max form
+// can only widen an interval whose planes are both behind the origin, which
+// the high >= 0 test rejects anyway.
 struct SlabRay {
-    rv3 o;
-    float ip[3], im[3];  // 1/(d + beta), -1/(beta - d)
-    int mode[3];         // 1: d > beta, -1: d < -beta, 0: |d| <= beta
-    float alpha;
+    float ip[3], im[3];  // 1 / c_lo, 1 / c_hi
+    float nol[3], noh[3];  // -(o + alpha) / c_lo, -(o - alpha) / c_hi
+    float k[3];          // -inf, or +inf for |d| <= beta
 };
+
+RTM_HD float rt_med3(float a, float b, float c) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_fmed3f(a, b, c);
+#else
+    return fmaxf(fminf(a, b), fminf(fmaxf(a, b), c));
+#endif
+}
 
 RTM_HD SlabRay slab_ray(const BvhView& V, rv3 o, rv3 d) {
     SlabRay r;
-    r.o = o;
     const float beta = 16.0f * RT_U;
-    const float dv[3] = {d.x, d.y, d.z};
-    for (int k = 0; k < 3; k++) {
-        r.ip[k] = 1.0f / (dv[k] + beta);
-        r.im[k] = -1.0f / (beta - dv[k]);
-        r.mode[k] = dv[k] > beta ? 1 : (dv[k] < -beta ? -1 : 0);
-    }
+    const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
     const float oi = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
-    r.alpha = 32.0f * RT_U * (oi + V.scale);
+    const float alpha = 40.0f * RT_U * (oi + V.scale);
+    for (int k = 0; k < 3; k++) {
+        const bool par = !(dv[k] > beta) && !(dv[k] < -beta);
+        const float clo = par ? fmaxf(dv[k] + beta, beta) : dv[k] + beta;
+        const float chi = par ? fminf(dv[k] - beta, -beta) : dv[k] - beta;
+        r.ip[k] = 1.0f / clo;
+        r.im[k] = 1.0f / chi;
+        r.nol[k] = -((ov[k] + alpha) * r.ip[k]);
+        r.noh[k] = -((ov[k] - alpha) * r.im[k]);
+        r.k[k] = par ? INFINITY : -INFINITY;
+    }
     return r;
 }
 
-// NaN-ignoring min/max: a NaN bound comes from 0 * inf, i.e. a constraint that
-// holds for every t.
+// Entry distance tn = max(0, low) of the fat box; accepted iff tn <= high.
 RTM_HD bool slab(const float* lo, const float* hi, const SlabRay& r, float& tn) {
-    const float ov[3] = {r.o.x, r.o.y, r.o.z};
-    float tmin = -INFINITY, tmax = INFINITY;
+    float tmin = 0.0f, tmax = INFINITY;
     for (int k = 0; k < 3; k++) {
-        const float t1 = ((lo[k] - r.alpha) - ov[k]) * r.ip[k];
-        const float t2 = ((hi[k] + r.alpha) - ov[k]) * r.im[k];
-        const float l = r.mode[k] > 0 ? t1 : (r.mode[k] < 0 ? t2 : fmaxf(t1, t2));
-        const float h = r.mode[k] > 0 ? t2 : (r.mode[k] < 0 ? t1 : INFINITY);
-        tmin = fmaxf(tmin, l);
-        tmax = fminf(tmax, h);
+        const float t1 = fmaf(lo[k], r.ip[k], r.nol[k]);
+        const float t2 = fmaf(hi[k], r.im[k], r.noh[k]);
+        tmin = fmaxf(tmin, rt_med3(t1, t2, r.k[k]));
+        tmax = fminf(tmax, fmaxf(fmaxf(t1, t2), r.k[k]));
     }
     tn = tmin;
-    return tmin <= tmax && tmax >= 0.0f;
+    return tmin <= tmax;
 }
 
 // Far-search threshold for a ray: a hit with t < T_j = (D_hi(j) - R)(1 - 1e-4),
@@ -484,6 +504,99 @@ RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true, float 
     }
     if (!V.has_far || !with_far) return false;
     return far_any(V, o, d);
+}
+
+// Whole-record loads (one batch of 16-byte loads per node / primitive on the
+// device, so a traversal step waits for memory once, not once per field).
+RTM_HD void load_node4(const Bvh4Node* p, Bvh4Node& out) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const float4* s = reinterpret_cast<const float4*>(p);
+    float4* d = reinterpret_cast<float4*>(&out);
+#pragma unroll
+    for (int i = 0; i < 8; i++) d[i] = s[i];
+#else
+    out = *p;
+#endif
+}
+RTM_HD void load_prim(const rt_prim* p, rt_prim& out) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const float4* s = reinterpret_cast<const float4*>(p);
+    float4* d = reinterpret_cast<float4*>(&out);
+#pragma unroll
+    for (int i = 0; i < 4; i++) d[i] = s[i];
+#else
+    out = *p;
+#endif
+}
+
+// bvh_any's near part over the 4-wide tree (same boxes, same leaves, same
+// tests; only the grouping differs, so the same boolean). Per node: the fat
+// slab test of its up to four children (branch-free), the nearest accepted
+// child entered, the other accepted ones stacked. While-while loop: a lane
+// descends inner nodes until it holds a leaf, then tests the leaf.
+RTM_HD bool bvh4_any_near(const BvhView& V, rv3 o, rv3 d, float tmax = INFINITY) {
+    RT_CNT(brute_tests, V.n_brute);
+    for (int k = 0; k < V.n_brute; k++)
+        if (prim_hit_within(V.all[V.brute[k]], o, d, tmax)) return true;
+    if (!V.has_tree || dir_zero(d)) return false;
+    const SlabRay sr = slab_ray(V, o, d);
+    uint32_t stk[RT_BVH_STACK + 4];
+    int sp = 0;
+    int32_t c = 0, n = 0;  // root (internal)
+    for (;;) {
+        while (n == 0) {
+            RT_CNT(nodes, 1);
+            Bvh4Node nd;
+            load_node4(V.nodes4 + c, nd);
+            float t[4];
+            bool ok[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float lo[3] = {nd.lo[0][j], nd.lo[1][j], nd.lo[2][j]};
+                const float hi[3] = {nd.hi[0][j], nd.hi[1][j], nd.hi[2][j]};
+                const bool in = slab(lo, hi, sr, t[j]);
+                ok[j] = (nd.n[j] >= 0) & in & !(t[j] > tmax);
+            }
+            int best = -1;
+            float bt = INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (ok[j] & ((best < 0) | (t[j] < bt))) {
+                    best = j;
+                    bt = t[j];
+                }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                stk[sp] = ((uint32_t)nd.n[j] << 27) | (uint32_t)nd.c[j];
+                sp += (ok[j] & (j != best)) ? 1 : 0;
+            }
+            if (best >= 0) {
+                c = best == 0 ? nd.c[0] : best == 1 ? nd.c[1] : best == 2 ? nd.c[2] : nd.c[3];
+                n = best == 0 ? nd.n[0] : best == 1 ? nd.n[1] : best == 2 ? nd.n[2] : nd.n[3];
+            } else {
+                if (sp == 0) return false;
+                sp--;
+                c = (int32_t)(stk[sp] & 0x7ffffffu);
+                n = (int32_t)(stk[sp] >> 27);
+            }
+        }
+        RT_CNT(leaf_tris, n);
+        for (int k = c; k < c + n; k++) {
+            rt_prim P;
+            load_prim(V.prims + k, P);
+            float tt, a, b, g;
+            if (tri_test<false, true>(P, o, d, tt, a, b, g) && !(tt > tmax)) return true;
+        }
+        if (sp == 0) return false;
+        sp--;
+        c = (int32_t)(stk[sp] & 0x7ffffffu);
+        n = (int32_t)(stk[sp] >> 27);
+    }
+}
+
+// The near any-hit query: 4-wide tree when present, else the binary one.
+RTM_HD bool bvh_any_near(const BvhView& V, rv3 o, rv3 d, float tmax = INFINITY) {
+    return V.nodes4 ? bvh4_any_near(V, o, d, tmax) : bvh_any(V, o, d, /*with_far=*/false, tmax);
 }
 
 }  // namespace rt580

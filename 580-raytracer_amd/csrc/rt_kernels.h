@@ -99,6 +99,9 @@ struct DevWork {
     void* sort_tmp;
     size_t sort_tmp_bytes;
     uint32_t far_cap;
+    // split AO pass (ao_trace_kernel): (o.xyz, call), (d.xyz, flag) per item of a chunk
+    float4* ao_rays;       // [2 * ao_cap] or null
+    uint32_t ao_cap;
     // provisional closest hits of the tree rays (node id) between the near and
     // far phases of a BVH trace level: (t, alpha, beta, gamma), prim (-1: none)
     float4* hit4;          // [node_cap]

@@ -617,7 +617,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             // neighbouring pixels' shadow rays share a directional light's direction
             const bool nh = (wave_near && isinf(tmax))
                                 ? bvh_any_near_wave(S.bv, lit && !brute, so, L2, wstk[threadIdx.x >> 6])
-                                : (lit && !brute && bvh_any(S.bv, so, L2, /*with_far=*/false, tmax));
+                                : (lit && !brute && bvh_any_near(S.bv, so, L2, tmax));
             if (nh) flag = 1;
             else q = lit && (brute || (!dir_zero(L2) && isinf(tmax)));
             if (active) W.shadow[(size_t)dl * W.far_cap + (item - i0)] = flag;
@@ -898,6 +898,41 @@ __device__ __forceinline__ void ao_draws(const DevFrame& F, const DevWork& W, ui
     }
 }
 
+// After an AO ray's any-hit query: BVH scenes queue the near misses for the
+// sorted far-hit pass (and count the far-origin rays); hits count towards the
+// call's occlusion (W.occ). With N a multiple of 64 a wave holds one call's
+// samples (items are aligned chunks), so one atomic per wave.
+template <bool BVH>
+__device__ __forceinline__ void ao_finish(const DevScene& S, const DevWork& W, uint32_t N, bool active, bool ao_brute,
+                                          bool hit, uint64_t c, rv3 o, rv3 d) {
+    if (BVH) {
+        // rays that miss every near triangle go to the sorted far-hit pass
+        const bool q = active && !hit && S.bv.has_far;
+        const uint64_t qm = __ballot(q);
+        const uint64_t bm = __ballot(ao_brute);
+        if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
+        if (qm) {
+            const int leader = __ffsll((unsigned long long)qm) - 1;
+            uint32_t base = 0;
+            if ((threadIdx.x & 63) == leader) base = atomicAdd(W.far_count, (uint32_t)__popcll(qm));
+            base = __shfl(base, leader);
+            if (q) {
+                const uint32_t slot = base + (uint32_t)__popcll(qm & lanemask_lt());
+                W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
+                W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, INFINITY);  // .w: t bound
+                W.far_keys[slot] = ao_brute ? RT_KEY_BRUTE : dir_key(d);
+                W.far_vals[slot] = slot;
+            }
+        }
+    }
+    if ((N & 63u) == 0) {
+        const uint64_t m = __ballot(active && hit);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.occ[c], (uint32_t)__popcll(m));
+    } else if (active && hit) {
+        atomicAdd(&W.occ[c], 1u);
+    }
+}
+
 // CalculateAmbientOcclusion (Raytracer.cpp:315-330) + RandomInHemisphere (:283-292)
 // + RandomUnitVector (:269-281): one lane per (call, sample).
 // VARIANT bits (A/B switches, results identical): 1 = sincos table in LDS,
@@ -1019,40 +1054,29 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                 }
             }
         }
+        if (VARIANT & 16384) {
+            // generation only: the ray record for ao_trace_kernel (flag 0: no ray,
+            // 1: near query, 2: far origin)
+            if (item < items) {
+                const uint32_t flag = active ? (ao_brute ? 2u : 1u) : 0u;
+                float4* r = W.ao_rays + 2 * (size_t)(item - item_begin);
+                r[0] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
+                r[1] = make_float4(d.x, d.y, d.z, __uint_as_float(flag));
+            }
+            continue;
+        }
         const bool hit =
 #ifdef RT580_DIAGNOSTICS
                          (VARIANT & 32) ? (d.x > 2.0f) :  // DIAGNOSTIC build only (wrong output)
 #endif
                          (VARIANT & 8192) ? bvh_any_near_wave(S.bv, active && !ao_brute, o, d, ao_wstk[threadIdx.x >> 6])
-                       : (VARIANT & 512) ? (active && !ao_brute && bvh_any(S.bv, o, d, /*with_far=*/false))
+#ifdef RT580_DIAG_NO_NEAR
+                       : (VARIANT & 512) ? (active && !ao_brute)  // DIAGNOSTIC build only: every AO ray occluded, no traversal
+#endif
+                       : (VARIANT & 512) ? (active && !ao_brute && bvh_any_near(S.bv, o, d))
                        : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
                                        : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
-        if (VARIANT & 512) {
-            // rays that miss every near triangle go to the sorted far-hit pass
-            const bool q = active && !hit && S.bv.has_far;
-            const uint64_t qm = __ballot(q);
-            const uint64_t bm = __ballot(ao_brute);
-            if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
-            if (qm) {
-                const int leader = __ffsll((unsigned long long)qm) - 1;
-                uint32_t base = 0;
-                if ((threadIdx.x & 63) == leader) base = atomicAdd(W.far_count, (uint32_t)__popcll(qm));
-                base = __shfl(base, leader);
-                if (q) {
-                    const uint32_t slot = base + (uint32_t)__popcll(qm & lanemask_lt());
-                    W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
-                    W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, INFINITY);  // .w: t bound
-                    W.far_keys[slot] = ao_brute ? RT_KEY_BRUTE : dir_key(d);
-                    W.far_vals[slot] = slot;
-                }
-            }
-        }
-        if ((N & 63u) == 0) {
-            const uint64_t m = __ballot(active && hit);
-            if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.occ[c], (uint32_t)__popcll(m));
-        } else if (active && hit) {
-            atomicAdd(&W.occ[c], 1u);
-        }
+        ao_finish<(VARIANT & 512) != 0>(S, W, N, active, ao_brute, hit, c, o, d);
     }
 }
 
@@ -1087,7 +1111,7 @@ __device__ void ao_fix_item(const DevScene& S, const DevFrame& F, const DevWork&
     bool hit = false;
     if (S.use_bvh) {
         const bool brute = S.bv.has_far && far_origin(S, o);
-        hit = !brute && bvh_any(S.bv, o, d, /*with_far=*/!S.bv.has_far);
+        hit = !brute && bvh_any_near(S.bv, o, d);
         if (!hit && S.bv.has_far) {
             if (brute) atomicAdd(W.far_count + 1, 1u);
             const uint32_t slot = atomicAdd(W.far_count, 1u);
@@ -1145,6 +1169,37 @@ ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
     ao_body<V>(S, F, W, b, e);
 }
 
+// Split AO pass (default for BVH scenes): ao_near_kernel_w<.., V | 16384>
+// writes each item's ray (W.ao_rays), this kernel runs the near any-hit query
+// over the 4-wide tree with nothing else live, then ao_finish. Rays
+// [0, e - b) of the chunk whose first item is b.
+template <int WPE>
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
+ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
+    for (uint64_t b0 = (uint64_t)blockIdx.x * TB; b0 < n; b0 += (uint64_t)gridDim.x * TB) {
+        const uint64_t i = b0 + threadIdx.x;
+        float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
+        if (i < n) {
+            r0 = W.ao_rays[2 * i];
+            r1 = W.ao_rays[2 * i + 1];
+        }
+        const uint32_t flag = __float_as_uint(r1.w);
+        const bool active = flag != 0u, ao_brute = flag == 2u;
+        const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
+        const bool hit = flag == 1u && bvh4_any_near(S.bv, o, d);
+        ao_finish<true>(S, W, N, active, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o, d);
+    }
+}
+
+static int ao_split() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_SPLIT");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
+}
+
 // RT580_NEAR_WAVE=1 (A/B): the wave-cooperative near traversal
 // (bvh_any_near_wave, VARIANT 8192) for AO and shadow rays instead of the
 // per-lane bvh_any. Measured on 100k 1080p: AO 139 ms vs 85 ms per lane (the
@@ -1157,6 +1212,15 @@ static bool near_wave() {
         v = e ? atoi(e) : 0;
     }
     return v != 0;
+}
+
+static int trace_wpe() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_TRACE_WPE");
+        v = e ? atoi(e) : 6;  // cornell10k AO: 8 (spills) 117 ms, 6: 97 ms, 4: 102 ms
+    }
+    return v;
 }
 
 static int near_wpe() {
@@ -2090,12 +2154,35 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return e;
         const uint64_t items = calls * (uint64_t)F.ao_samples;
-        const uint64_t chunk = S.bv.has_far ? (uint64_t)W.far_cap : items;
+        const bool split = ao_split() != 0 && W.ao_rays && S.bv.nodes4 && !near_wave();
+        uint64_t chunk = S.bv.has_far ? (uint64_t)W.far_cap : items;
+        if (split && chunk > (uint64_t)W.ao_cap) chunk = W.ao_cap;
         for (uint64_t b = 0; b < items; b += chunk) {
             const uint64_t e1 = b + chunk < items ? b + chunk : items;
             if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(W.aofix_count, 0, 4, s)) != hipSuccess) return e;
             const int wpe = near_wpe();
+            if (split) {
+                constexpr int V = 512 | 1024 | 2048 | 4096 | 16384;
+                if (wpe == 5)
+                    hipLaunchKernelGGL((ao_near_kernel_w<5, V>), dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+                else if (wpe == 6)
+                    hipLaunchKernelGGL((ao_near_kernel_w<6, V>), dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+                else
+                    hipLaunchKernelGGL((ao_near_kernel_w<8, V>), dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                kt_begin(s);
+                const int twpe = trace_wpe();
+                if (twpe == 4)
+                    hipLaunchKernelGGL(ao_trace_kernel<4>, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
+                                       (uint32_t)F.ao_samples, e1 - b);
+                else if (twpe == 8)
+                    hipLaunchKernelGGL(ao_trace_kernel<8>, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
+                                       (uint32_t)F.ao_samples, e1 - b);
+                else
+                    hipLaunchKernelGGL(ao_trace_kernel<6>, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
+                                       (uint32_t)F.ao_samples, e1 - b);
+            } else {
             kt_begin(s);
             if (near_wave())
                 hipLaunchKernelGGL((ao_near_kernel_w<8, 512 | 1024 | 2048 | 4096 | 8192>), dim3(grid_for(e1 - b, 8192)),
@@ -2108,6 +2195,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 hipLaunchKernelGGL(ao_near_kernel_w<8>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
             else
                 hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+            }
             kt_end(s, e1 - b);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             // exact recompute of the fast pass's failing samples; their misses join the far queue

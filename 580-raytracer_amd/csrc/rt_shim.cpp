@@ -58,7 +58,7 @@ struct State {
     std::vector<int> shadow_lights;  // scene indices of the directional and point lights
     bool have_scene = false;
     // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
-    DevBuf bvh_nodes, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always, scan_prims;
+    DevBuf bvh_nodes, bvh_nodes4, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always, scan_prims;
     BvhBuild bvh;
     bool bvh_ok = false;
     int grid_log2 = 0, grid_n_always = 0;  // far-search direction grid (uploaded; host copy dropped)
@@ -74,9 +74,11 @@ struct State {
     hipEvent_t user_mark[2] = {nullptr, nullptr};  // the caller's stream at the start of a frame call
     bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
     // BVH far-queue buffers (BVH frames always run serialized on slot 0)
+    DevBuf ao_rays;
     DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim, shadow;
     uint32_t* far_count_host = nullptr;  // pinned
     uint32_t far_cap = 0;
+    uint32_t ao_cap = 0;
     uint32_t node_cap = 0, call_cap = 0;
     double node_factor = 4.0;         // node capacity per pixel (grown on overflow)
     uint32_t* needed_host = nullptr;  // pinned
@@ -253,6 +255,7 @@ DevScene dev_scene(const rt_render_params* p) {
     BvhView& v = s.bv;
     v.all = s.prims;
     v.nodes = (const BvhNode*)g.bvh_nodes.p;
+    v.nodes4 = g.bvh.nodes4.empty() ? nullptr : (const Bvh4Node*)g.bvh_nodes4.p;
     v.prims = (const rt_prim*)g.bvh_prims.p;
     v.ids = (const uint32_t*)g.bvh_ids.p;
     v.far_nodes = (const FarNode*)g.far_nodes.p;
@@ -342,6 +345,8 @@ DevWork dev_work() {
     w.sort_tmp = g.sort_tmp.p;
     w.sort_tmp_bytes = g.sort_tmp.bytes;
     w.far_cap = g.far_cap;
+    w.ao_rays = g.ao_cap ? (float4*)g.ao_rays.p : nullptr;
+    w.ao_cap = g.ao_cap;
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
     w.hit4 = split ? (float4*)g.hit4.p : nullptr;
     w.hit_prim = split ? (int32_t*)g.hit_prim.p : nullptr;
@@ -402,6 +407,12 @@ int ensure_work(const rt_render_params* p, int n_rows) {
             ensure(g.sort_tmp, far_sort_tmp_bytes(fc) + 256))
             return RT_FAILURE;
         g.far_cap = fc;
+    }
+    // ray records of the split AO pass (ao_trace_kernel), one chunk
+    if (g.bvh_ok && g.ao_cap == 0) {
+        const uint32_t ac = 1u << 26;
+        if (ensure(g.ao_rays, (size_t)ac * 32)) return RT_FAILURE;
+        g.ao_cap = ac;
     }
     if (g.bvh_ok && !g.bvh.far_nodes.empty() &&
         (ensure(g.hit4, (size_t)cap * 16) || ensure(g.hit_prim, (size_t)cap * 4)))
@@ -597,7 +608,10 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         int glog2 = 10;
         if (const char* e = std::getenv("RT580_GRID_LOG2")) glog2 = std::atoi(e);
         if (g.bvh_ok && glog2 > 0 && glog2 <= 12) build_dir_grid(s->prims, g.bvh, glog2);
-        if (g.bvh_ok && (upload_vec(g.bvh_nodes, g.bvh.nodes) || upload_vec(g.bvh_prims, g.bvh.prims) ||
+        // the 4-wide form for the any-hit queries (AO, shadows); RT580_BVH4=0: binary only
+        const char* b4 = std::getenv("RT580_BVH4");
+        if (g.bvh_ok && !(b4 && std::atoi(b4) == 0)) collapse_bvh4(g.bvh);
+        if (g.bvh_ok && (upload_vec(g.bvh_nodes, g.bvh.nodes) || upload_vec(g.bvh_nodes4, g.bvh.nodes4) || upload_vec(g.bvh_prims, g.bvh.prims) ||
                          upload_vec(g.bvh_ids, g.bvh.ids) || upload_vec(g.far_nodes, g.bvh.far_nodes) ||
                          upload_vec(g.far_tris, g.bvh.far_tris) || upload_vec(g.brute, g.bvh.brute) ||
                          upload_vec(g.grid_start, g.bvh.grid_start) || upload_vec(g.grid_items, g.bvh.grid_items) ||
@@ -866,8 +880,8 @@ void shutdown_ctx() {
     (void)sync_all();
     for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always})
         release(*b);
-    for (DevBuf* b : {&g.bvh_nodes, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
-                      &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
+    for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
+                      &g.ao_rays, &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
                       &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.shadow})
         release(*b);
     for (Slot& sl : g.slot) {

@@ -116,11 +116,13 @@ def _preload_torch_hip_runtime():
         ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
 
 
-def load(path=LIB_PATH):
-    """Load lib580rt.so (built by `make -C 580-raytracer_amd`); raise if absent."""
+def load(path=None):
+    """Load lib580rt.so (built by `make -C 580-raytracer_amd`); raise if absent.
+    $RT580_LIB selects another build (the diagnostic timing library, A/B only)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("RT580_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError("lib580rt.so not built (%s); run __graft_entry__.build()" % path)
     _preload_torch_hip_runtime()

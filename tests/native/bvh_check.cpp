@@ -77,9 +77,12 @@ int main(int argc, char** argv) {
         std::printf("mismatches=0 (no BVH for this scene)\n");
         return 0;
     }
+    collapse_bvh4(B);
+    std::printf("bvh4 nodes=%zu\n", B.nodes4.size());
     BvhView V;
     V.all = P.data();
     V.nodes = B.nodes.data();
+    V.nodes4 = B.nodes4.empty() ? nullptr : B.nodes4.data();
     V.prims = B.prims.data();
     V.ids = B.ids.data();
     V.far_nodes = B.far_nodes.empty() ? nullptr : B.far_nodes.data();
@@ -110,9 +113,9 @@ int main(int argc, char** argv) {
         if (P[j].kind == RT_PRIM_TRIANGLE) tris.push_back(j);
     BvhView Vnear = V;  // control: without the far search some results must differ
     Vnear.has_far = 0;
-    std::atomic<long> bad{0}, hits{0}, anyhits{0}, far_closest{0}, near_only_bad{0}, point_checks{0};
+    std::atomic<long> bad{0}, hits{0}, anyhits{0}, far_closest{0}, near_only_bad{0}, point_checks{0}, bad4{0};
 #ifdef RT_BVH_COUNT
-    std::atomic<long> cnt[2][6] = {};  // [closest, any][counter]
+    std::atomic<long> cnt[3][6] = {};  // [closest, any, any 4-wide near][counter]
 #endif
     const int NT = 8;
     std::vector<std::thread> th;
@@ -179,6 +182,23 @@ int main(int argc, char** argv) {
                         point_checks++;
                     }
                 }
+                // the 4-wide near query answers exactly as the binary one (with and without a t bound)
+                if (V.nodes4) {
+#ifdef RT_BVH_COUNT
+                    g_bvh_cnt = BvhCounters{};
+#endif
+                    const bool a2 = bvh_any(V, o, d, false), a4 = bvh4_any_near(V, o, d);
+#ifdef RT_BVH_COUNT
+                    if (kind == 1 || kind == 2) {
+                        const long* c = &g_bvh_cnt.nodes;
+                        for (int q = 0; q < 6; q++) cnt[2][q] += c[q];
+                    }
+#endif
+                    const float tb = std::ldexp(U(rng), (int)(rng() % 6));
+                    if (a2 != a4 || bvh_any(V, o, d, false, tb) != bvh4_any_near(V, o, d, tb)) {
+                        if (bad4.fetch_add(1) < 10) std::printf("MISMATCH4 ray %ld kind %d: binary %d 4-wide %d\n", r, kind, a2, a4);
+                    }
+                }
                 bool same = cb == cv && ab == av && point_ok;
                 if (same && cb)
                     same = hb.prim == hv.prim && fbits(hb.t) == fbits(hv.t) && fbits(hb.a) == fbits(hv.a) &&
@@ -204,15 +224,16 @@ int main(int argc, char** argv) {
     for (auto& t : th) t.join();
 #ifdef RT_BVH_COUNT
     const char* names[6] = {"nodes", "leaf_tris", "far_nodes", "far_cands", "far_tests", "brute_tests"};
-    for (int w = 0; w < 2; w++) {
-        std::printf("%s per ray:", w ? "any-hit (AO-style rays)" : "closest (all rays)");
+    for (int w = 0; w < 3; w++) {
+        std::printf("%s per ray:", w == 2 ? "any-hit near 4-wide (AO-style rays)"
+                                          : (w ? "any-hit (AO-style rays)" : "closest (all rays)"));
         const double div = w ? nrays / 2.0 : (double)nrays;
         for (int q = 0; q < 6; q++) std::printf(" %s=%.1f", names[q], cnt[w][q] / div);
         std::printf("\n");
     }
 #endif
     std::printf("rays=%ld closest_hits=%ld any_hits=%ld far_closest_hits=%ld differ_without_far_search=%ld "
-                "point_shadow_checks=%ld mismatches=%ld\n", nrays, (long)hits, (long)anyhits, (long)far_closest,
-                (long)near_only_bad, (long)point_checks, (long)bad);
-    return bad ? 1 : 0;
+                "point_shadow_checks=%ld mismatches=%ld bvh4_mismatches=%ld\n", nrays, (long)hits, (long)anyhits, (long)far_closest,
+                (long)near_only_bad, (long)point_checks, (long)bad, (long)bad4);
+    return (bad || bad4) ? 1 : 0;
 }

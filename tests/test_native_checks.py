@@ -73,7 +73,9 @@ def test_bvh_queries_equal_brute_force(scene, rays, far):
     brute-force IntersectScene loop on camera, AO, reflection and grazing rays:
     same primitive, bit-identical t and barycentrics, same any-hit boolean. The
     grazing rays provoke the reference's far "hits" (rt_bvh.h), which only the
-    plane-tree search finds: the control count without it must be non-zero."""
+    plane-tree search finds: the control count without it must be non-zero.
+    The 4-wide collapse of the tree (the AO / shadow any-hit traversal) answers
+    every near any-hit query, with and without a t bound, as the binary one."""
     root = helpers.synthetic_root(scene)
     exe = _build("bvh_check", [os.path.join(CSRC, "rt_scene.cpp"), os.path.join(CSRC, "rt_bvh.cpp")])
     env = dict(os.environ, RT_FAR_TREE="1" if far == "tree" else "0")
@@ -81,5 +83,6 @@ def test_bvh_queries_equal_brute_force(scene, rays, far):
     assert p.returncode == 0 and "mismatches=0" in p.stdout, p.stdout + p.stderr
     out = p.stdout
     assert ("grid log2=10" in out) == (far == "grid"), out
+    assert "bvh4 nodes=0\n" not in out and "bvh4_mismatches=0" in out, out  # the 4-wide any-hit tree
     if scene == "cornell10k":
         assert "differ_without_far_search=0 " not in out, out
