@@ -179,11 +179,14 @@ RTM_HD bool lex_better(float t, int id, bool found, const Hit& h) {
 // with c_lo = d + beta, c_hi = d - beta. Raising c_lo or lowering c_hi only
 // weakens a constraint at t >= 0, so for |d| <= beta (where c_lo, c_hi may be
 // 0) c_lo = max(d + beta, beta), c_hi = min(d - beta, -beta): every reciprocal
-// is finite. Each bound is one FMA, lo * (1/c_lo) - (o + alpha) / c_lo; the
-// rounding of the hoisted product (o + alpha) / c_lo and of o + alpha moves
-// the plane by at most 2u (|o| + alpha), which alpha = 40u (|o| + S) covers
-// on top of the 32u the bound itself needs. The culling is then conservative
-// for every t >= 0, with no bound on the ray length.
+// is finite. (Axis-parallel rays are common -- the shadow rays of an
+// axis-aligned directional light -- so such an axis keeps its one-sided
+// bounds rather than going untested.) Each bound is one FMA,
+// lo * (1/c_lo) - (o + alpha) / c_lo; the rounding of the hoisted product
+// (o + alpha) / c_lo and of o + alpha moves the plane by at most
+// 2u (|o| + alpha), which alpha = 40u (|o| + S) covers on top of the 32u the
+// bound itself needs. The culling is then conservative for every t >= 0, with
+// no bound on the ray length.
 //   Per axis the two plane distances t1 (lo), t2 (hi) give, for d > beta, the
 // interval [t1, t2]; for d < -beta [t2, t1]; for |d| <= beta [max(t1, t2),
 // inf). With k = -inf (|d| > beta) or +inf (|d| <= beta): low =
@@ -191,9 +194,9 @@ RTM_HD bool lex_better(float t, int id, bool found, const Hit& h) {
 // can only widen an interval whose planes are both behind the origin, which
 // the high >= 0 test rejects anyway.
 struct SlabRay {
-    float ip[3], im[3];  // 1 / c_lo, 1 / c_hi
+    float ip[3], im[3];    // 1 / c_lo, 1 / c_hi
     float nol[3], noh[3];  // -(o + alpha) / c_lo, -(o - alpha) / c_hi
-    float k[3];          // -inf, or +inf for |d| <= beta
+    float k[3];            // -inf, or +inf for |d| <= beta
 };
 
 RTM_HD float rt_med3(float a, float b, float c) {
@@ -533,64 +536,122 @@ RTM_HD void load_prim(const rt_prim* p, rt_prim& out) {
 // tests; only the grouping differs, so the same boolean). Per node: the fat
 // slab test of its up to four children (branch-free), the nearest accepted
 // child entered, the other accepted ones stacked. While-while loop: a lane
-// descends inner nodes until it holds a leaf, then tests the leaf.
+// descends inner nodes until it holds a leaf (bvh4_descend), then tests the
+// leaf (bvh4_leaf_hit), then resumes from the stack (bvh4_pop).
+// Stack entries: n << 27 | c (BvhNode's child link); RT_BVH_STACK + 4 slots
+// (collapse_bvh4 bounds the depth; the branch-free push writes one past).
+// The stack as a plain per-lane array ...
+struct ArrStack {
+    uint32_t* a;
+    RTM_HDM void put(int i, uint32_t v) const { a[i] = v; }
+    RTM_HDM uint32_t get(int i) const { return a[i]; }
+};
+// ... or (device) its first D entries in LDS, one column per lane (stride
+// TB: lanes hit consecutive banks), the rest in a per-lane array.
+template <int D, int STRIDE>
+struct LdsStack {
+    uint32_t* l;  // &lds[0][lane]
+    uint32_t* a;  // entries D..
+    RTM_HDM void put(int i, uint32_t v) const {
+        if (i < D) l[i * STRIDE] = v;
+        else a[i - D] = v;
+    }
+    RTM_HDM uint32_t get(int i) const { return i < D ? l[i * STRIDE] : a[i - D]; }
+};
+
+template <class STK>
+RTM_HD bool bvh4_pop(const STK& stk, int& sp, int32_t& c, int32_t& n) {
+    if (sp == 0) return false;
+    sp--;
+    const uint32_t e = stk.get(sp);
+    c = (int32_t)(e & 0x7ffffffu);
+    n = (int32_t)(e >> 27);
+    return true;
+}
+
+// From (c, n) down to a leaf (n > 0): false when the subtree and the stack hold none.
+template <class STK>
+RTM_HD bool bvh4_descend(const BvhView& V, const SlabRay& sr, float tmax, const STK& stk, int& sp, int32_t& c,
+                         int32_t& n) {
+    while (n == 0) {
+        RT_CNT(nodes, 1);
+        Bvh4Node nd;
+        load_node4(V.nodes4 + c, nd);
+        float t[4];
+        bool ok[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const float lo[3] = {nd.lo[0][j], nd.lo[1][j], nd.lo[2][j]};
+            const float hi[3] = {nd.hi[0][j], nd.hi[1][j], nd.hi[2][j]};
+            const bool in = slab(lo, hi, sr, t[j]);
+            ok[j] = (nd.n[j] >= 0) & in & !(t[j] > tmax);
+        }
+        int best = -1;
+        float bt = INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (ok[j] & ((best < 0) | (t[j] < bt))) {
+                best = j;
+                bt = t[j];
+            }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            stk.put(sp, ((uint32_t)nd.n[j] << 27) | (uint32_t)nd.c[j]);
+            sp += (ok[j] & (j != best)) ? 1 : 0;
+        }
+        if (best >= 0) {
+            c = best == 0 ? nd.c[0] : best == 1 ? nd.c[1] : best == 2 ? nd.c[2] : nd.c[3];
+            n = best == 0 ? nd.n[0] : best == 1 ? nd.n[1] : best == 2 ? nd.n[2] : nd.n[3];
+        } else if (!bvh4_pop(stk, sp, c, n)) {
+            return false;
+        }
+    }
+    return true;
+}
+
+// Any primitive of leaf slots [c, c + n) hit with !(t > tmax)?
+RTM_HD bool bvh4_leaf_hit(const BvhView& V, rv3 o, rv3 d, float tmax, int32_t c, int32_t n) {
+    RT_CNT(leaf_tris, n);
+    for (int k = c; k < c + n; k++) {
+        rt_prim P;
+        load_prim(V.prims + k, P);
+        float tt, a, b, g;
+        if (tri_test<false, true>(P, o, d, tt, a, b, g) && !(tt > tmax)) return true;
+    }
+    return false;
+}
+
+// bvh4_any_near with a caller-provided stack
+template <class STK>
+RTM_HD bool bvh4_any_near_s(const BvhView& V, rv3 o, rv3 d, const STK& stk, float tmax = INFINITY) {
+    RT_CNT(brute_tests, V.n_brute);
+    for (int k = 0; k < V.n_brute; k++)
+        if (prim_hit_within(V.all[V.brute[k]], o, d, tmax)) return true;
+    if (!V.has_tree || dir_zero(d)) return false;
+    const SlabRay sr = slab_ray(V, o, d);
+    int sp = 0;
+    int32_t c = 0, n = 0;  // root (internal)
+    for (;;) {
+        if (!bvh4_descend(V, sr, tmax, stk, sp, c, n)) return false;
+        if (bvh4_leaf_hit(V, o, d, tmax, c, n)) return true;
+        if (!bvh4_pop(stk, sp, c, n)) return false;
+    }
+}
+
 RTM_HD bool bvh4_any_near(const BvhView& V, rv3 o, rv3 d, float tmax = INFINITY) {
     RT_CNT(brute_tests, V.n_brute);
     for (int k = 0; k < V.n_brute; k++)
         if (prim_hit_within(V.all[V.brute[k]], o, d, tmax)) return true;
     if (!V.has_tree || dir_zero(d)) return false;
     const SlabRay sr = slab_ray(V, o, d);
-    uint32_t stk[RT_BVH_STACK + 4];
+    uint32_t stk_a[RT_BVH_STACK + 4];
+    const ArrStack stk{stk_a};
     int sp = 0;
     int32_t c = 0, n = 0;  // root (internal)
     for (;;) {
-        while (n == 0) {
-            RT_CNT(nodes, 1);
-            Bvh4Node nd;
-            load_node4(V.nodes4 + c, nd);
-            float t[4];
-            bool ok[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float lo[3] = {nd.lo[0][j], nd.lo[1][j], nd.lo[2][j]};
-                const float hi[3] = {nd.hi[0][j], nd.hi[1][j], nd.hi[2][j]};
-                const bool in = slab(lo, hi, sr, t[j]);
-                ok[j] = (nd.n[j] >= 0) & in & !(t[j] > tmax);
-            }
-            int best = -1;
-            float bt = INFINITY;
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                if (ok[j] & ((best < 0) | (t[j] < bt))) {
-                    best = j;
-                    bt = t[j];
-                }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                stk[sp] = ((uint32_t)nd.n[j] << 27) | (uint32_t)nd.c[j];
-                sp += (ok[j] & (j != best)) ? 1 : 0;
-            }
-            if (best >= 0) {
-                c = best == 0 ? nd.c[0] : best == 1 ? nd.c[1] : best == 2 ? nd.c[2] : nd.c[3];
-                n = best == 0 ? nd.n[0] : best == 1 ? nd.n[1] : best == 2 ? nd.n[2] : nd.n[3];
-            } else {
-                if (sp == 0) return false;
-                sp--;
-                c = (int32_t)(stk[sp] & 0x7ffffffu);
-                n = (int32_t)(stk[sp] >> 27);
-            }
-        }
-        RT_CNT(leaf_tris, n);
-        for (int k = c; k < c + n; k++) {
-            rt_prim P;
-            load_prim(V.prims + k, P);
-            float tt, a, b, g;
-            if (tri_test<false, true>(P, o, d, tt, a, b, g) && !(tt > tmax)) return true;
-        }
-        if (sp == 0) return false;
-        sp--;
-        c = (int32_t)(stk[sp] & 0x7ffffffu);
-        n = (int32_t)(stk[sp] >> 27);
+        if (!bvh4_descend(V, sr, tmax, stk, sp, c, n)) return false;
+        if (bvh4_leaf_hit(V, o, d, tmax, c, n)) return true;
+        if (!bvh4_pop(stk, sp, c, n)) return false;
     }
 }
 

@@ -1173,9 +1173,11 @@ ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
 // writes each item's ray (W.ao_rays), this kernel runs the near any-hit query
 // over the 4-wide tree with nothing else live, then ao_finish. Rays
 // [0, e - b) of the chunk whose first item is b.
-template <int WPE>
+// LDS_D > 0: the first LDS_D traversal-stack entries of each lane live in LDS.
+template <int WPE, int LDS_D = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
+    __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
     for (uint64_t b0 = (uint64_t)blockIdx.x * TB; b0 < n; b0 += (uint64_t)gridDim.x * TB) {
         const uint64_t i = b0 + threadIdx.x;
         float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
@@ -1186,10 +1188,24 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
         const uint32_t flag = __float_as_uint(r1.w);
         const bool active = flag != 0u, ao_brute = flag == 2u;
         const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
-        const bool hit = flag == 1u && bvh4_any_near(S.bv, o, d);
+        bool hit;
+        if (LDS_D > 0) {
+            uint32_t stk_a[RT_BVH_STACK + 4 - (LDS_D > 0 ? LDS_D : 0)];
+            const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
+            hit = flag == 1u && bvh4_any_near_s(S.bv, o, d, stk);
+        } else {
+            hit = flag == 1u && bvh4_any_near(S.bv, o, d);
+        }
         ao_finish<true>(S, W, N, active, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o, d);
     }
 }
+
+// (Persistent forms of ao_trace_kernel -- lanes refilled from the chunk as
+// they finish, per-iteration atomic fetch, static per-wave ranges, or batched
+// fetch with prefetched records -- measured 94 / 137 / 133 ms against 89 ms
+// for this kernel on cornell10k's AO; the SIMD-efficiency model
+// tools/simd_sim.cpp predicts fewer lock-step iterations for them, but their
+// extra live state spills. Not kept.)
 
 static int ao_split() {
     static int v = -1;
@@ -1212,6 +1228,18 @@ static bool near_wave() {
         v = e ? atoi(e) : 0;
     }
     return v != 0;
+}
+
+// The first 16 traversal-stack entries of ao_trace_kernel in LDS
+// (RT580_TRACE_LDS=0: all in scratch). cornell10k AO 91.7 -> 84.9 ms,
+// field100k 1080p 72.7 -> 67.8 ms.
+static int trace_lds() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_TRACE_LDS");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
 }
 
 static int trace_wpe() {
@@ -2173,7 +2201,10 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 kt_begin(s);
                 const int twpe = trace_wpe();
-                if (twpe == 4)
+                if (twpe == 6 && trace_lds())  // 16-entry LDS stacks (default)
+                    hipLaunchKernelGGL((ao_trace_kernel<6, 16>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
+                                       (uint32_t)F.ao_samples, e1 - b);
+                else if (twpe == 4)
                     hipLaunchKernelGGL(ao_trace_kernel<4>, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
                 else if (twpe == 8)

@@ -11,8 +11,10 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define RTM_HD __host__ __device__ __forceinline__
+#define RTM_HDM __host__ __device__ __forceinline__  // member functions
 #else
 #define RTM_HD static inline
+#define RTM_HDM inline
 #endif
 
 struct rv3 {

@@ -5,7 +5,7 @@ directory, for bench.py's roofline block.
 Reads the kernel stats + PMC passes (summarize_profile.summarize) and the bench
 JSON line of the trace pass (trace.log: AO rays per launch, measured live in
 that run), and writes profiles/r02/roofline_<workload>.json:
-  kernel, avg_ms               the AO ray kernel (ao_kernel* / ao_near_kernel*)
+  kernel, avg_ms               the AO ray kernel (ao_kernel* / ao_near_kernel* / ao_trace_kernel*)
   valu_per_ao_ray              SQ_INSTS_VALU per dispatch / AO rays per dispatch
   hbm_bytes_per_ao_ray         (FETCH_SIZE + WRITE_SIZE) x 1 KiB per dispatch / AO rays
   valu_issue_frac              SQ_INSTS_VALU / (avg duration x VALU issue peak)
@@ -36,7 +36,7 @@ def main():
     b = bench_line(os.path.join(d, "trace.log"))
     rays_launch = b["roofline"]["ao_rays_per_launch"]
     ks = summ["kernels"]
-    name = max((k for k in ks if k.startswith(("ao_kernel", "ao_near_kernel"))), key=lambda k: ks[k]["total_ns"])
+    name = max((k for k in ks if k.startswith(("ao_kernel", "ao_near_kernel", "ao_trace_kernel"))), key=lambda k: ks[k]["total_ns"])
     k = ks[name]
     c = k["counters"]
     total = sum(v["total_ns"] for v in ks.values())
