@@ -655,6 +655,105 @@ RTM_HD bool bvh4_any_near(const BvhView& V, rv3 o, rv3 d, float tmax = INFINITY)
     }
 }
 
+// bvh_closest's near part (with_far = false) over the 4-wide tree: the same
+// lexicographic minimum of (t, primitive index) -- a box is skipped only when
+// its entry t is above the best t, and a primitive hit at the best t with a
+// lower index lies in a box entered at or before that t. Stack entries carry
+// their entry t for that pruning at pop time.
+RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
+    bool found = false;
+    h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
+    RT_CNT(brute_tests, V.n_brute);
+    for (int k = 0; k < V.n_brute; k++) {
+        const int j = (int)V.brute[k];
+        float t, a, b, g;
+        if (prim_test_closest(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
+            found = true;
+            h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
+        }
+    }
+    if (!V.has_tree || dir_zero(d)) return found;
+    const SlabRay sr = slab_ray(V, o, d);
+    uint32_t stk[RT_BVH_STACK + 4];
+    float tstk[RT_BVH_STACK + 4];
+    int sp = 0;
+    int32_t c = 0, n = 0;  // root (internal)
+    for (;;) {
+        bool have = true;
+        while (n == 0) {
+            RT_CNT(nodes, 1);
+            Bvh4Node nd;
+            load_node4(V.nodes4 + c, nd);
+            float t[4];
+            bool ok[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float lo[3] = {nd.lo[0][j], nd.lo[1][j], nd.lo[2][j]};
+                const float hi[3] = {nd.hi[0][j], nd.hi[1][j], nd.hi[2][j]};
+                const bool in = slab(lo, hi, sr, t[j]);
+                ok[j] = (nd.n[j] >= 0) & in & (!found || t[j] <= h.t);
+            }
+            int best = -1;
+            float bt = INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (ok[j] & ((best < 0) | (t[j] < bt))) {
+                    best = j;
+                    bt = t[j];
+                }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                stk[sp] = ((uint32_t)nd.n[j] << 27) | (uint32_t)nd.c[j];
+                tstk[sp] = t[j];
+                sp += (ok[j] & (j != best)) ? 1 : 0;
+            }
+            if (best >= 0) {
+                c = best == 0 ? nd.c[0] : best == 1 ? nd.c[1] : best == 2 ? nd.c[2] : nd.c[3];
+                n = best == 0 ? nd.n[0] : best == 1 ? nd.n[1] : best == 2 ? nd.n[2] : nd.n[3];
+                continue;
+            }
+            have = false;
+            while (sp > 0) {
+                sp--;
+                if (found && tstk[sp] > h.t) continue;
+                c = (int32_t)(stk[sp] & 0x7ffffffu);
+                n = (int32_t)(stk[sp] >> 27);
+                have = true;
+                break;
+            }
+            if (!have) return found;
+        }
+        RT_CNT(leaf_tris, n);
+        for (int k = c; k < c + n; k++) {
+            rt_prim P;
+            load_prim(V.prims + k, P);
+            float t, a, b, g;
+            if (tri_test<true, true>(P, o, d, t, a, b, g)) {
+                const int id = (int)V.ids[k];
+                if (lex_better(t, id, found, h)) {
+                    found = true;
+                    h.t = t; h.a = a; h.b = b; h.g = g; h.prim = id;
+                }
+            }
+        }
+        have = false;
+        while (sp > 0) {
+            sp--;
+            if (found && tstk[sp] > h.t) continue;
+            c = (int32_t)(stk[sp] & 0x7ffffffu);
+            n = (int32_t)(stk[sp] >> 27);
+            have = true;
+            break;
+        }
+        if (!have) return found;
+    }
+}
+
+// The near closest-hit query: 4-wide tree when present, else the binary one.
+RTM_HD bool bvh_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
+    return V.nodes4 ? bvh4_closest_near(V, o, d, h) : bvh_closest(V, o, d, h, /*with_far=*/false);
+}
+
 // The near any-hit query: 4-wide tree when present, else the binary one.
 RTM_HD bool bvh_any_near(const BvhView& V, rv3 o, rv3 d, float tmax = INFINITY) {
     return V.nodes4 ? bvh4_any_near(V, o, d, tmax) : bvh_any(V, o, d, /*with_far=*/false, tmax);

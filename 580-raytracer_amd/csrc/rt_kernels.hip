@@ -555,7 +555,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
         if (PHASE == 1) {
             const FarNode root = load_far_node(S.bv.far_nodes, 0);
             const bool brute = active && far_origin(S, o);
-            const bool nh = active && !brute && bvh_closest(S.bv, o, d, h, /*with_far=*/false);
+            const bool nh = active && !brute && bvh_closest_near(S.bv, o, d, h);
             bool q = false;
             if (active) {
                 W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);

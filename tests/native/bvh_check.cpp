@@ -198,6 +198,14 @@ int main(int argc, char** argv) {
                     if (a2 != a4 || bvh_any(V, o, d, false, tb) != bvh4_any_near(V, o, d, tb)) {
                         if (bad4.fetch_add(1) < 10) std::printf("MISMATCH4 ray %ld kind %d: binary %d 4-wide %d\n", r, kind, a2, a4);
                     }
+                    Hit h2, h4;
+                    const bool c2 = bvh_closest(V, o, d, h2, false), c4 = bvh4_closest_near(V, o, d, h4);
+                    if (c2 != c4 || (c2 && (h2.prim != h4.prim || fbits(h2.t) != fbits(h4.t) || fbits(h2.a) != fbits(h4.a) ||
+                                            fbits(h2.b) != fbits(h4.b) || fbits(h2.g) != fbits(h4.g)))) {
+                        if (bad4.fetch_add(1) < 10)
+                            std::printf("MISMATCH4 closest ray %ld kind %d: binary (%d, %d) 4-wide (%d, %d)\n", r, kind, c2,
+                                        c2 ? h2.prim : -1, c4, c4 ? h4.prim : -1);
+                    }
                 }
                 bool same = cb == cv && ab == av && point_ok;
                 if (same && cb)
