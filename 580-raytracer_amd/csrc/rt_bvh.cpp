@@ -14,7 +14,18 @@ namespace rt580 {
 namespace {
 
 constexpr int kBins = 16;
-constexpr int kLeafMax = 4;   // triangles per spatial leaf
+// triangles per spatial leaf (RT580_LEAF_MAX, 1..8, for A/B). 2: a wave's
+// lanes test fewer triangles per leaf step (tools/simd_sim.cpp); AO
+// cornell10k 82.5 -> 80.9 ms, field100k 1080p 61.4 -> 59.1 ms against 4.
+static int leaf_max() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("RT580_LEAF_MAX");
+        v = e ? std::atoi(e) : 2;
+        if (v < 1 || v > 8) v = 2;
+    }
+    return v;
+}
 constexpr int kFarLeaf = 8;   // planes per far-tree leaf
 constexpr int kSahDepth = 40; // below this depth: median splits (bounded stack)
 constexpr double kU = 5.9604644775390625e-08;  // 2^-24
@@ -199,7 +210,7 @@ struct Builder {
 
     void build_child(int b, int e, int depth, int32_t& c, int32_t& n, Box& box) {
         box = bounds(b, e);
-        if (e - b <= kLeafMax) {
+        if (e - b <= leaf_max()) {
             c = leaf(b, e);
             n = e - b;
             return;
@@ -344,7 +355,7 @@ bool build_bvh(const rt_prim* prims, int n, BvhBuild& out) {
         out.prims.reserve(nt);
         out.ids.reserve(nt);
         out.nodes.emplace_back();  // root
-        if (nt <= kLeafMax) {
+        if (nt <= leaf_max()) {
             Box b = B.bounds(0, nt);
             BvhNode& r = out.nodes[0];
             std::memset(&r, 0, sizeof r);
