@@ -95,7 +95,8 @@ int main(int argc, char** argv) {
     V.scale = B.scale;
     // far search: the direction grid (default) or, with RT_FAR_TREE=1, the plane tree only
     const bool use_grid = !(std::getenv("RT_FAR_TREE") && std::atoi(std::getenv("RT_FAR_TREE")) == 1);
-    if (use_grid) build_dir_grid(P.data(), B, 10);
+    const int glog2 = std::getenv("RT_GRID_LOG2") ? std::atoi(std::getenv("RT_GRID_LOG2")) : 10;
+    if (use_grid) build_dir_grid(P.data(), B, glog2);
     V.grid_start = B.grid_start.empty() ? nullptr : B.grid_start.data();
     V.grid_items = B.grid_items.data();
     V.grid_always = B.grid_always.data();
