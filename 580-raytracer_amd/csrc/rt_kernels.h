@@ -114,6 +114,11 @@ struct DevWork {
     // exactly by ao_fix_kernel: item ids, count (may exceed the capacity)
     uint64_t* aofix_items; // [aofix_cap]
     uint32_t* aofix_count; // [1]
+    // brute any-hit scans of far-origin AO rays: per AO call, a record (scan
+    // order) that accepted one of its samples, tried first by its other
+    // samples (they share the origin; tools/far_origin_study.cpp). 0xffffffff:
+    // none yet. [call_cap] or null
+    uint32_t* call_hint;
     uint32_t aofix_cap;
 };
 

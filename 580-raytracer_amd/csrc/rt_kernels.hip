@@ -369,6 +369,14 @@ __device__ __forceinline__ bool far_origin(const DevScene& S, rv3 o) {
     const float oi = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     return oi > 64.0f * S.bv.scale || !(far_T(far_ray(S.bv, o), 0.5f * S.bv.dhi_median) > 0.0f);
 }
+__device__ __forceinline__ uint32_t dir_key(rv3 d);
+// Sort key of a far-pass ray: its direction-grid cell (rays of one cell are
+// then contiguous: waves share a cell list) when the origin uses the grid,
+// else the 4096^2 direction key. Below RT_KEY_BRUTE.
+__device__ __forceinline__ uint32_t far_key(const BvhView& V, rv3 o, rv3 d) {
+    if (grid_origin(V, o)) return grid_cell(d, V.grid_log2) << (24 - 2 * V.grid_log2);
+    return dir_key(d);
+}
 __device__ __forceinline__ uint32_t dir_key(rv3 d) {
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
     float x = d.x / s, y = d.y / s;
@@ -574,7 +582,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                     const uint32_t slot = qb + (uint32_t)__popcll(qm & lanemask_lt());
                     W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float(node));
                     W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, 0.0f);
-                    W.far_keys[slot] = brute ? RT_KEY_BRUTE : dir_key(d);
+                    W.far_keys[slot] = brute ? RT_KEY_BRUTE : far_key(S.bv, o, d);
                     W.far_vals[slot] = slot;
                 }
             }
@@ -633,7 +641,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                     const uint32_t slot = qb + (uint32_t)__popcll(qm & lanemask_lt());
                     W.far_rays[2 * (size_t)slot] = make_float4(so.x, so.y, so.z, __uint_as_float(item - i0));
                     W.far_rays[2 * (size_t)slot + 1] = make_float4(L2.x, L2.y, L2.z, tmax);
-                    W.far_keys[slot] = brute ? RT_KEY_BRUTE : dir_key(L2);
+                    W.far_keys[slot] = brute ? RT_KEY_BRUTE : far_key(S.bv, so, L2);
                     W.far_vals[slot] = slot;
                 }
             }
@@ -920,7 +928,7 @@ __device__ __forceinline__ void ao_finish(const DevScene& S, const DevWork& W, u
                 const uint32_t slot = base + (uint32_t)__popcll(qm & lanemask_lt());
                 W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
                 W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, INFINITY);  // .w: t bound
-                W.far_keys[slot] = ao_brute ? RT_KEY_BRUTE : dir_key(d);
+                W.far_keys[slot] = ao_brute ? RT_KEY_BRUTE : far_key(S.bv, o, d);
                 W.far_vals[slot] = slot;
             }
         }
@@ -1117,7 +1125,7 @@ __device__ void ao_fix_item(const DevScene& S, const DevFrame& F, const DevWork&
             const uint32_t slot = atomicAdd(W.far_count, 1u);
             W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
             W.far_rays[2 * (size_t)slot + 1] = make_float4(d.x, d.y, d.z, INFINITY);
-            W.far_keys[slot] = brute ? RT_KEY_BRUTE : dir_key(d);
+            W.far_keys[slot] = brute ? RT_KEY_BRUTE : far_key(S.bv, o, d);
             W.far_vals[slot] = slot;
             return;
         }
@@ -1263,25 +1271,23 @@ static int near_wpe() {
 // ---------------------------------------------------------------- far-hit pass
 // Direction-grid candidates (rt_bvh.h build_dir_grid) of a lane whose origin is
 // within grid_r: the "always" entries, then its cell's list. When every grid
-// lane of the wave shares one cell, the list is read with wave-uniform scalar
-// loads. Each candidate gets far_candidate + the full reference test.
+// lane of the wave shares one cell (queues are sorted by cell, far_key), the
+// list is read 64 planes at a time: each lane gathers one plane into the
+// wave's LDS tile, then every lane walks the tile by broadcast reads; else
+// each lane walks its own cell's list. (Walking a wave's distinct cells one
+// after the other instead: field1m AO 2.26 -> 5.54 s -- waves hold many.)
+// Each candidate gets far_candidate + the full reference test. Must be called
+// by the whole wave.
 template <bool CLOSEST>
 __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o, rv3 d, const FarRay& fr, Hit& h,
-                                              bool& found) {
+                                              bool& found, FarTri* tile) {
     const BvhView& V = S.bv;
     bool hit = false;
     const uint32_t cell = gl ? grid_cell(d, V.grid_log2) : 0u;
-    const uint64_t glm = __ballot(gl);
-    uint32_t c0 = 0;
-    bool uniform = false;
-    if (glm) {
-        c0 = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)cell, __ffsll((unsigned long long)glm) - 1));
-        uniform = __ballot(gl && cell != c0) == 0;
-    }
-    auto test = [&](const FarTri& ft, bool uni) {
-        if (!(gl && !(CLOSEST ? false : hit))) return;
+    auto test = [&](bool on, const FarTri& ft) {
+        if (!(on && !(CLOSEST ? false : hit))) return;
         if (!far_candidate(ft, fr, o, d)) return;
-        const rt_prim P = uni ? load_prim_scalar(S.prims, (int)ft.id) : S.prims[ft.id];
+        const rt_prim P = load_prim_scalar(S.prims, (int)__builtin_amdgcn_readfirstlane(ft.id));
         if (CLOSEST) {
             float t, a, b, g;
             if (tri_test<true, true>(P, o, d, t, a, b, g) && lex_better(t, (int)ft.id, found, h)) {
@@ -1293,17 +1299,51 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
             hit = true;
         }
     };
-    for (int q = 0; q < V.n_always; q++) test(load_far_tri(V.far_tris, (int)V.grid_always[q]), true);
+    for (int q = 0; q < V.n_always; q++) test(gl, load_far_tri(V.far_tris, (int)V.grid_always[q]));
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t glm = __ballot(gl);
+    uint32_t c0 = 0;
+    bool uniform = false;
+    if (glm) {
+        c0 = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)cell, __ffsll((unsigned long long)glm) - 1));
+        uniform = __ballot(gl && cell != c0) == 0;
+    }
     if (uniform) {
+        const bool mine = gl;
         const uint32_t b = V.grid_start[c0], e = V.grid_start[c0 + 1];
-        for (uint32_t k = b; k < e; k++) {
-            if (!CLOSEST && __ballot(gl && !hit) == 0) break;
-            const uint32_t idx = __builtin_amdgcn_readfirstlane(V.grid_items[k]);
-            test(load_far_tri(V.far_tris, (int)idx), true);
+        for (uint32_t t0 = b; t0 < e; t0 += 64) {
+            if (!CLOSEST && __ballot(mine && !hit) == 0) break;
+            // the previous tile's reads are done before it is overwritten
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (t0 + lane < e) tile[lane] = V.far_tris[V.grid_items[t0 + lane]];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const uint32_t m = e - t0 < 64u ? e - t0 : 64u;
+            for (uint32_t j = 0; j < m; j++) {
+                if (!CLOSEST && (j & 7u) == 0 && __ballot(mine && !hit) == 0) break;
+                test(mine, tile[j]);
+            }
         }
     } else if (gl) {
         const uint32_t b = V.grid_start[cell], e = V.grid_start[cell + 1];
-        for (uint32_t k = b; k < e && (CLOSEST || !hit); k++) test(V.far_tris[V.grid_items[k]], false);
+        for (uint32_t k = b; k < e && (CLOSEST || !hit); k++) {
+            const FarTri ft = V.far_tris[V.grid_items[k]];
+            if (!far_candidate(ft, fr, o, d)) continue;
+            const rt_prim P = S.prims[ft.id];
+            if (CLOSEST) {
+                float t, a, bb, g;
+                if (tri_test<true, true>(P, o, d, t, a, bb, g) && lex_better(t, (int)ft.id, found, h)) {
+                    found = true;
+                    hit = true;
+                    h.t = t; h.a = a; h.b = bb; h.g = g; h.prim = (int)ft.id;
+                }
+            } else if (prim_test_any(P, o, d)) {
+                hit = true;
+            }
+        }
     }
     return hit;
 }
@@ -1325,6 +1365,7 @@ __device__ __forceinline__ void any_hit_out(const DevWork& W, uint8_t* flag, uin
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
 far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
+    __shared__ FarTri ftile[TB / 64][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * TB;
     for (uint32_t base = (blockIdx.x * (TB / 64) + wave) * 64u; base < n; base += stride) {
@@ -1345,7 +1386,7 @@ far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
             const bool gl = live && grid_origin(S.bv, o);
             Hit hd;
             bool fd = false;
-            if (far_grid_lane<false>(S, gl, o, d, fr, hd, fd)) hit = true;
+            if (far_grid_lane<false>(S, gl, o, d, fr, hd, fd, ftile[wave])) hit = true;
             if (gl) live = false;  // done: the tree walk below serves the other lanes
         }
         int sp = 0;
@@ -1413,6 +1454,11 @@ __global__ void __launch_bounds__(TB) far_closest_lane_kernel(DevScene S, DevWor
 // for sparse queues, where sorted waves no longer share directions.
 // brute != 0: every primitive in scene order with the plain tests (the
 // reference's IntersectScene loop), for the far-origin rays.
+#ifdef RT580_DIAGNOSTICS
+// DIAGNOSTIC build only: brute any-hit scan statistics (rays, steps, rays
+// without an acceptor, their steps, rays decided by the call hint)
+__device__ unsigned long long g_brute_stats[5];
+#endif
 #ifndef BRUTE_ANY_U
 #define BRUTE_ANY_U 2  // far_scan_kernel brute any-hit: records per lane per ballot step
 #endif
@@ -1430,7 +1476,22 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
         const FarRay fr = far_ray(S.bv, o);
         if (!closest) {
             bool hit = false;
-            if (brute) {
+            // AO rays (flag null, tag = call): the record that accepted another
+            // sample of the same call, first (its samples share the far origin and
+            // mostly share an acceptor, tools/far_origin_study.cpp)
+            uint32_t* hintp = (brute && !flag && W.call_hint) ? W.call_hint + tag : nullptr;
+            if (hintp) {
+                const uint32_t hk = __builtin_amdgcn_readfirstlane(*hintp);
+                if (hk < (uint32_t)n_scan && lane == 0 && prim_hit_within(S.scan_prims[hk], o, d, tmax)) hit = true;
+            }
+#ifdef RT580_DIAGNOSTICS
+            if (brute && lane == 0) {
+                atomicAdd(&g_brute_stats[0], 1ull);
+                if (hit) atomicAdd(&g_brute_stats[4], 1ull);
+            }
+            int diag_steps = 0;
+#endif
+            if (brute && !__ballot(hit)) {
                 // BRUTE_ANY_U records per lane in flight per step, then one
                 // ballot; any order gives the same boolean
                 // in the shuffled order (DevScene::scan_prims): the first acceptor
@@ -1442,10 +1503,23 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
                         const int k = k0 + u * 64 + lane;
                         if (k < n_scan) p[u] = S.scan_prims[k];
                     }
+#ifdef RT580_DIAGNOSTICS
+                    diag_steps++;
+#endif
+                    int found_k = -1;
 #pragma unroll
-                    for (int u = 0; u < BRUTE_ANY_U; u++)
-                        if (k0 + u * 64 + lane < n_scan && prim_hit_within(p[u], o, d, tmax)) hit = true;
-                    if (__ballot(hit)) break;
+                    for (int u = 0; u < BRUTE_ANY_U; u++) {
+                        const int k = k0 + u * 64 + lane;
+                        if (k < n_scan && prim_hit_within(p[u], o, d, tmax)) {
+                            hit = true;
+                            if (found_k < 0) found_k = k;
+                        }
+                    }
+                    const uint64_t fm = __ballot(found_k >= 0);
+                    if (fm) {
+                        if (hintp && lane == __ffsll((unsigned long long)fm) - 1) *hintp = (uint32_t)found_k;
+                        break;
+                    }
                 }
             }
             for (int k0 = 0; !brute && k0 < n_scan; k0 += 64) {
@@ -1458,6 +1532,15 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
                 }
                 if (__ballot(hit)) break;
             }
+#ifdef RT580_DIAGNOSTICS
+            if (brute && lane == 0) {
+                atomicAdd(&g_brute_stats[1], (unsigned long long)diag_steps);
+                if (!__ballot(hit)) {
+                    atomicAdd(&g_brute_stats[2], 1ull);
+                    atomicAdd(&g_brute_stats[3], (unsigned long long)diag_steps);
+                }
+            }
+#endif
             if (__ballot(hit) && lane == 0) any_hit_out(W, flag, tag);
             continue;
         }
@@ -1517,6 +1600,7 @@ static int far_mode(uint32_t nq) {
 // rule; wave-cooperative like far_any_kernel.
 __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, uint32_t n) {
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
+    __shared__ FarTri ftile[TB / 64][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * TB;
     for (uint32_t base = (blockIdx.x * (TB / 64) + wave) * 64u; base < n; base += stride) {
@@ -1541,7 +1625,7 @@ __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, 
         const FarRay fr = far_ray(S.bv, o);
         bool changed = false;
         const bool gl = live && grid_origin(S.bv, o);
-        if (far_grid_lane<true>(S, gl, o, d, fr, h, found)) changed = true;
+        if (far_grid_lane<true>(S, gl, o, d, fr, h, found, ftile[wave])) changed = true;
         const bool walk = live && !gl;
         int sp = 0;
         stk[wave][sp++] = 0;
@@ -2183,6 +2267,9 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         if (e != hipSuccess) return e;
         const uint64_t items = calls * (uint64_t)F.ao_samples;
         const bool split = ao_split() != 0 && W.ao_rays && S.bv.nodes4 && !near_wave();
+        if (W.call_hint && S.bv.has_far && calls &&
+            (e = hipMemsetAsync(W.call_hint, 0xff, calls * 4, s)) != hipSuccess)
+            return e;
         uint64_t chunk = S.bv.has_far ? (uint64_t)W.far_cap : items;
         if (split && chunk > (uint64_t)W.ao_cap) chunk = W.ao_cap;
         for (uint64_t b = 0; b < items; b += chunk) {
@@ -2242,6 +2329,16 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             }
             progress("AO items [%llu, %llu) of %llu: far queue %u (brute %u)", (unsigned long long)b,
                      (unsigned long long)e1, (unsigned long long)items, nq, nb);
+#ifdef RT580_DIAGNOSTICS
+            {
+                unsigned long long st[5] = {0, 0, 0, 0, 0};
+                if (hipMemcpyFromSymbolAsync(st, HIP_SYMBOL(g_brute_stats), sizeof st, 0, hipMemcpyDeviceToHost, s) ==
+                        hipSuccess &&
+                    hipStreamSynchronize(s) == hipSuccess)
+                    progress("brute any-hit so far: rays %llu, steps %llu, no acceptor %llu (steps %llu), by hint %llu",
+                             st[0], st[1], st[2], st[3], st[4]);
+            }
+#endif
             if (nq == 0) continue;
             const int fm = far_mode(nq);
             if (fm == 1)

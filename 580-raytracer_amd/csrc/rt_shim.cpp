@@ -38,7 +38,8 @@ struct Slot {
     hipStream_t stream = nullptr;  // frame stream (non-blocking)
     hipEvent_t done = nullptr;     // end of the slot's last enqueued phase
     DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
-        row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream, aofix_items, aofix_count;
+        row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream, aofix_items, aofix_count,
+        call_hint;
 };
 
 struct State {
@@ -355,6 +356,14 @@ DevWork dev_work() {
                                                                                                     : nullptr;
     w.aofix_items = (uint64_t*)SL.aofix_items.p;
     w.aofix_count = (uint32_t*)SL.aofix_count.p;
+    {   // RT580_CALL_HINT=0 (A/B): no per-call acceptor hints
+        static int hint = -1;
+        if (hint < 0) {
+            const char* e = std::getenv("RT580_CALL_HINT");
+            hint = e ? std::atoi(e) : 1;
+        }
+        w.call_hint = hint ? (uint32_t*)SL.call_hint.p : nullptr;
+    }
     w.aofix_cap = (uint32_t)(SL.aofix_items.bytes / 8);
     return w;
 }
@@ -396,6 +405,7 @@ int ensure_work(const rt_render_params* p, int n_rows) {
         ensure(SL.totals, 64) || ensure(SL.call_node, ccap * 4) || ensure(SL.call_rng, ccap * 8) ||
         ensure(SL.occ, ccap * 4) || ensure(SL.aofix_items, (size_t)8 << 20) || ensure(SL.aofix_count, 64))
         return RT_FAILURE;
+    if (g.bvh_ok && !g.bvh.far_nodes.empty() && ensure(SL.call_hint, ccap * 4)) return RT_FAILURE;
     g.node_cap = (uint32_t)cap;
     g.call_cap = (uint32_t)ccap;
     // far-hit queue of the BVH AO pass (chunks of at most far_cap AO rays)
@@ -890,7 +900,8 @@ void shutdown_ctx() {
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
                           &sl.row_calls, &sl.row_hits, &sl.row_nodes, &sl.row_base_local, &sl.totals, &sl.call_node,
-                          &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.mt_stream, &sl.aofix_items, &sl.aofix_count})
+                          &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.mt_stream, &sl.aofix_items, &sl.aofix_count,
+                          &sl.call_hint})
             release(*b);
         if (sl.stream) (void)hipStreamDestroy(sl.stream);
         if (sl.done) (void)hipEventDestroy(sl.done);
