@@ -98,7 +98,11 @@ int Raytracer::Render(const std::string outputName) {
     }
     // Selected rows land in their frame positions; other rows keep their contents.
     const int nsel = (mParams.row_end - mParams.row_begin + mParams.row_step - 1) / mParams.row_step;
-    std::vector<int16_t> rows((size_t)(nsel > 0 ? nsel : 0) * mWidth * 3);
+    const bool whole = mParams.row_begin == 0 && mParams.row_step == 1 && mParams.row_end == mHeight;
+    static_assert(sizeof(Pixel) == 6, "Pixel is int16 r, g, b");
+    // a whole frame lands in mFrameBuffer directly; selected rows through a row buffer
+    std::vector<int16_t> rows(whole ? 0 : (size_t)(nsel > 0 ? nsel : 0) * mWidth * 3);
+    int16_t* dst = whole ? reinterpret_cast<int16_t*>(mFrameBuffer.data()) : rows.data();
     // Whole frames shard across the node's GPUs (interleaved rows, RCCL
     // exchange + gather, rt_gpu_render_multi); SetGpuCount / $RT580_GPUS
     // choose how many (default: every visible device).
@@ -107,11 +111,10 @@ int Raytracer::Render(const std::string outputName) {
         const char* e = std::getenv("RT580_GPUS");
         gpus = e ? std::atoi(e) : rt_gpu_device_count();
     }
-    const bool whole = mParams.row_begin == 0 && mParams.row_step == 1 && mParams.row_end == mHeight;
-    const int st = (gpus > 1 && whole) ? rt_gpu_render_multi(&mParams, rows.data(), gpus, nullptr)
-                                       : rt_gpu_render(&mParams, rows.data());
+    const int st = (gpus > 1 && whole) ? rt_gpu_render_multi(&mParams, dst, gpus, nullptr)
+                                       : rt_gpu_render(&mParams, dst);
     if (st != RT_SUCCESS) return RT_FAILURE;
-    for (int k = 0; k < nsel; k++) {
+    for (int k = 0; !whole && k < nsel; k++) {
         int y = mParams.row_begin + k * mParams.row_step;
         std::memcpy(&mFrameBuffer[(size_t)y * mWidth], &rows[(size_t)k * mWidth * 3], (size_t)mWidth * 6);
     }

@@ -73,6 +73,10 @@ struct State {
     int last_slot = -1;        // slot of the previous frame call
     uint64_t frames = 0;       // frames begun
     hipEvent_t user_mark[2] = {nullptr, nullptr};  // the caller's stream at the start of a frame call
+    // rt_gpu_render's host copy: pinned staging, filled in chunks (one event each)
+    int16_t* stage = nullptr;
+    size_t stage_bytes = 0;
+    std::array<hipEvent_t, 16> stage_ev{};
     bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
     // BVH far-queue buffers (BVH frames always run serialized on slot 0)
     DevBuf ao_rays;
@@ -715,11 +719,43 @@ int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     return fail("node capacity could not be sized");
 }
 
+// The framebuffer to the caller's (pageable) memory: device -> pinned staging in
+// up to 16 chunks, each chunk's host copy overlapping the next chunks' DMA.
+int copy_out(const int16_t* dev, int16_t* fb_out, size_t bytes) {
+    if (g.stage_bytes < bytes) {
+        if (g.stage) (void)hipHostFree(g.stage);
+        g.stage = nullptr;
+        g.stage_bytes = 0;
+        HIP_TRY(hipHostMalloc((void**)&g.stage, bytes, hipHostMallocDefault));
+        g.stage_bytes = bytes;
+    }
+    if (!g.stage_ev[0])
+        for (auto& ev : g.stage_ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const size_t nch = g.stage_ev.size();
+    size_t chunk = (bytes + nch - 1) / nch;
+    if (chunk < ((size_t)1 << 20)) chunk = (size_t)1 << 20;
+    const char* src = (const char*)dev;
+    char* stg = (char*)g.stage;
+    size_t k = 0;
+    for (size_t off = 0; off < bytes; off += chunk, k++) {
+        const size_t n = bytes - off < chunk ? bytes - off : chunk;
+        HIP_TRY(hipMemcpyAsync(stg + off, src + off, n, hipMemcpyDeviceToHost, g.stream));
+        HIP_TRY(hipEventRecord(g.stage_ev[k], g.stream));
+    }
+    k = 0;
+    for (size_t off = 0; off < bytes; off += chunk, k++) {
+        const size_t n = bytes - off < chunk ? bytes - off : chunk;
+        HIP_TRY(hipEventSynchronize(g.stage_ev[k]));
+        std::memcpy((char*)fb_out + off, stg + off, n);
+    }
+    return RT_SUCCESS;
+}
+
 int rt_gpu_render(const rt_render_params* p, int16_t* fb_out) {
     int16_t* dev = nullptr;
     if (rt_gpu_render_device(p, &dev)) return RT_FAILURE;
     const size_t bytes = (size_t)n_selected_rows(p) * p->width * 6;
-    if (bytes && fb_out) HIP_TRY(hipMemcpyAsync(fb_out, dev, bytes, hipMemcpyDeviceToHost, g.stream));
+    if (bytes && fb_out && copy_out(dev, fb_out, bytes)) return RT_FAILURE;
     HIP_TRY(hipStreamSynchronize(g.stream));
     return RT_SUCCESS;
 }
@@ -914,6 +950,9 @@ void shutdown_ctx() {
         for (auto& ev : q) (void)hipEventDestroy(ev);
     if (g.needed_host) (void)hipHostFree(g.needed_host);
     if (g.far_count_host) (void)hipHostFree(g.far_count_host);
+    if (g.stage) (void)hipHostFree(g.stage);
+    for (auto& ev : g.stage_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (g.own_stream) (void)hipStreamDestroy(g.own_stream);
     g = State();
 }
@@ -1106,7 +1145,7 @@ int multi_finish(const rt_render_params* p, int n, int n_max, int16_t* fb_out) {
     }
     HIP_TRY(launch_deinterleave((const int16_t*)g_multi.root_tiles.p, n, n_max, W, H, (int16_t*)g_multi.frame.p,
                                 g.stream));
-    HIP_TRY(hipMemcpyAsync(fb_out, g_multi.frame.p, (size_t)H * W * 6, hipMemcpyDeviceToHost, g.stream));
+    if (copy_out((const int16_t*)g_multi.frame.p, fb_out, (size_t)H * W * 6)) return RT_FAILURE;
     HIP_TRY(hipStreamSynchronize(g.stream));
     for (int k = 1; k < n; k++) {  // the other devices' streams are idle again before the next frame
         g_cur = k;

@@ -345,9 +345,11 @@ def roofline(workload, k_ms, k_launches, k_rays, rays_ao_frame):
 def render_latency(lib, rt580, params, torch, n=3):
     """Blocking rt_gpu_render (what Render() calls): first launch -> int16
     framebuffer on the host (SURVEY §8d ms/frame), excluding scene load/upload
-    and the PPM write. Mean of n calls after the timed region."""
+    and the PPM write. Mean of n calls after the timed region, after one untimed
+    call (the first sizes the pinned staging buffer of the host copy)."""
     import numpy as np
     host = np.zeros(params.width * params.height * 3, dtype=np.int16)
+    rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
     times = []
     for _ in range(n):
         torch.cuda.synchronize()
