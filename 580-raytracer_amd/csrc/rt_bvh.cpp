@@ -551,7 +551,9 @@ void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells) {
     if (out.far_tris.empty() || log2_cells <= 0) return;
     const int L = log2_cells, M = 1 << L;
     const double S = out.scale;
-    const double R = 4.0 * S;  // origins on (or 0.2 off) the scene's surfaces; farther ones walk the plane tree
+    double rmul = 4.0;  // (RT580_GRID_R: A/B of the origin radius, in units of S)
+    if (const char* e = std::getenv("RT580_GRID_R")) rmul = std::atof(e);
+    const double R = rmul * S;  // origins on (or 0.2 off) the scene's surfaces; farther ones walk the plane tree
     std::vector<GridTri> gt(out.far_tris.size());
     std::vector<uint8_t> ok(out.far_tris.size());
     for (size_t k = 0; k < out.far_tris.size(); k++) {
