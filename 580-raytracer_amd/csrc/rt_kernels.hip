@@ -1182,12 +1182,59 @@ ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
 // over the 4-wide tree with nothing else live, then ao_finish. Rays
 // [0, e - b) of the chunk whose first item is b.
 // LDS_D > 0: the first LDS_D traversal-stack entries of each lane live in LDS.
-template <int WPE, int LDS_D = 0>
+// SORT > 0: the workgroup takes SORT * TB consecutive samples (SORT * TB / N
+// calls of neighbouring pixels) at a time and traces them in the order of a
+// counting sort by octahedral direction cell (8 x 8): a wave then holds rays
+// of similar direction from nearby origins, which share more of their paths
+// (tools/simd_sim.cpp "block sort"). Hits are then counted per lane.
+template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
-    for (uint64_t b0 = (uint64_t)blockIdx.x * TB; b0 < n; b0 += (uint64_t)gridDim.x * TB) {
-        const uint64_t i = b0 + threadIdx.x;
+    constexpr int SN = SORT > 0 ? SORT * TB : 1;
+    constexpr int NB = 1 << (2 * KL);  // direction cells
+    __shared__ uint32_t s_order[SN];
+    __shared__ uint32_t s_bin[SORT > 0 ? NB + 1 : 1];
+    const uint64_t span = SORT > 0 ? (uint64_t)SN : (uint64_t)TB;
+    for (uint64_t blk = (uint64_t)blockIdx.x * span; blk < n; blk += (uint64_t)gridDim.x * span)
+    for (int round = 0; round < (SORT > 0 ? SORT : 1); round++) {
+        uint64_t i = blk + threadIdx.x;
+        if (SORT > 0) {
+            if (round == 0) {
+                // counting sort of the block's samples by direction cell
+                __syncthreads();
+                for (int k = threadIdx.x; k < NB + 1; k += TB) s_bin[k] = 0;
+                __syncthreads();
+                uint32_t key[SORT > 0 ? SORT : 1];
+#pragma unroll
+                for (int q = 0; q < SORT; q++) {
+                    const uint64_t j = blk + (uint64_t)q * TB + threadIdx.x;
+                    key[q] = NB;  // past the end: last
+                    if (j < n) {
+                        const float4 r1 = W.ao_rays[2 * j + 1];
+                        key[q] = grid_cell(v3(r1.x, r1.y, r1.z), KL);
+                    }
+                    atomicAdd(&s_bin[key[q]], 1u);
+                }
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    uint32_t acc = 0;
+                    for (int k = 0; k < NB + 1; k++) {
+                        const uint32_t c = s_bin[k];
+                        s_bin[k] = acc;
+                        acc += c;
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < SORT; q++) {
+                    const uint32_t pos = atomicAdd(&s_bin[key[q]], 1u);
+                    s_order[pos] = (uint32_t)(q * TB + threadIdx.x);
+                }
+                __syncthreads();
+            }
+            i = blk + s_order[round * TB + threadIdx.x];
+        }
         float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
         if (i < n) {
             r0 = W.ao_rays[2 * i];
@@ -1204,7 +1251,8 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
         } else {
             hit = flag == 1u && bvh4_any_near(S.bv, o, d);
         }
-        ao_finish<true>(S, W, N, active, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o, d);
+        // sorted: a wave's lanes are no longer one call's samples
+        ao_finish<true>(S, W, SORT > 0 ? 1u : N, active, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o, d);
     }
 }
 
@@ -1246,6 +1294,19 @@ static int trace_lds() {
     if (v < 0) {
         const char* e = getenv("RT580_TRACE_LDS");
         v = e ? atoi(e) : 1;
+    }
+    return v;
+}
+
+static int ao_sort() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_SORT");
+        // 3: blocks of 2048 samples by 16 x 16 direction cells. AO field100k
+        // 1080p 53.9 -> 49.3 ms, cornell10k 80.1 -> 77.9 ms (0: unsorted;
+        // 1: 1024 / 8 x 8 50.6 / 79.4; 2: 2048 / 8 x 8 49.4; 4096 samples
+        // lose occupancy: 59.1 / 88.4)
+        v = e ? atoi(e) : 3;
     }
     return v;
 }
@@ -2288,7 +2349,17 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 kt_begin(s);
                 const int twpe = trace_wpe();
-                if (twpe == 6 && trace_lds())  // 16-entry LDS stacks (default)
+                const int so = ao_sort();
+                if (twpe == 6 && trace_lds() && so == 1)  // (A/B) direction-sorted blocks of 1024 samples
+                    hipLaunchKernelGGL((ao_trace_kernel<6, 16, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
+                                       (uint32_t)F.ao_samples, e1 - b);
+                else if (twpe == 6 && trace_lds() && so == 2)  // 2048 samples, 8 x 8 cells
+                    hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
+                                       (uint32_t)F.ao_samples, e1 - b);
+                else if (twpe == 6 && trace_lds() && so == 3)  // 2048 samples, 16 x 16 cells (default)
+                    hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S,
+                                       W, (uint32_t)F.ao_samples, e1 - b);
+                else if (twpe == 6 && trace_lds())  // 16-entry LDS stacks (default)
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
                 else if (twpe == 4)
