@@ -38,8 +38,12 @@ RTM_HD bool quot_lt0(float num, float den) {
 // IntersectTriangle. WANT_BARY: also return alpha/beta/gamma (closest hit); the
 // any-hit form only needs the accept/reject decision. Both decide exactly as
 // the reference's divisions would.
+// tcut: a hit with t > tcut is reported as a miss before the sub-areas are
+// computed (closest-hit callers pass their best t -- such a hit cannot win;
+// bounded any-hit callers their bound): the same decision for every hit that
+// matters, less work for the ones that do not.
 template <bool WANT_BARY, bool SIGN = false>
-RTM_HD bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
+RTM_HD bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g, float tcut = INFINITY) {
     const rv3 N = ld3(P.nrm);
     const float nd = v3_dot(N, d);
     if (rt_lt_eps(fabsf(nd))) return false;  // NearlyEquals(nd, 0)
@@ -48,6 +52,7 @@ RTM_HD bool tri_test(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& 
     if (SIGN && num == num && (num == 0.0f || signbit(num) != signbit(nd))) return false;
     t = num / nd;
     if (rt_lt_eps(t)) return false;           // t <= EPSILON
+    if (t > tcut) return false;
     const rv3 Pp = v3_add(o, v3_scale(d, t));
     const rv3 v0 = ld3(P.p0), v1 = ld3(P.p1), v2 = ld3(P.p2);
     // CalcTriangleAreaSigned (Raytracer.cpp:937-942): 0.5 * dot(cross(B-A, C-A), N)
@@ -90,9 +95,10 @@ RTM_HD bool sph_test(const rt_prim& P, rv3 o, rv3 d, float& t) {
     return true;
 }
 
-RTM_HD bool prim_test_closest(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g) {
+RTM_HD bool prim_test_closest(const rt_prim& P, rv3 o, rv3 d, float& t, float& a, float& b, float& g,
+                              float tcut = INFINITY) {
     a = b = g = 0.0f;
-    return P.kind == RT_PRIM_TRIANGLE ? tri_test<true, true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+    return P.kind == RT_PRIM_TRIANGLE ? tri_test<true, true>(P, o, d, t, a, b, g, tcut) : sph_test(P, o, d, t);
 }
 
 RTM_HD bool prim_test_any(const rt_prim& P, rv3 o, rv3 d) {
@@ -307,7 +313,7 @@ RTM_HD bool far_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool found) {
             RT_CNT(far_tests, 1);
             const int j = (int)ft.id;
             float t, a, bb, g;
-            if (tri_test<true, true>(V.all[j], o, d, t, a, bb, g) && lex_better(t, j, found, h)) {
+            if (tri_test<true, true>(V.all[j], o, d, t, a, bb, g, found ? h.t : INFINITY) && lex_better(t, j, found, h)) {
                 found = true;
                 h.t = t; h.a = a; h.b = bb; h.g = g; h.prim = j;
             }
@@ -335,7 +341,7 @@ RTM_HD bool far_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool found) {
             RT_CNT(far_tests, 1);
             const int j = (int)ft.id;
             float t, a, b, g;
-            if (tri_test<true, true>(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
+            if (tri_test<true, true>(V.all[j], o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, j, found, h)) {
                 found = true;
                 h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
             }
@@ -353,7 +359,7 @@ RTM_HD bool bvh_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool with_far = 
     for (int k = 0; k < V.n_brute; k++) {
         const int j = (int)V.brute[k];
         float t, a, b, g;
-        if (prim_test_closest(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
+        if (prim_test_closest(V.all[j], o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, j, found, h)) {
             found = true;
             h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
         }
@@ -390,7 +396,7 @@ RTM_HD bool bvh_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool with_far = 
             RT_CNT(leaf_tris, n);
             for (int k = c; k < c + n; k++) {
                 float t, a, b, g;
-                if (tri_test<true, true>(V.prims[k], o, d, t, a, b, g)) {
+                if (tri_test<true, true>(V.prims[k], o, d, t, a, b, g, found ? h.t : INFINITY)) {
                     const int id = (int)V.ids[k];
                     if (lex_better(t, id, found, h)) {
                         found = true;
@@ -460,7 +466,7 @@ RTM_HD bool far_any(const BvhView& V, rv3 o, rv3 d) {
 // is entered at or before t).
 RTM_HD bool prim_hit_within(const rt_prim& P, rv3 o, rv3 d, float tmax) {
     float t, a, b, g;
-    const bool h = P.kind == RT_PRIM_TRIANGLE ? tri_test<false, true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+    const bool h = P.kind == RT_PRIM_TRIANGLE ? tri_test<false, true>(P, o, d, t, a, b, g, tmax) : sph_test(P, o, d, t);
     return h && !(t > tmax);
 }
 
@@ -497,7 +503,7 @@ RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true, float 
             RT_CNT(leaf_tris, n);
             for (int k = c; k < c + n; k++) {
                 float t, a, b, g;
-                if (tri_test<false, true>(V.prims[k], o, d, t, a, b, g) && !(t > tmax)) return true;
+                if (tri_test<false, true>(V.prims[k], o, d, t, a, b, g, tmax) && !(t > tmax)) return true;
             }
         }
         if (sp == 0) break;
@@ -616,7 +622,7 @@ RTM_HD bool bvh4_leaf_hit(const BvhView& V, rv3 o, rv3 d, float tmax, int32_t c,
         rt_prim P;
         load_prim(V.prims + k, P);
         float tt, a, b, g;
-        if (tri_test<false, true>(P, o, d, tt, a, b, g) && !(tt > tmax)) return true;
+        if (tri_test<false, true>(P, o, d, tt, a, b, g, tmax) && !(tt > tmax)) return true;
     }
     return false;
 }
@@ -667,7 +673,7 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
     for (int k = 0; k < V.n_brute; k++) {
         const int j = (int)V.brute[k];
         float t, a, b, g;
-        if (prim_test_closest(V.all[j], o, d, t, a, b, g) && lex_better(t, j, found, h)) {
+        if (prim_test_closest(V.all[j], o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, j, found, h)) {
             found = true;
             h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
         }
@@ -728,7 +734,7 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
             rt_prim P;
             load_prim(V.prims + k, P);
             float t, a, b, g;
-            if (tri_test<true, true>(P, o, d, t, a, b, g)) {
+            if (tri_test<true, true>(P, o, d, t, a, b, g, found ? h.t : INFINITY)) {
                 const int id = (int)V.ids[k];
                 if (lex_better(t, id, found, h)) {
                     found = true;

@@ -107,7 +107,8 @@ __device__ bool closest_hit(const DevScene& S, rt_prim* tile, bool resident, boo
             for (int j = 0; j < n; j++) {
                 const rt_prim& P = tile[j];
                 float t, a = 0, b = 0, g = 0;
-                bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test<true>(P, o, d, t, a, b, g) : sph_test(P, o, d, t);
+                bool hit = P.kind == RT_PRIM_TRIANGLE ? tri_test<true>(P, o, d, t, a, b, g, found ? h.t : INFINITY)
+                                                      : sph_test(P, o, d, t);
                 if (hit && (!found || t < h.t)) {
                     found = true;
                     h.t = t; h.a = a; h.b = b; h.g = g; h.prim = base + j;
@@ -165,8 +166,9 @@ __device__ bool closest_hit_scalar(const DevScene& S, bool active, rv3 o, rv3 d,
     for (int j = 0; j < S.n_prims; j++) {
         const rt_prim P = load_prim_scalar(S.prims, j);
         float t, a = 0, b = 0, g = 0;
-        const bool hit = active && (P.kind == RT_PRIM_TRIANGLE ? tri_test<true, SIGN>(P, o, d, t, a, b, g)
-                                                               : sph_test(P, o, d, t));
+        const bool hit = active && (P.kind == RT_PRIM_TRIANGLE
+                                        ? tri_test<true, SIGN>(P, o, d, t, a, b, g, found ? h.t : INFINITY)
+                                        : sph_test(P, o, d, t));
         if (hit && (!found || t < h.t)) {
             found = true;
             h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
@@ -1351,7 +1353,7 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
         const rt_prim P = load_prim_scalar(S.prims, (int)__builtin_amdgcn_readfirstlane(ft.id));
         if (CLOSEST) {
             float t, a, b, g;
-            if (tri_test<true, true>(P, o, d, t, a, b, g) && lex_better(t, (int)ft.id, found, h)) {
+            if (tri_test<true, true>(P, o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, (int)ft.id, found, h)) {
                 found = true;
                 hit = true;
                 h.t = t; h.a = a; h.b = b; h.g = g; h.prim = (int)ft.id;
@@ -1396,7 +1398,7 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
             const rt_prim P = S.prims[ft.id];
             if (CLOSEST) {
                 float t, a, bb, g;
-                if (tri_test<true, true>(P, o, d, t, a, bb, g) && lex_better(t, (int)ft.id, found, h)) {
+                if (tri_test<true, true>(P, o, d, t, a, bb, g, found ? h.t : INFINITY) && lex_better(t, (int)ft.id, found, h)) {
                     found = true;
                     hit = true;
                     h.t = t; h.a = a; h.b = bb; h.g = g; h.prim = (int)ft.id;
@@ -1616,7 +1618,7 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
                 id = (int)ft.id;
             }
             float t, aa, bb, gg;
-            if (prim_test_closest(S.prims[id], o, d, t, aa, bb, gg) && lex_better(t, id, found, h)) {
+            if (prim_test_closest(S.prims[id], o, d, t, aa, bb, gg, found ? h.t : INFINITY) && lex_better(t, id, found, h)) {
                 found = true;
                 h.t = t; h.a = aa; h.b = bb; h.g = gg; h.prim = id;
             }
@@ -1707,7 +1709,7 @@ __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, 
                 if (__ballot(cand) == 0) continue;
                 const rt_prim P = load_prim_scalar(S.prims, (int)ft.id);
                 float t, a, b, g;
-                if (cand && prim_test_closest(P, o, d, t, a, b, g) && lex_better(t, (int)ft.id, found, h)) {
+                if (cand && prim_test_closest(P, o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, (int)ft.id, found, h)) {
                     found = true;
                     changed = true;
                     h.t = t; h.a = a; h.b = b; h.g = g; h.prim = (int)ft.id;
