@@ -1646,6 +1646,78 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
     }
 }
 
+// Brute closest hit of far-origin tree rays, split: wave w scans slice
+// w % splits of the scene for ray w / splits (few rays, each a full scan: one
+// wave per ray left most of the GPU idle and each wave waiting on its loads);
+// the slices' lexicographic (t, primitive) minima meet in best[r] by a 64-bit
+// atomicMin (t > EPSILON > 0: float bits order like the values).
+__global__ void __launch_bounds__(TB) far_brute_split_kernel(DevScene S, DevWork W, uint32_t first, uint32_t nb,
+                                                             uint32_t splits, unsigned long long* best) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t total = (uint64_t)nb * splits;
+    for (uint64_t w = (uint64_t)blockIdx.x * (TB / 64) + (threadIdx.x >> 6); w < total;
+         w += (uint64_t)gridDim.x * (TB / 64)) {
+        const uint32_t r = (uint32_t)(w / splits), sl = (uint32_t)(w % splits);
+        const uint32_t q = W.far_vals_alt[first + r];
+        const float4 a = W.far_rays[2 * (size_t)q], b = W.far_rays[2 * (size_t)q + 1];
+        const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+        const int n = S.n_prims;
+        const int k0 = (int)((uint64_t)n * sl / splits), k1 = (int)((uint64_t)n * (sl + 1) / splits);
+        Hit h;
+        h.t = 0; h.prim = -1;
+        bool found = false;
+        for (int k = k0 + lane; k < k1; k += 64) {
+            float t, aa, bb, gg;
+            if (prim_test_closest(S.prims[k], o, d, t, aa, bb, gg, found ? h.t : INFINITY) && lex_better(t, k, found, h)) {
+                found = true;
+                h.t = t; h.prim = k;
+            }
+        }
+        uint64_t key = found ? (((uint64_t)__float_as_uint(h.t) << 32) | (uint32_t)h.prim) : ~0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t other = __shfl_xor(key, off);
+            key = other < key ? other : key;
+        }
+        if (lane == 0 && key != ~0ull) atomicMin(best + r, (unsigned long long)key);
+    }
+}
+
+// The winners of far_brute_split_kernel: the exact test again for (t, alpha,
+// beta, gamma), merged into the ray's provisional hit with the same rule.
+__global__ void __launch_bounds__(TB) far_brute_merge_kernel(DevScene S, DevWork W, uint32_t first, uint32_t nb,
+                                                             const unsigned long long* best) {
+    for (uint32_t r = blockIdx.x * TB + threadIdx.x; r < nb; r += gridDim.x * TB) {
+        const unsigned long long key = best[r];
+        if (key == ~0ull) continue;
+        const uint32_t q = W.far_vals_alt[first + r];
+        const float4 a = W.far_rays[2 * (size_t)q], b = W.far_rays[2 * (size_t)q + 1];
+        const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+        const uint32_t tag = __float_as_uint(a.w);
+        const int id = (int)(uint32_t)key;
+        Hit h;
+        float t, aa, bb, gg;
+        if (!prim_test_closest(S.prims[id], o, d, t, aa, bb, gg)) continue;  // (same test: cannot fail)
+        h.t = t; h.a = aa; h.b = bb; h.g = gg; h.prim = id;
+        const float4 hv = W.hit4[tag];
+        const int32_t hp = W.hit_prim[tag];
+        Hit cur;
+        cur.t = hv.x; cur.prim = hp;
+        if (lex_better(h.t, h.prim, hp >= 0, cur)) {
+            W.hit4[tag] = make_float4(h.t, h.a, h.b, h.g);
+            W.hit_prim[tag] = h.prim;
+        }
+    }
+}
+
+static int brute_split() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_BRUTE_SPLIT");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
+}
+
 // Far-pass flavour for a queue of nq rays: 1 = wave union (sorted, dense
 // queues), 2 = per lane, 3 = scan. RT580_FAR_MODE overrides the size rule (A/B only).
 static int far_mode(uint32_t nq) {
@@ -2196,8 +2268,21 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
                 if (nb) {
                     RT_STEP("trace brute scan");
-                    hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W,
-                                       nq - nb, nq, 1, (int)S.bv.n_far, 1, (uint8_t*)nullptr);
+                    if (brute_split() && (uint64_t)nb * 2 <= W.far_cap) {
+                        // the sort's input keys are free now: 64-bit minima per brute ray
+                        unsigned long long* best = reinterpret_cast<unsigned long long*>(W.far_keys);
+                        if ((e = hipMemsetAsync(best, 0xff, (size_t)nb * 8, s)) != hipSuccess) return e;
+                        uint32_t splits = 32768u / nb;
+                        splits = splits < 1u ? 1u : (splits > 512u ? 512u : splits);
+                        hipLaunchKernelGGL(far_brute_split_kernel, dim3(grid_for((uint64_t)nb * splits * 64, 16384)),
+                                           dim3(TB), 0, s, S, W, nq - nb, nb, splits, best);
+                        if ((e = hipGetLastError()) != hipSuccess) return e;
+                        hipLaunchKernelGGL(far_brute_merge_kernel, dim3(grid_for(nb, 4096)), dim3(TB), 0, s, S, W,
+                                           nq - nb, nb, (const unsigned long long*)best);
+                    } else {
+                        hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s,
+                                           S, W, nq - nb, nq, 1, (int)S.bv.n_far, 1, (uint8_t*)nullptr);
+                    }
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                     nq -= nb;
                 }
