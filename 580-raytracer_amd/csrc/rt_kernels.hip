@@ -1341,7 +1341,7 @@ static int near_wpe() {
 // after the other instead: field1m AO 2.26 -> 5.54 s -- waves hold many.)
 // Each candidate gets far_candidate + the full reference test. Must be called
 // by the whole wave.
-template <bool CLOSEST>
+template <bool CLOSEST, int U = 1>
 __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o, rv3 d, const FarRay& fr, Hit& h,
                                               bool& found, FarTri* tile) {
     const BvhView& V = S.bv;
@@ -1391,9 +1391,20 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
             }
         }
     } else if (gl) {
+        // U candidates per step: their list entries, then their planes, in
+        // flight together (the lane's loads are a dependent chain otherwise)
         const uint32_t b = V.grid_start[cell], e = V.grid_start[cell + 1];
-        for (uint32_t k = b; k < e && (CLOSEST || !hit); k++) {
-            const FarTri ft = V.far_tris[V.grid_items[k]];
+        for (uint32_t k0 = b; k0 < e && (CLOSEST || !hit); k0 += U) {
+          uint32_t idx[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) idx[u] = k0 + u < e ? V.grid_items[k0 + u] : 0u;
+          FarTri fts[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) fts[u] = V.far_tris[idx[u]];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            if (k0 + u >= e || !(CLOSEST || !hit)) continue;
+            const FarTri& ft = fts[u];
             if (!far_candidate(ft, fr, o, d)) continue;
             const rt_prim P = S.prims[ft.id];
             if (CLOSEST) {
@@ -1406,6 +1417,7 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
             } else if (prim_test_any(P, o, d)) {
                 hit = true;
             }
+          }
         }
     }
     return hit;
@@ -1425,6 +1437,7 @@ __device__ __forceinline__ void any_hit_out(const DevWork& W, uint8_t* flag, uin
     else atomicAdd(&W.occ[tag], 1u);
 }
 
+template <int U = 1>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
 far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
@@ -1449,7 +1462,7 @@ far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
             const bool gl = live && grid_origin(S.bv, o);
             Hit hd;
             bool fd = false;
-            if (far_grid_lane<false>(S, gl, o, d, fr, hd, fd, ftile[wave])) hit = true;
+            if (far_grid_lane<false, U>(S, gl, o, d, fr, hd, fd, ftile[wave])) hit = true;
             if (gl) live = false;  // done: the tree walk below serves the other lanes
         }
         int sp = 0;
@@ -1967,6 +1980,23 @@ static int grid_for(uint64_t items, int cap) {
     return (int)(b < (uint64_t)cap ? b : (uint64_t)cap);
 }
 
+// Candidates in flight per lane in far_any_kernel's per-lane list walk
+// (RT580_FAR_U = 1, 2, 4).
+static void launch_far_any(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s) {
+    static int u = -1;
+    if (u < 0) {
+        const char* e = getenv("RT580_FAR_U");
+        u = e ? atoi(e) : 2;  // field1m frame 2252 (1) -> 2207 ms (2); 4 spills (2402)
+    }
+    if (u == 4)
+        hipLaunchKernelGGL(far_any_kernel<4>, dim3(grid_for(n, 16384)), dim3(TB), 0, s, S, W, n, flag);
+    else if (u == 2)
+        hipLaunchKernelGGL(far_any_kernel<2>, dim3(grid_for(n, 16384)), dim3(TB), 0, s, S, W, n, flag);
+    else
+        hipLaunchKernelGGL(far_any_kernel<1>, dim3(grid_for(n, 16384)), dim3(TB), 0, s, S, W, n, flag);
+}
+
+
 __constant__ uint8_t c_gamma_lut[256];
 
 __global__ void gamma_u8_kernel(const int16_t* __restrict__ fb, uint64_t n, uint8_t* __restrict__ out) {
@@ -2333,7 +2363,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         }
                         if (sq) {
                             RT_STEP("trace shadow far pass");
-                            hipLaunchKernelGGL(far_any_kernel, dim3(grid_for(sq, 16384)), dim3(TB), 0, s, S, W, sq, flags);
+                            launch_far_any(S, W, sq, flags, s);
                             if ((e = hipGetLastError()) != hipSuccess) return e;
                         }
                     }
@@ -2500,7 +2530,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if (nq == 0) continue;
             const int fm = far_mode(nq);
             if (fm == 1)
-                hipLaunchKernelGGL(far_any_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq, (uint8_t*)nullptr);
+                launch_far_any(S, W, nq, (uint8_t*)nullptr, s);
             else if (fm == 2)
                 hipLaunchKernelGGL(far_any_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq,
                                    (uint8_t*)nullptr);
