@@ -39,22 +39,35 @@ VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0   # 1228.8 G wave-instructions/s
 HBM_PEAK_GBS = 8000.0
 
 # name -> (scene, synthetic?, width, height, depth, AO samples,
-#          CPU-baseline sample (w, h, depth, ao), label)
-# The CPU sample is a downscaled frame of the same scene (~10-30 s for the
-# ref-faithful restatement on one core); the reference is O(primitives) per ray,
-# so the triangle scenes get tiny samples.
+#          CPU-baseline sample, label)
+# CPU sample (~10-30 s for the ref-faithful restatement on one core):
+#   (w, h, depth, ao)  a downscaled frame of the same scene (config 2: exact bytes);
+#   ("pixels", P[, A]) P pixels of the workload's own full-resolution frame on a
+#                      stratified grid, at its depth and AO count (A: a smaller AO
+#                      count, config 5 only: one 1M-triangle pixel at AO 256 is
+#                      minutes of CPU; the reference's IntersectScene loops over every
+#                      primitive for every ray, Raytracer.cpp:476-521, so its cost
+#                      per ray does not depend on the ray's kind).
 WORKLOADS = {
     "config2": ("simpleSphereScene.json", False, 1920, 1080, 4, 64, (480, 270, 4, 64),
                 "BASELINE config 2: simpleSphereScene.json 1920x1080 depth=4 AO=64"),
-    "cornell10k": ("cornell10k.json", True, 1920, 1080, 4, 64, (6, 4, 4, 64),
+    "cornell10k": ("cornell10k.json", True, 1920, 1080, 4, 64, ("pixels", 16),
                    "BASELINE config 3: 10k-triangle Cornell box 1920x1080 depth=4 AO=64"),
-    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64, (2, 2, 4, 64),
+    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64, ("pixels", 8),
                         "north_star target: 100k-triangle field 1920x1080 depth=4 AO=64"),
-    "field100k": ("field100k.json", True, 3840, 2160, 6, 256, (2, 1, 6, 64),
+    "field100k": ("field100k.json", True, 3840, 2160, 6, 256, ("pixels", 2),
                   "BASELINE config 4: 100k-triangle field 3840x2160 depth=6 AO=256"),
-    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, (1, 1, 8, 2),
+    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, ("pixels", 1, 16),
                 "BASELINE config 5: 1M-triangle field 7680x4320 depth=8 AO=256"),
 }
+
+
+def stratified_pixels(n, w, h):
+    """n pixel centres of a gx x gy (>= n cells) grid over the w x h frame (raster order)."""
+    gx = max(1, int(round((n * w / h) ** 0.5)))
+    gy = (n + gx - 1) // gx
+    pts = [(int((i + 0.5) * w / gx), int((j + 0.5) * h / gy)) for j in range(gy) for i in range(gx)]
+    return [pts[k * len(pts) // n] for k in range(n)]  # n cells spread over the whole grid
 
 
 def env_int(k, d):
@@ -364,17 +377,38 @@ def cpu_baseline(lib, rt580, helpers, root):
     reference's per-call work: string mesh lookup and ComputeModelMatrix per
     shape per IntersectScene call, the unused Matrix::Inverse + TransformPoint
     per triangle test; oracle_set_mode(1)) on a bounded sample of the same
-    workload, on 1 core and on all of this host's cores (threads), rows of the
-    same RNG stream. The reference itself does not travel to this box."""
-    w, h, depth, ao = CPU_SAMPLE
+    workload (CPU_SAMPLE), on 1 core and on all of this host's cores (threads).
+    The reference itself does not travel to this box."""
     threads = env_int("OMP_NUM_THREADS", os.cpu_count() or 1)
+    if CPU_SAMPLE[0] == "pixels":
+        pts = stratified_pixels(CPU_SAMPLE[1], WIDTH, HEIGHT)
+        ao = CPU_SAMPLE[2] if len(CPU_SAMPLE) > 2 else AO
+        threads = min(threads, len(pts))
+
+        def run(nt):
+            return helpers.oracle_time_pixels(SCENE, WIDTH, HEIGHT, DEPTH, ao, pts, threads=nt, root=root,
+                                              faithful=True)
+        sample = ("%s %dx%d depth=%d AO=%d: %d pixel(s) of the full-resolution frame on a stratified grid "
+                  "(RNG at an estimated draw offset: same work per pixel, not the frame's exact bytes)%s"
+                  % (SCENE, WIDTH, HEIGHT, DEPTH, ao, len(pts),
+                     "" if ao == AO else "; AO %d instead of %d (CPU cost per ray is independent of the ray's "
+                     "kind: the reference tests every primitive per ray)" % (ao, AO)))
+    else:
+        w, h, depth, ao = CPU_SAMPLE
+
+        def run(nt):
+            return helpers.oracle_render(SCENE, w, h, depth, ao, True, threads=nt, root=root, faithful=True)[1]
+        sample = ("%s %dx%d depth=%d AO=%d (a downscaled frame of the workload, %.4g%% of its pixels)"
+                  % (SCENE, w, h, depth, ao, 100.0 * w * h / (WIDTH * HEIGHT)))
     t0 = time.perf_counter()
-    _, cnt = helpers.oracle_render(SCENE, w, h, depth, ao, True, threads=1, root=root, faithful=True)
+    cnt = run(1)
     secs1 = time.perf_counter() - t0
     rays = cnt["rays_total"]
-    t0 = time.perf_counter()
-    helpers.oracle_render(SCENE, w, h, depth, ao, True, threads=threads, root=root, faithful=True)
-    secsn = time.perf_counter() - t0
+    secsn = secs1
+    if threads > 1:
+        t0 = time.perf_counter()
+        run(threads)
+        secsn = time.perf_counter() - t0
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -392,10 +426,9 @@ def cpu_baseline(lib, rt580, helpers, root):
         "rays": rays,
         "all_cores": {"value": float("%.4g" % (rays / secsn / 1e6)), "cores": threads, "seconds": round(secsn, 3)},
         "cpu": cpu,
-        "sample": "%s %dx%d depth=%d AO=%d (a downscaled frame of the workload, %.4g%% of its pixels), "
-                  "oracle/rt_oracle.cpp in ref-faithful mode (same bytes as the reference; its cost model "
-                  "checked against the reference binary in the build container, DESIGN.md)"
-                  % (SCENE, w, h, depth, ao, 100.0 * w * h / (WIDTH * HEIGHT)),
+        "sample": sample + ", oracle/rt_oracle.cpp in ref-faithful mode (the reference's arithmetic and "
+                  "per-call work; its cost model checked against the reference binary in the build container, "
+                  "DESIGN.md)",
     }
 
 

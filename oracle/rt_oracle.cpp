@@ -841,6 +841,65 @@ extern "C" int oracle_render(const char* assets_root, const char* scene, int w, 
     return 0;
 }
 
+// CPU-baseline timing (bench.py cpu_baseline): Raycast of n listed pixels of the
+// FULL-resolution w x h frame (xy = x0, y0, x1, y1, ...), the reference's per-pixel
+// work (Raytracer.cpp:916-935) on a stratified sample of the workload's own rays.
+// The RNG is positioned at draw 2*ao_n*(y*w + x) (one AO call per earlier pixel):
+// the exact offset would need the whole frame's count pass, and only the position
+// in the draw stream differs (the sample's cost, not its bytes, is measured).
+// Pixels are work items over `threads` threads; counters as oracle_render.
+extern "C" int oracle_time_pixels(const char* assets_root, const char* scene, int w, int h, int depth,
+                                  int ao_samples, int threads, int n, const int32_t* xy, uint64_t* counters) {
+    if (w <= 0 || h <= 0 || depth < 0 || ao_samples <= 0 || n < 0) return 2;
+    for (int i = 0; i < n; i++)
+        if (xy[2 * i] < 0 || xy[2 * i] >= w || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= h) return 2;
+    Scene sc;
+    if (load_scene(sc, assets_root, scene) != 0) return 1;
+    for (const Shape& s : sc.shapes)
+        if (s.mesh < 0) return 1;
+    Camera2 cam = init_camera(sc, w, h);
+    Tracer tr;
+    tr.sc = &sc;
+    tr.depth = depth;
+    tr.ao_n = ao_samples;
+    tr.ao_on = 1;
+    tr.ao_bmax = (float)(2 * kPI);
+    tr.n_amb = 0;
+    for (auto& l : sc.lights) tr.n_amb += l.type == LAMB;
+    if (threads <= 0) threads = default_threads();
+    DrawSource src;
+    src.engine = 0;
+    std::vector<Counters> pc((size_t)n);
+    std::atomic<int> next{0};
+    auto work = [&] {
+        RngCursor rng;
+        rng.src = &src;
+        for (;;) {
+            const int i = next.fetch_add(1);
+            if (i >= n) break;
+            const int x = xy[2 * i], y = xy[2 * i + 1];
+            rng.seek(2ull * (uint64_t)ao_samples * ((uint64_t)y * w + x));
+            Counters& c = pc[(size_t)i];
+            c.primary++;
+            (void)tr.raycast(generate_ray(cam, x, y), depth, &rng, c, false);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    Counters tot;
+    for (const Counters& c : pc) {
+        tot.primary += c.primary; tot.secondary += c.secondary; tot.shadow += c.shadow;
+        tot.ao += c.ao; tot.ao_calls += c.ao_calls;
+    }
+    if (counters) {
+        counters[0] = tot.primary + tot.secondary + tot.shadow + tot.ao;
+        counters[1] = tot.primary; counters[2] = tot.secondary; counters[3] = tot.shadow;
+        counters[4] = tot.ao; counters[5] = tot.ao_calls;
+    }
+    return 0;
+}
+
 // ---- row-level entry points (the multi-rank split of SURVEY §8e, for tests) ----
 namespace {
 struct Loaded {

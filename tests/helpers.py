@@ -149,6 +149,24 @@ def oracle_render(scene, w, h, depth, ao_samples=128, ao_enabled=True, engine=0,
     return fb, dict(zip(keys, (int(x) for x in cnt)))
 
 
+def oracle_time_pixels(scene, w, h, depth, ao_samples, pixels, threads=0, root=ASSETS_ROOT, faithful=True):
+    """CPU-baseline timing: Raycast of the listed (x, y) pixels of the full w x h
+    frame (oracle_time_pixels; RNG at an estimated offset) -> counters dict."""
+    lib = oracle_lib()
+    lib.oracle_time_pixels.restype = ctypes.c_int
+    lib.oracle_time_pixels.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 6 + \
+        [ctypes.c_void_p, ctypes.c_void_p]
+    xy = np.asarray(pixels, dtype=np.int32).reshape(-1)
+    cnt = np.zeros(6, dtype=np.uint64)
+    lib.oracle_set_mode(1 if faithful else 0)
+    st = lib.oracle_time_pixels(os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples, threads,
+                                len(xy) // 2, xy.ctypes.data, cnt.ctypes.data)
+    lib.oracle_set_mode(0)
+    assert st == 0, "oracle_time_pixels failed"
+    keys = ["rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"]
+    return dict(zip(keys, (int(x) for x in cnt)))
+
+
 @functools.lru_cache(None)
 def rt580_dist():
     spec = importlib.util.spec_from_file_location("rt580_dist", os.path.join(PKG, "rt580_dist.py"))

@@ -6,6 +6,7 @@
 #include "../../580-raytracer_amd/csrc/rt_isect.h"
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -17,14 +18,18 @@ static inline int32_t cvttss2si(float f) {
 }
 
 int main() {
-    std::atomic<long> bad{0};
+    // RT_STRIDE=k: only the bit patterns u with u % k == 0 (the CPU suite's quick
+    // default; RT580_EXHAUSTIVE=1 runs k = 1)
+    const char* se = std::getenv("RT_STRIDE");
+    const uint64_t st = se && std::atol(se) > 1 ? (uint64_t)std::atol(se) : 1;
+    std::atomic<long> bad{0}, checked{0};
     unsigned nt = std::thread::hardware_concurrency();
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; t++)
         th.emplace_back([&, t] {
-            long b = 0;
+            long b = 0, n = 0;
             uint64_t lo = (1ull << 32) * t / nt, hi = (1ull << 32) * (t + 1) / nt;
-            for (uint64_t u = lo; u < hi; u++) {
+            for (uint64_t u = (lo + st - 1) / st * st; u < hi; u += st, n++) {
                 uint32_t v = (uint32_t)u;
                 float x;
                 std::memcpy(&x, &v, 4);
@@ -42,8 +47,9 @@ int main() {
                     if (rt580::quot_lt0(x, den) != ((x / den) < 0.0f)) b++;
             }
             bad += b;
+            checked += n;
         });
     for (auto& x : th) x.join();
-    std::printf("mismatches=%ld\n", bad.load());
+    std::printf("mismatches=%ld checked=%ld\n", bad.load(), checked.load());
     return bad.load() ? 1 : 0;
 }

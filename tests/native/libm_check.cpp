@@ -16,6 +16,14 @@
 #include <random>
 
 static std::atomic<long> g_bad{0}, g_checked{0};
+
+// RT_STRIDE=k: only the inputs u with u % k == 0 (the quick default of the CPU
+// suite; k = 1, the exhaustive run, with RT580_EXHAUSTIVE=1)
+static uint64_t stride() {
+    const char* e = std::getenv("RT_STRIDE");
+    const long k = e ? std::atol(e) : 1;
+    return k > 1 ? (uint64_t)k : 1;
+}
 static std::atomic<int> g_printed{0};
 
 static void report(const char* what, double in1, double in2, double got, double want) {
@@ -61,13 +69,14 @@ int main(int argc, char** argv) {
             float y = std::strtof(argv[i], nullptr);
             uint32_t hi = rt_f2u(1.0001f) + 1;
             parallel(hi, [y](uint64_t lo, uint64_t hi) {
-                long bad = 0;
-                for (uint64_t u = lo; u < hi; u++) {
+                long bad = 0, n = 0;
+                const uint64_t st = stride();
+                for (uint64_t u = (lo + st - 1) / st * st; u < hi; u += st, n++) {
                     float x = rt_u2f((uint32_t)u);
                     float r0 = powf(x, y), r1 = rt_glibc_powf(x, y);
                     if (rt_f2u(r0) != rt_f2u(r1)) { bad++; report("powf", x, y, r1, r0); }
                 }
-                g_bad += bad; g_checked += (long)(hi - lo);
+                g_bad += bad; g_checked += n;
             });
         }
     } else if (!std::strcmp(argv[1], "powf_random")) {

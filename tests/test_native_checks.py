@@ -22,8 +22,21 @@ def _build(name, extra=()):
     return exe
 
 
-def _run(exe, *args):
-    p = subprocess.run([exe] + list(args), capture_output=True, text=True, timeout=600)
+# The two largest sweeps (powf over 23 exponents x 1.07e9 floats, all 2^32 floats
+# for the EPSILON/short checks: ~4 min on 8 cores) take every STRIDE-th input by
+# default; RT580_EXHAUSTIVE=1 runs them over every input (DESIGN.md records the
+# exhaustive runs).
+EXHAUSTIVE = os.environ.get("RT580_EXHAUSTIVE", "") not in ("", "0")
+STRIDE = 1 if EXHAUSTIVE else 11
+
+
+def _n_strided(n):
+    """inputs u in [0, n) with u % STRIDE == 0"""
+    return (n + STRIDE - 1) // STRIDE
+
+
+def _run(exe, *args, env=None):
+    p = subprocess.run([exe] + list(args), capture_output=True, text=True, timeout=1800, env=env)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "mismatches=0" in p.stdout
     return p.stdout
@@ -50,8 +63,8 @@ def test_powf_exhaustive_over_scene_exponents():
     3-5 (Raytracer.cpp:253; fmax(dot(V,R),0) of unit vectors)."""
     exps = helpers.scene_exponents()
     assert {2.0, 5.0, 64.0, 120.0, 900.0} <= set(exps) and len(exps) >= 20
-    out = _run(_build("libm_check"), "powf", *["%r" % e for e in exps])
-    assert "checked=%d" % (len(exps) * (0x3f800347 + 1)) in out, out
+    out = _run(_build("libm_check"), "powf", *["%r" % e for e in exps], env=dict(os.environ, RT_STRIDE=str(STRIDE)))
+    assert "checked=%d" % (len(exps) * _n_strided(0x3f800347 + 1)) in out, out
 
 
 def test_powf_random_pairs():
@@ -59,7 +72,8 @@ def test_powf_random_pairs():
 
 
 def test_eps_compares_and_float_to_short_all_floats():
-    _run(_build("eps_check"))
+    out = _run(_build("eps_check"), env=dict(os.environ, RT_STRIDE=str(STRIDE)))
+    assert "checked=%d" % _n_strided(1 << 32) in out, out
 
 
 CSRC = os.path.join(helpers.PKG, "csrc")

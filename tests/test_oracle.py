@@ -64,3 +64,15 @@ def test_scene_fixtures_are_the_reference_assets():
     ref = os.path.join(helpers.REFERENCE, "Assets")
     for f in os.listdir(ref):
         assert filecmp.cmp(os.path.join(ref, f), os.path.join(helpers.GOLDEN, "Assets", f), shallow=False), f
+
+
+def test_time_pixels_counts_the_frames_rays():
+    """bench.py's CPU-baseline sampler (oracle_time_pixels: listed pixels of the
+    full frame) traces exactly the rays oracle_render traces for those pixels,
+    in both cost modes (only the RNG position differs, not the work)."""
+    w, h = 24, 18
+    _, want = helpers.oracle_render("simpleSphereScene.json", w, h, 4, 8, True)
+    pts = [(x, y) for y in range(h) for x in range(w)]
+    for faithful in (False, True):
+        got = helpers.oracle_time_pixels("simpleSphereScene.json", w, h, 4, 8, pts, threads=4, faithful=faithful)
+        assert got == want
