@@ -776,6 +776,11 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
         if (attempt == 3) return fail("node capacity could not be sized");
         if (g.profiling) g.prof_frames--;
     }
+    // The counts go into the caller's buffer, which the caller may have just
+    // allocated or cleared on its stream (after the mark begin_slot waited on):
+    // the copy waits for the caller's stream as it is now; the trace above
+    // still overlaps the caller's earlier work (e.g. the previous frame's shading).
+    if (slot_wait_user()) return RT_FAILURE;
     if (n_rows)
         HIP_TRY(hipMemcpyAsync(row_calls_device, SL.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToDevice,
                                fs()));

@@ -94,12 +94,21 @@ def stdout_to_stderr():
 
 
 def main():
+    # stdout carries exactly one JSON line: everything else written to fd 1 (the
+    # drop-in's "Scene parsing completed!", RCCL's version banner at communicator
+    # init) goes to stderr; the JSON line goes to the saved original stdout
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default 20 (config2), 2 (synthetic)")
     ap.add_argument("--warmup", type=int, default=None, help="default 3 (config2), 1 (synthetic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--dist", action="store_true",
+                    help="the multi-rank path (torch.distributed + DistFrame) even with one rank: rehearses the "
+                         "RCCL all-gather/gather and the per-frame host overhead of N>1 on one GPU")
     ap.add_argument("--check", action="store_true", help="verify the frame against the golden sha256 (config2)")
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     ap.add_argument("--row-sample", type=int, default=1,
@@ -123,8 +132,10 @@ def main():
     local_rank = env_int("LOCAL_RANK", 0) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
+    dist_on = world > 1 or args.dist
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29581")
         if args.backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
         else:
@@ -150,9 +161,9 @@ def main():
     n_tri = sum(1 for p in prims if p.kind == 0)
 
     fbp = ctypes.c_void_p()
-    K = max(args.row_sample, 1) if world == 1 else 1
-    dist_mod = helpers.rt580_dist() if (world > 1 or K > 1) else None
-    backend = dist_mod.GpuRows(rt580, params, torch, device) if (world > 1 or K > 1) else None
+    K = max(args.row_sample, 1) if not dist_on else 1
+    dist_mod = helpers.rt580_dist() if (dist_on or K > 1) else None
+    backend = dist_mod.GpuRows(rt580, params, torch, device) if (dist_on or K > 1) else None
     sample_base = None
     if K > 1:
         # exact global RNG bases: every row's AO-call count, once, outside the timed region
@@ -166,13 +177,13 @@ def main():
     # steady-state multi-rank frames (RCCL): persistent buffers, async gather
     # overlapped with the next frame; gloo (rehearsal) uses the plain form
     dframe = dist_mod.DistFrame(backend, dist, torch, HEIGHT, WIDTH, rank, world, device) \
-        if (world > 1 and args.backend == "nccl") else None
+        if (dist_on and args.backend == "nccl") else None
 
     def step():
         if K > 1:
             backend.count(0, K)
             return backend.shade(0, K, sample_base)
-        if world == 1:
+        if not dist_on:
             rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(fbp)), "rt_gpu_render_device")
             return None
         if dframe is not None:
@@ -184,7 +195,7 @@ def main():
         return dframe.finish() if dframe is not None else None
 
     def barrier():
-        if world > 1:
+        if dist_on:
             dist.barrier()
 
     frame = None
@@ -200,7 +211,7 @@ def main():
     if args.check and rank == 0:
         # the frame of the (last warm-up) step vs the reference's config-2 hash
         import numpy as np
-        if world == 1:
+        if not dist_on:
             host = np.zeros(WIDTH * HEIGHT * 3, dtype=np.int16)
             rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
             frame_np = host.reshape(HEIGHT, WIDTH, 3)
@@ -272,7 +283,8 @@ def main():
                 "scene": SCENE, "width": WIDTH, "height": HEIGHT, "depth": DEPTH, "ao_samples": AO,
                 "rng": "minstd_rand0 (libstdc++ default_random_engine)",
                 "rays_per_frame": rays_frame,
-                "parallelism": "interleaved rows x%d + RCCL all_gather/gather" % world if world > 1 else "1 GPU",
+                "parallelism": ("interleaved rows x%d + %s all_gather/gather" % (world, "RCCL" if args.backend == "nccl"
+                                else args.backend)) if dist_on else "1 GPU",
                 "row_sample": ("rows r = 0 mod %d only (the exact pixels of rank 0 in a %d-way interleaved split; "
                                "RNG bases from a full-frame count outside the timed region); value and "
                                "rays_per_frame refer to the sample" % (K, K)) if K > 1 else None,
@@ -292,12 +304,12 @@ def main():
         # small-scene frame is one launch over all of its AO rays
         k_units = k_rays.value if k_rays.value else int(local["rays_ao"]) * max(frames.value, 1)
         out["roofline"] = roofline(args.workload, k_ms.value, k_launches.value, k_units, int(local["rays_ao"]))
-        if world == 1 and K == 1:
+        if not dist_on and K == 1:
             out["render_call_ms"] = render_latency(lib, rt580, params, torch)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(lib, rt580, helpers, root)
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        print(json.dumps(out), file=json_out, flush=True)
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 
