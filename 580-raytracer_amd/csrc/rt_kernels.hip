@@ -1980,6 +1980,18 @@ static int grid_for(uint64_t items, int cap) {
     return (int)(b < (uint64_t)cap ? b : (uint64_t)cap);
 }
 
+// Workgroups of a recursion level > 0 (trace and resolve; grid-stride over the
+// level's count, which only the device knows): RT580_DEEP_GRID for A/B.
+static int deep_grid() {
+    static int g = -1;
+    if (g < 0) {
+        const char* e = getenv("RT580_DEEP_GRID");
+        g = e ? atoi(e) : 512;  // 4096 / 1024 / 512: config 2 1.562 / 1.561 / 1.550 ms, its 8-way share 0.324 / 0.323 / 0.319
+        if (g < 64 || g > 65536) g = 512;
+    }
+    return g;
+}
+
 // Candidates in flight per lane in far_any_kernel's per-lane list walk
 // (RT580_FAR_U = 1, 2, 4).
 static void launch_far_any(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s) {
@@ -2376,7 +2388,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
             continue;
         }
         // level 0 has exactly npix rays; deeper levels read their count on the device
-        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, 4096);
+        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, deep_grid());
         if (S.use_bvh) hipLaunchKernelGGL((trace_kernel<true, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
         else if (S.n_prims <= TILE && trace_scalar())
             hipLaunchKernelGGL((trace_kernel<false, 0, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
@@ -2609,7 +2621,7 @@ hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W
         return hipGetLastError();
     }
     for (int level = F.depth; level >= 0; level--) {
-        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, 4096);
+        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, deep_grid());
         hipLaunchKernelGGL(resolve_level_kernel, dim3(grid), dim3(TB), 0, s, S, F, W, level, fb);
     }
     return hipGetLastError();

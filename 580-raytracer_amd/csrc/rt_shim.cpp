@@ -776,15 +776,15 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
         if (attempt == 3) return fail("node capacity could not be sized");
         if (g.profiling) g.prof_frames--;
     }
+    if (end_slot()) return RT_FAILURE;  // the caller's stream waits for the count pass
     // The counts go into the caller's buffer, which the caller may have just
-    // allocated or cleared on its stream (after the mark begin_slot waited on):
-    // the copy waits for the caller's stream as it is now; the trace above
-    // still overlaps the caller's earlier work (e.g. the previous frame's shading).
-    if (slot_wait_user()) return RT_FAILURE;
+    // allocated or cleared on its own stream (after the mark begin_slot waited
+    // on): the copy is queued on the caller's stream, behind that work and the
+    // count pass. The slot's next frame (two calls on) waits for this call's
+    // copy through the user mark of the next call's start (begin_slot).
     if (n_rows)
         HIP_TRY(hipMemcpyAsync(row_calls_device, SL.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToDevice,
-                               fs()));
-    if (end_slot()) return RT_FAILURE;  // the caller's stream (all-gather) sees the counts
+                               g.stream));
     g.split_params = *p;
     g.split_ready = true;
     return RT_SUCCESS;

@@ -227,8 +227,11 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_s = 0.0  # host time inside step(): the enqueue cost of a frame (its kernels run asynchronously)
     for i in range(args.steps):
+        th = time.perf_counter()
         step()
+        host_s += time.perf_counter() - th
         if i == args.steps - 1:
             finish()  # the last frame's gather + de-interleave belong to the timed region
         if SYNTH:  # long frames: keep a progress line per step (sync costs microseconds)
@@ -291,6 +294,7 @@ def main():
                 "scene_query": "exact BVH + plane tree (rt_bvh.h)" if lib.rt_gpu_accel_active() else
                                "brute force (every primitive per ray, as the reference)",
             },
+            "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "kernel_ms_per_frame": {
                 "trace": round(per_frame[0], 4),
                 "rank": round(per_frame[1], 4),
