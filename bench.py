@@ -49,15 +49,15 @@ HBM_PEAK_GBS = 8000.0
 #                      primitive for every ray, Raytracer.cpp:476-521, so its cost
 #                      per ray does not depend on the ray's kind).
 WORKLOADS = {
-    "config2": ("simpleSphereScene.json", False, 1920, 1080, 4, 64, (480, 270, 4, 64),
+    "config2": ("simpleSphereScene.json", False, 1920, 1080, 4, 64, (640, 360, 4, 64),
                 "BASELINE config 2: simpleSphereScene.json 1920x1080 depth=4 AO=64"),
-    "cornell10k": ("cornell10k.json", True, 1920, 1080, 4, 64, ("pixels", 16),
+    "cornell10k": ("cornell10k.json", True, 1920, 1080, 4, 64, ("pixels", 64),
                    "BASELINE config 3: 10k-triangle Cornell box 1920x1080 depth=4 AO=64"),
-    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64, ("pixels", 8),
+    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64, ("pixels", 32),
                         "north_star target: 100k-triangle field 1920x1080 depth=4 AO=64"),
     "field100k": ("field100k.json", True, 3840, 2160, 6, 256, ("pixels", 2),
                   "BASELINE config 4: 100k-triangle field 3840x2160 depth=6 AO=256"),
-    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, ("pixels", 1, 16),
+    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, ("pixels", 1, 8),
                 "BASELINE config 5: 1M-triangle field 7680x4320 depth=8 AO=256"),
 }
 
