@@ -644,6 +644,25 @@ RTM_HD bool bvh4_any_near_s(const BvhView& V, rv3 o, rv3 d, const STK& stk, floa
     }
 }
 
+// bvh4_any_near_s with at most `budget` leaf visits (descent to a leaf + its
+// tests): 1 hit, 0 no hit, -1 undecided (the caller runs the full query later;
+// the boolean does not depend on the order or the split of the visits).
+template <class STK>
+RTM_HD int bvh4_any_near_budget(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget) {
+    for (int k = 0; k < V.n_brute; k++)
+        if (prim_hit_within(V.all[V.brute[k]], o, d, INFINITY)) return 1;
+    if (!V.has_tree || dir_zero(d)) return 0;
+    const SlabRay sr = slab_ray(V, o, d);
+    int sp = 0;
+    int32_t c = 0, n = 0;  // root (internal)
+    for (int visits = 0;; visits++) {
+        if (visits == budget) return -1;
+        if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, n)) return 0;
+        if (bvh4_leaf_hit(V, o, d, INFINITY, c, n)) return 1;
+        if (!bvh4_pop(stk, sp, c, n)) return 0;
+    }
+}
+
 RTM_HD bool bvh4_any_near(const BvhView& V, rv3 o, rv3 d, float tmax = INFINITY) {
     RT_CNT(brute_tests, V.n_brute);
     for (int k = 0; k < V.n_brute; k++)

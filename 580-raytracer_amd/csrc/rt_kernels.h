@@ -102,6 +102,10 @@ struct DevWork {
     // split AO pass (ao_trace_kernel): (o.xyz, call), (d.xyz, flag) per item of a chunk
     float4* ao_rays;       // [2 * ao_cap] or null
     uint32_t ao_cap;
+    // AO rays of a chunk whose near traversal ran out of its step budget in
+    // ao_trace_kernel (item index in the chunk), finished by ao_late_kernel
+    uint32_t* ao_late;       // [ao_cap] or null
+    uint32_t* ao_late_count; // [1]
     // provisional closest hits of the tree rays (node id) between the near and
     // far phases of a BVH trace level: (t, alpha, beta, gamma), prim (-1: none)
     float4* hit4;          // [node_cap]

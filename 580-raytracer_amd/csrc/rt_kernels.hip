@@ -1189,7 +1189,10 @@ ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
 // counting sort by octahedral direction cell (8 x 8): a wave then holds rays
 // of similar direction from nearby origins, which share more of their paths
 // (tools/simd_sim.cpp "block sort"). Hits are then counted per lane.
-template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3>
+// BUDGET > 0: a lane gives up after BUDGET leaf visits; its item goes to
+// W.ao_late (ao_late_kernel re-runs the full query), so a wave is not held by
+// its few long traversals (tools/simd_sim.cpp "budget").
+template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
@@ -1245,8 +1248,22 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
         const uint32_t flag = __float_as_uint(r1.w);
         const bool active = flag != 0u, ao_brute = flag == 2u;
         const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
-        bool hit;
-        if (LDS_D > 0) {
+        bool hit, late = false;
+        if (BUDGET > 0 && LDS_D > 0) {
+            uint32_t stk_a[RT_BVH_STACK + 4 - (LDS_D > 0 ? LDS_D : 0)];
+            const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
+            const int r = flag == 1u ? bvh4_any_near_budget(S.bv, o, d, stk, BUDGET) : 0;
+            hit = r > 0;
+            late = r < 0;
+            const uint64_t lm = __ballot(late);
+            if (lm) {
+                const int leader = __ffsll((unsigned long long)lm) - 1;
+                uint32_t base = 0;
+                if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count, (uint32_t)__popcll(lm));
+                base = __shfl(base, leader);
+                if (late) W.ao_late[base + (uint32_t)__popcll(lm & lanemask_lt())] = (uint32_t)i;
+            }
+        } else if (LDS_D > 0) {
             uint32_t stk_a[RT_BVH_STACK + 4 - (LDS_D > 0 ? LDS_D : 0)];
             const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
             hit = flag == 1u && bvh4_any_near_s(S.bv, o, d, stk);
@@ -1254,7 +1271,33 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
             hit = flag == 1u && bvh4_any_near(S.bv, o, d);
         }
         // sorted: a wave's lanes are no longer one call's samples
-        ao_finish<true>(S, W, SORT > 0 ? 1u : N, active, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o, d);
+        ao_finish<true>(S, W, SORT > 0 ? 1u : N, active && !late, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o,
+                        d);
+    }
+}
+
+// The chunk's AO rays that ran out of ao_trace_kernel's step budget: the full
+// near query, then the same bookkeeping (hits counted per call, misses queued
+// for the far pass). Grid-stride over the device-side count.
+template <int WPE, int LDS_D>
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
+ao_late_kernel(DevScene S, DevWork W) {
+    __shared__ uint32_t lstk[LDS_D][TB];
+    const uint32_t cnt = *W.ao_late_count;
+    for (uint32_t b0 = blockIdx.x * TB; b0 < cnt; b0 += gridDim.x * TB) {
+        const uint32_t k = b0 + threadIdx.x;
+        const bool live = k < cnt;
+        float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
+        if (live) {
+            const uint32_t i = W.ao_late[k];
+            r0 = W.ao_rays[2 * (size_t)i];
+            r1 = W.ao_rays[2 * (size_t)i + 1];
+        }
+        const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
+        uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
+        const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
+        const bool hit = live && bvh4_any_near_s(S.bv, o, d, stk);
+        ao_finish<true>(S, W, 1u, live, false, hit, (uint64_t)__float_as_uint(r0.w), o, d);
     }
 }
 
@@ -1309,6 +1352,18 @@ static int ao_sort() {
         // 1: 1024 / 8 x 8 50.6 / 79.4; 2: 2048 / 8 x 8 49.4; 4096 samples
         // lose occupancy: 59.1 / 88.4)
         v = e ? atoi(e) : 3;
+    }
+    return v;
+}
+
+// RT580_AO_BUDGET: leaf visits per AO ray in ao_trace_kernel before the ray is
+// left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
+// 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
+static int ao_budget() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_BUDGET");
+        v = e ? atoi(e) : 4;
     }
     return v;
 }
@@ -2485,7 +2540,27 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 else if (twpe == 6 && trace_lds() && so == 2)  // 2048 samples, 8 x 8 cells
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
-                else if (twpe == 6 && trace_lds() && so == 3)  // 2048 samples, 16 x 16 cells (default)
+                else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
+                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 4, s)) != hipSuccess) return e;
+                    const int bu = ao_budget();
+                    if (bu <= 2)
+                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 2>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
+                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
+                    else if (bu == 3)
+                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 3>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
+                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
+                    else if (bu == 5 || bu == 6)
+                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 6>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
+                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
+                    else if (bu <= 4)
+                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
+                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
+                    else
+                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
+                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
+                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                    hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
+                } else if (twpe == 6 && trace_lds() && so == 3)  // 2048 samples, 16 x 16 cells (default)
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S,
                                        W, (uint32_t)F.ao_samples, e1 - b);
                 else if (twpe == 6 && trace_lds())  // 16-entry LDS stacks (default)

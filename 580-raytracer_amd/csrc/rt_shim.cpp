@@ -79,7 +79,7 @@ struct State {
     std::array<hipEvent_t, 16> stage_ev{};
     bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
     // BVH far-queue buffers (BVH frames always run serialized on slot 0)
-    DevBuf ao_rays;
+    DevBuf ao_rays, ao_late, ao_late_count;
     DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim, shadow;
     uint32_t* far_count_host = nullptr;  // pinned
     uint32_t far_cap = 0;
@@ -352,6 +352,8 @@ DevWork dev_work() {
     w.far_cap = g.far_cap;
     w.ao_rays = g.ao_cap ? (float4*)g.ao_rays.p : nullptr;
     w.ao_cap = g.ao_cap;
+    w.ao_late = g.ao_cap ? (uint32_t*)g.ao_late.p : nullptr;
+    w.ao_late_count = g.ao_cap ? (uint32_t*)g.ao_late_count.p : nullptr;
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
     w.hit4 = split ? (float4*)g.hit4.p : nullptr;
     w.hit_prim = split ? (int32_t*)g.hit_prim.p : nullptr;
@@ -425,7 +427,8 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     // ray records of the split AO pass (ao_trace_kernel), one chunk
     if (g.bvh_ok && g.ao_cap == 0) {
         const uint32_t ac = 1u << 26;
-        if (ensure(g.ao_rays, (size_t)ac * 32)) return RT_FAILURE;
+        if (ensure(g.ao_rays, (size_t)ac * 32) || ensure(g.ao_late, (size_t)ac * 4) || ensure(g.ao_late_count, 64))
+            return RT_FAILURE;
         g.ao_cap = ac;
     }
     if (g.bvh_ok && !g.bvh.far_nodes.empty() &&
@@ -935,7 +938,7 @@ void shutdown_ctx() {
     for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always})
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
-                      &g.ao_rays, &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
+                      &g.ao_rays, &g.ao_late, &g.ao_late_count, &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
                       &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.shadow})
         release(*b);
     for (Slot& sl : g.slot) {

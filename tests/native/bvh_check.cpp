@@ -199,6 +199,13 @@ int main(int argc, char** argv) {
                     if (a2 != a4 || bvh_any(V, o, d, false, tb) != bvh4_any_near(V, o, d, tb)) {
                         if (bad4.fetch_add(1) < 10) std::printf("MISMATCH4 ray %ld kind %d: binary %d 4-wide %d\n", r, kind, a2, a4);
                     }
+                    // ao_trace_kernel's step budget: a decided answer equals the full query's
+                    for (int budget : {1, 2, 4, 8}) {
+                        uint32_t sa[RT_BVH_STACK + 4];
+                        const int q = bvh4_any_near_budget(V, o, d, ArrStack{sa}, budget);
+                        if (q >= 0 && (q == 1) != a4 && bad4.fetch_add(1) < 10)
+                            std::printf("MISMATCH4 budget %d ray %ld kind %d: %d vs %d\n", budget, r, kind, q, a4);
+                    }
                     Hit h2, h4;
                     const bool c2 = bvh_closest(V, o, d, h2, false), c4 = bvh4_closest_near(V, o, d, h4);
                     if (c2 != c4 || (c2 && (h2.prim != h4.prim || fbits(h2.t) != fbits(h4.t) || fbits(h2.a) != fbits(h4.a) ||

@@ -222,6 +222,59 @@ int main(int argc, char** argv) {
                         ln / 64.0 / cn, lt / 64.0 / ct, cn / nw, ct / nw);
         }
     }
+    // step budget K, then compaction: lanes run at most K steps in the first
+    // pass; the unfinished rays (queued in order) run in a second pass, either
+    // resumed (stack saved) or restarted from the root (redo their K steps)
+    for (int K : {4, 8, 16, 32}) {
+        std::mt19937 r4(argc > 4 ? std::atoi(argv[4]) : 580);
+        std::vector<std::vector<Step>> all;
+        all.reserve(waves * 64);
+        for (long w = 0; w < waves; w++) {
+            const rt_prim& T = P[tris[r4() % tris.size()]];
+            float u = U(r4), v = U(r4);
+            if (u + v > 1) { u = 1 - u; v = 1 - v; }
+            const rv3 p0 = ld3(T.p0), p1 = ld3(T.p1), p2 = ld3(T.p2), N = v3_normalize(ld3(T.nrm));
+            const rv3 hp = v3_add(p0, v3_add(v3_scale(v3_sub(p1, p0), u), v3_scale(v3_sub(p2, p0), v)));
+            for (int l = 0; l < 64; l++) {
+                const float z = U(r4) * 2 - 1, a = U(r4) * 6.2831853f, r = std::sqrt(1 - z * z);
+                rv3 d = v3_normalize(v3(r * std::cos(a), r * std::sin(a), z));
+                if (!(v3_dot(d, N) > 0.0f)) d = v3_neg(d);
+                const rv3 o = v3_add(hp, v3_scale(d, 0.2f));
+                std::vector<Step> st;
+                trace(V, o, d, st);
+                all.push_back(st);
+            }
+        }
+        auto wave_cost = [&](const std::vector<const std::vector<Step>*>& ws, size_t from, size_t lim, double& cn,
+                             double& ct) {
+            size_t maxs = 0;
+            for (auto* x : ws) maxs = std::max(maxs, std::min(x->size(), lim));
+            for (size_t i = from; i < maxs; i++) {
+                int mn = 0, mt = 0;
+                for (auto* x : ws)
+                    if (i < x->size() && i < lim) { mn = std::max(mn, (*x)[i].nodes); mt = std::max(mt, (*x)[i].tris); }
+                cn += mn; ct += mt;
+            }
+        };
+        double c1n = 0, c1t = 0, cRn = 0, cRt = 0, cSn = 0, cSt = 0, base_n = 0, base_t = 0;
+        std::vector<const std::vector<Step>*> late;
+        for (size_t w0 = 0; w0 < all.size(); w0 += 64) {
+            std::vector<const std::vector<Step>*> ws;
+            for (size_t l = w0; l < w0 + 64; l++) ws.push_back(&all[l]);
+            wave_cost(ws, 0, (size_t)-1, base_n, base_t);
+            wave_cost(ws, 0, (size_t)K, c1n, c1t);
+            for (auto* x : ws) if (x->size() > (size_t)K) late.push_back(x);
+        }
+        for (size_t w0 = 0; w0 < late.size(); w0 += 64) {
+            std::vector<const std::vector<Step>*> ws(late.begin() + w0, late.begin() + std::min(late.size(), w0 + 64));
+            wave_cost(ws, 0, (size_t)-1, cRn, cRt);        // restart: all steps again
+            wave_cost(ws, (size_t)K, (size_t)-1, cSn, cSt); // resume: steps K..
+        }
+        std::printf("budget K=%d: late rays %.3f | lock-step nodes+tris: base %.0f, resume %.0f (%.3f), restart %.0f (%.3f)\n",
+                    K, late.size() / (double)all.size(), base_n + base_t, c1n + c1t + cSn + cSt,
+                    (c1n + c1t + cSn + cSt) / (base_n + base_t), c1n + c1t + cRn + cRt,
+                    (c1n + c1t + cRn + cRt) / (base_n + base_t));
+    }
     const double R = waves * 64.0;
     std::printf("rays=%.0f hit=%.3f per ray: nodes=%.2f tris=%.2f steps=%.2f | per wave (lock-step): nodes=%.1f tris=%.1f "
                 "steps=%.1f | node eff=%.3f tri eff=%.3f\n", R, hits / R, lane_nodes / R, lane_tris / R, lane_steps / R,
