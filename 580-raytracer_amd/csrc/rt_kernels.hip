@@ -1279,25 +1279,48 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
 // The chunk's AO rays that ran out of ao_trace_kernel's step budget: the full
 // near query, then the same bookkeeping (hits counted per call, misses queued
 // for the far pass). Grid-stride over the device-side count.
-template <int WPE, int LDS_D>
+// SRC: the queue read (0: ao_trace_kernel's, at W.ao_late; 1: this kernel's
+// own second level, at W.ao_late + ao_cap / 2). BUDGET2 > 0 (with SRC 0): a
+// second budget, the rays still undecided go to queue 1 for a last launch
+// (RT580_AO_BUDGET2, A/B); skipped when queue 0 fills more than half the buffer.
+template <int WPE, int LDS_D, int BUDGET2 = 0, int SRC = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_late_kernel(DevScene S, DevWork W) {
     __shared__ uint32_t lstk[LDS_D][TB];
-    const uint32_t cnt = *W.ao_late_count;
+    const uint32_t half = W.ao_cap / 2;
+    const uint32_t cnt = W.ao_late_count[SRC];
+    const uint32_t* q = W.ao_late + (SRC ? half : 0u);
+    const bool two = BUDGET2 > 0 && cnt <= half;
     for (uint32_t b0 = blockIdx.x * TB; b0 < cnt; b0 += gridDim.x * TB) {
         const uint32_t k = b0 + threadIdx.x;
         const bool live = k < cnt;
+        uint32_t i = 0;
         float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
         if (live) {
-            const uint32_t i = W.ao_late[k];
+            i = q[k];
             r0 = W.ao_rays[2 * (size_t)i];
             r1 = W.ao_rays[2 * (size_t)i + 1];
         }
         const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
         uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
         const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
-        const bool hit = live && bvh4_any_near_s(S.bv, o, d, stk);
-        ao_finish<true>(S, W, 1u, live, false, hit, (uint64_t)__float_as_uint(r0.w), o, d);
+        bool hit, late = false;
+        if (BUDGET2 > 0 && two) {
+            const int r = live ? bvh4_any_near_budget(S.bv, o, d, stk, BUDGET2) : 0;
+            hit = r > 0;
+            late = r < 0;
+            const uint64_t lm = __ballot(late);
+            if (lm) {
+                const int leader = __ffsll((unsigned long long)lm) - 1;
+                uint32_t base = 0;
+                if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count + 1, (uint32_t)__popcll(lm));
+                base = __shfl(base, leader);
+                if (late) W.ao_late[half + base + (uint32_t)__popcll(lm & lanemask_lt())] = i;
+            }
+        } else {
+            hit = live && bvh4_any_near_s(S.bv, o, d, stk);
+        }
+        ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w), o, d);
     }
 }
 
@@ -1364,6 +1387,17 @@ static int ao_budget() {
     if (v < 0) {
         const char* e = getenv("RT580_AO_BUDGET");
         v = e ? atoi(e) : 4;
+    }
+    return v;
+}
+
+// RT580_AO_BUDGET2=1 (A/B): ao_late_kernel itself stops after 16 leaf visits and
+// a third launch finishes the rest
+static int ao_budget2() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_BUDGET2");
+        v = e ? atoi(e) : 0;
     }
     return v;
 }
@@ -2541,7 +2575,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
                 else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
-                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 4, s)) != hipSuccess) return e;
+                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
                     const int bu = ao_budget();
                     if (bu <= 2)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 2>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
@@ -2559,7 +2593,12 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
-                    hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
+                    if (ao_budget2() > 0) {
+                        hipLaunchKernelGGL((ao_late_kernel<6, 16, 16, 0>), dim3(4096), dim3(TB), 0, s, S, W);
+                        hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 1>), dim3(1024), dim3(TB), 0, s, S, W);
+                    } else {
+                        hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
+                    }
                 } else if (twpe == 6 && trace_lds() && so == 3)  // 2048 samples, 16 x 16 cells (default)
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S,
                                        W, (uint32_t)F.ao_samples, e1 - b);
