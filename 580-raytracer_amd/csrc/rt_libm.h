@@ -42,11 +42,13 @@
 // same generated initialisers through a second, host-only definition.
 namespace rt_dev {
 #include "glibc_tables.inc"
+#include "sct128_table.inc"
 }
 namespace rt_host {
 #undef RT_TABLE_QUAL
 #define RT_TABLE_QUAL static const
 #include "glibc_tables.inc"
+#include "sct128_table.inc"
 }
 #if defined(__HIP_DEVICE_COMPILE__)
 #define RT_T(name) rt_dev::name
@@ -56,6 +58,7 @@ namespace rt_host {
 #else
 namespace rt_host {
 #include "glibc_tables.inc"
+#include "sct128_table.inc"
 }
 #define RT_T(name) rt_host::name
 #endif
@@ -325,10 +328,12 @@ RT_HD void rt_glibc_sincos(double x, double* sinx, double* cosx) {
 // AO hemisphere direction, x = (float)((double)r * cos(a)), y = (float)((double)r * sin(a))
 // (RandomUnitVector, Raytracer.cpp:277-278), fast path with an exact fallback.
 //
-// rt_fast_sincos: Cody-Waite reduction by pi/2 (k <= 4) and Taylor polynomials
-// (sin to x^13, cos to x^14; truncation < 2e-15 on |x| <= pi/4), Horner with
-// fma. Its distance from glibc's sincos is at most RT_AO_SC_ERR for every float
-// angle in [0, 2*pi) (exhaustive: tests/native/libm_check.cpp "aodir").
+// rt_fast_sincos: Cody-Waite reduction by pi/128 (k <= 256), a table of
+// sin/cos(k pi/128) (sct128_table.inc, correctly rounded, tools/gen_sct128.py)
+// and short Taylor polynomials of the remainder (|x| <= pi/256: sin to x^5,
+// truncation < 1e-17; cos to x^6, < 1e-19), combined by the angle-addition
+// formulas. Its distance from glibc's sincos is at most RT_AO_SC_ERR for every
+// float angle in [0, 2*pi) (exhaustive: tests/native/libm_check.cpp "aodir").
 //
 // Only the float rounding of r*cos(a) reaches the output. With r <= 1 and
 // E = RT_AO_SC_ERR, the reference's double product X_g and ours X_f differ by at
@@ -337,32 +342,19 @@ RT_HD void rt_glibc_sincos(double x, double* sinx, double* cosx) {
 // to the same f. Otherwise (rare: |r cos a| tiny) the lane takes glibc's exact
 // sincos (rt_glibc_sincos_simd_t).
 // ---------------------------------------------------------------------------
-#define RT_AO_SC_ERR 0x1p-44
+#define RT_AO_SC_ERR 0x1p-50
 
 RT_HD void rt_fast_sincos(double a, double* sinx, double* cosx) {
-    const double kd = rint(a * 0x1.45f306dc9c883p-1);          // round(a * 2/pi)
-    double x = fma(-kd, 0x1.921fb54442d18p+0, a);               // a - k*pi/2 (head, one rounding)
-    x = fma(-kd, 0x1.1a62633145c07p-54, x);                     // - k*(pi/2 tail)
+    const double kd = rint(a * 0x1.45f306dc9c883p+5);           // round(a * 128/pi): 0..256 on [0, 2pi]
+    double x = fma(-kd, 0x1.921fb54442d18p-6, a);               // a - k*pi/128 (head, one rounding)
+    x = fma(-kd, 0x1.1a62633145c07p-60, x);                     // - k*(pi/128 tail); |x| <= pi/256
     const double x2 = x * x;
-    double ps = 0x1.6124613a86d09p-33;                          //  1/13!
-    ps = fma(ps, x2, -0x1.ae64567f544e4p-26);                   // -1/11!
-    ps = fma(ps, x2, 0x1.71de3a556c734p-19);                    //  1/9!
-    ps = fma(ps, x2, -0x1.a01a01a01a01ap-13);                   // -1/7!
-    ps = fma(ps, x2, 0x1.1111111111111p-7);                     //  1/5!
-    ps = fma(ps, x2, -0x1.5555555555555p-3);                    // -1/3!
-    const double s = fma(x * x2, ps, x);
-    double pc = 0x1.93974a8c07c9dp-37;                          //  1/14!
-    pc = fma(pc, x2, -0x1.1eed8eff8d898p-29);                   // -1/12!
-    pc = fma(pc, x2, 0x1.27e4fb7789f5cp-22);                    //  1/10!
-    pc = fma(pc, x2, -0x1.a01a01a01a01ap-16);                   // -1/8!
-    pc = fma(pc, x2, 0x1.6c16c16c16c17p-10);                    //  1/6!
-    pc = fma(pc, x2, -0x1.5555555555555p-5);                    // -1/4!
-    pc = fma(pc, x2, 0.5);
-    const double c = fma(-x2, pc, 1.0);                         // 1 - x^2/2 + x^4/4! - ...
-    const int q = (int)kd & 3;
-    const double sv = (q & 1) ? c : s, cv = (q & 1) ? s : c;
-    *sinx = (q & 2) ? -sv : sv;
-    *cosx = ((q + 1) & 2) ? -cv : cv;
+    const double sx = fma(x * x2, fma(x2, 0x1.1111111111111p-7, -0x1.5555555555555p-3), x);  // sin x to x^5
+    const double cm = x2 * fma(fma(x2, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5), x2, -0.5);  // cos x - 1 to x^6
+    const int k = (int)kd;
+    const double S = RT_T(rt_sct128)[2 * k], C = RT_T(rt_sct128)[2 * k + 1];  // sin, cos (k pi/128)
+    *sinx = S + fma(C, sx, S * cm);                             // S cos x + C sin x
+    *cosx = C + fma(-S, sx, C * cm);                            // C cos x - S sin x
 }
 
 // Would RN_float(X_g) equal f = RN_float(X) for every X_g within RT_AO_SC_ERR + 2^-53
