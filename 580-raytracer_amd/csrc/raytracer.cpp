@@ -103,13 +103,22 @@ int Raytracer::Render(const std::string outputName) {
     // a whole frame lands in mFrameBuffer directly; selected rows through a row buffer
     std::vector<int16_t> rows(whole ? 0 : (size_t)(nsel > 0 ? nsel : 0) * mWidth * 3);
     int16_t* dst = whole ? reinterpret_cast<int16_t*>(mFrameBuffer.data()) : rows.data();
-    // Whole frames shard across the node's GPUs (interleaved rows, RCCL
-    // exchange + gather, rt_gpu_render_multi); SetGpuCount / $RT580_GPUS
-    // choose how many (default: every visible device).
+    // Whole frames can shard across the node's GPUs (interleaved rows, RCCL
+    // exchange + gather, rt_gpu_render_multi) when SetGpuCount or $RT580_GPUS
+    // asks for more than one; the default is the one device of rt_gpu_init
+    // (one process per GPU stays one GPU per process, e.g. under torchrun).
     int gpus = mGpus;
     if (gpus <= 0) {
-        const char* e = std::getenv("RT580_GPUS");
-        gpus = e ? std::atoi(e) : rt_gpu_device_count();
+        gpus = 1;
+        if (const char* e = std::getenv("RT580_GPUS")) {
+            char* end = nullptr;
+            const long v = std::strtol(e, &end, 10);
+            if (end == e || *end || v < 1 || v > 16) {
+                std::cerr << "RT580_GPUS=" << e << ": not an integer in [1, 16]\n";
+                return RT_FAILURE;
+            }
+            gpus = (int)v;
+        }
     }
     const int st = (gpus > 1 && whole) ? rt_gpu_render_multi(&mParams, dst, gpus, nullptr)
                                        : rt_gpu_render(&mParams, dst);

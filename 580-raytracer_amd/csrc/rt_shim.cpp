@@ -84,6 +84,7 @@ struct State {
     uint32_t* far_count_host = nullptr;  // pinned
     uint32_t far_cap = 0;
     uint32_t ao_cap = 0;
+    int chunk_log2 = 26;  // largest far-queue / AO-ray chunk: 2^chunk_log2 rays (RT580_CHUNK_LOG2)
     uint32_t node_cap = 0, call_cap = 0;
     double node_factor = 4.0;         // node capacity per pixel (grown on overflow)
     uint32_t* needed_host = nullptr;  // pinned
@@ -102,32 +103,13 @@ struct State {
 };
 
 constexpr int kMaxCtx = 16;
+constexpr int kChunkLog2Min = 6, kChunkLog2Max = 26;  // chunk capacities of BVH frames (rays)
 State g_ctx[kMaxCtx];
 int g_cur = 0;  // context the entry points act on (0 outside rt_gpu_render_multi)
 #define g (g_ctx[g_cur])
 char g_err[512] = "";
 uint64_t g_scene_counter = 0;  // process-wide upload counter (survives rt_gpu_shutdown)
 
-// The scene last uploaded to context 0, kept on the host for the other devices.
-struct HostScene {
-    std::vector<rt_prim> prims;
-    std::vector<rt_prim_shade> shade;
-    std::vector<rt_material> mats;
-    std::vector<rt_light> lights;
-    rt_scene_soa view() const {
-        rt_scene_soa v;
-        std::memset(&v, 0, sizeof v);
-        v.abi_version = RT580_ABI_VERSION;
-        v.n_prims = (int32_t)prims.size();
-        v.prims = prims.data();
-        v.shade = shade.data();
-        v.n_materials = (int32_t)mats.size();
-        v.materials = mats.data();
-        v.n_lights = (int32_t)lights.size();
-        v.lights = lights.data();
-        return v;
-    }
-} g_host_scene;
 #define SL (g.slot[g.cur])
 
 // Stream of the frame being enqueued.
@@ -393,6 +375,17 @@ int begin_frame() {
     return RT_SUCCESS;
 }
 
+// A new chunk limit: the next frame sizes the chunk buffers again (at most
+// 2^log2 rays). The context's streams are idle.
+void set_chunk_log2(int log2) {
+    if (g.chunk_log2 == log2) return;
+    g.chunk_log2 = log2;
+    for (DevBuf* b : {&g.far_rays, &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.sort_tmp, &g.ao_rays,
+                      &g.ao_late, &g.shadow})
+        release(*b);
+    g.far_cap = g.ao_cap = 0;
+}
+
 // Size the workspace for n_rows x width pixels.
 int ensure_work(const rt_render_params* p, int n_rows) {
     const uint64_t npix = (uint64_t)n_rows * p->width;
@@ -414,22 +407,28 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     if (g.bvh_ok && !g.bvh.far_nodes.empty() && ensure(SL.call_hint, ccap * 4)) return RT_FAILURE;
     g.node_cap = (uint32_t)cap;
     g.call_cap = (uint32_t)ccap;
-    // far-hit queue of the BVH AO pass (chunks of at most far_cap AO rays)
-    if (g.bvh_ok && !g.bvh.far_nodes.empty() && g.far_cap == 0) {
-        const uint32_t fc = 1u << 26;  // rays per sorted chunk: more rays, more coherent waves
+    // Chunked passes of BVH frames: the far-hit queue (one trace level's rays,
+    // or the misses of one AO chunk) and the AO ray records. Sized to what the
+    // frame can need, at most 2^chunk_log2 rays, and grown on demand; a larger
+    // frame runs in several chunks (same results, checked by the GPU tests with
+    // small chunks).
+    auto pow2ceil = [](uint64_t v) { uint64_t r = 1024; while (r < v) r <<= 1; return r; };
+    const uint64_t chunk_max = 1ull << g.chunk_log2;
+    const uint64_t ao_items = p->ao_enabled && g.n_ambient > 0 ? ccap * (uint64_t)p->ao_samples : 0;
+    const uint32_t ac = (uint32_t)std::min(chunk_max, pow2ceil(ao_items));
+    if (g.bvh_ok && g.ao_cap < ac) {  // ray records of the split AO pass (ao_trace_kernel)
+        if (ensure(g.ao_rays, (size_t)ac * 32) || ensure(g.ao_late, (size_t)ac * 4) || ensure(g.ao_late_count, 64))
+            return RT_FAILURE;
+        g.ao_cap = ac;
+    }
+    const uint32_t fc = (uint32_t)std::min(chunk_max, pow2ceil(std::max<uint64_t>(cap, ac)));
+    if (g.bvh_ok && !g.bvh.far_nodes.empty() && g.far_cap < fc) {
         if (ensure(g.far_rays, (size_t)fc * 32) || ensure(g.far_keys, (size_t)fc * 4) ||
             ensure(g.far_keys_alt, (size_t)fc * 4) || ensure(g.far_vals, (size_t)fc * 4) ||
             ensure(g.far_vals_alt, (size_t)fc * 4) || ensure(g.far_count, 64) ||
             ensure(g.sort_tmp, far_sort_tmp_bytes(fc) + 256))
             return RT_FAILURE;
         g.far_cap = fc;
-    }
-    // ray records of the split AO pass (ao_trace_kernel), one chunk
-    if (g.bvh_ok && g.ao_cap == 0) {
-        const uint32_t ac = 1u << 26;
-        if (ensure(g.ao_rays, (size_t)ac * 32) || ensure(g.ao_late, (size_t)ac * 4) || ensure(g.ao_late_count, 64))
-            return RT_FAILURE;
-        g.ao_cap = ac;
     }
     if (g.bvh_ok && !g.bvh.far_nodes.empty() &&
         (ensure(g.hit4, (size_t)cap * 16) || ensure(g.hit_prim, (size_t)cap * 4)))
@@ -533,6 +532,49 @@ int check_capacity(const rt_render_params* p, bool& retry) {
     return RT_SUCCESS;
 }
 
+// Every device buffer of the resident scene (records, shading table, BVH,
+// plane tree, direction grid, shuffled scan order).
+std::vector<DevBuf State::*> scene_bufs() {
+    return {&State::prims, &State::shade, &State::mats, &State::lights, &State::bvh_nodes, &State::bvh_nodes4,
+            &State::bvh_prims, &State::bvh_ids, &State::far_nodes, &State::far_tris, &State::brute,
+            &State::grid_start, &State::grid_items, &State::grid_always, &State::scan_prims};
+}
+
+// The scene of context `src` into the current context without building
+// anything again (the scene is built once and replicated): its
+// device buffers by device-to-device copies (xGMI peer copies between GPUs),
+// the small host-side description by assignment. Both contexts are idle.
+int clone_scene(int src) {
+    const State& c = g_ctx[src];
+    if (!c.have_scene) return fail("clone_scene: context %d has no scene", src);
+    HIP_TRY(hipSetDevice(g.device));
+    if (sync_all()) return RT_FAILURE;
+    for (DevBuf State::*m : scene_bufs()) {
+        const DevBuf& from = c.*m;
+        DevBuf& to = g.*m;
+        if (!from.p) {
+            release(to);
+            continue;
+        }
+        if (ensure(to, from.bytes)) return RT_FAILURE;
+        HIP_TRY(hipMemcpyPeerAsync(to.p, g.device, from.p, c.device, from.bytes, g.stream));
+    }
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    g.bvh = c.bvh;  // the host copy keeps only the small arrays (nodes, far nodes, brute list)
+    g.bvh_ok = c.bvh_ok;
+    g.grid_log2 = c.grid_log2;
+    g.grid_n_always = c.grid_n_always;
+    g.n_prims = c.n_prims;
+    g.n_lights = c.n_lights;
+    g.n_ambient = c.n_ambient;
+    g.n_nonambient = c.n_nonambient;
+    g.shadow_lights = c.shadow_lights;
+    g.have_scene = true;
+    g.scene_gen = ++g_scene_counter;
+    g.verified_valid = false;
+    return RT_SUCCESS;
+}
+
 }  // namespace
 
 extern "C" {
@@ -555,6 +597,13 @@ int rt_gpu_init(int device) {
     {
         const char* e = std::getenv("RT580_PIPELINE");
         g.pipeline = !(e && std::atoi(e) == 0);
+    }
+    if (const char* e = std::getenv("RT580_CHUNK_LOG2")) {
+        char* end = nullptr;
+        const long v = std::strtol(e, &end, 10);
+        if (end == e || *end || v < kChunkLog2Min || v > kChunkLog2Max)
+            return fail("RT580_CHUNK_LOG2=%s: not an integer in [%d, %d]", e, kChunkLog2Min, kChunkLog2Max);
+        g.chunk_log2 = (int)v;
     }
     for (auto& sl : g.slot) {
         HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
@@ -673,12 +722,6 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     }
     g.have_scene = true;
     g.scene_gen = ++g_scene_counter;
-    if (g_cur == 0) {
-        g_host_scene.prims.assign(s->prims, s->prims + s->n_prims);
-        g_host_scene.shade.assign(s->shade, s->shade + s->n_prims);
-        g_host_scene.mats.assign(s->materials, s->materials + s->n_materials);
-        g_host_scene.lights.assign(s->lights, s->lights + s->n_lights);
-    }
     return RT_SUCCESS;
 }
 
@@ -855,6 +898,16 @@ int rt_gpu_set_accel(int mode) {
 
 int rt_gpu_accel_active(void) { return g.last_accel ? 1 : 0; }
 
+int rt580_set_chunk_log2(int log2) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (log2 < kChunkLog2Min || log2 > kChunkLog2Max)
+        return fail("chunk log2 %d outside [%d, %d]", log2, kChunkLog2Min, kChunkLog2Max);
+    HIP_TRY(hipSetDevice(g.device));
+    if (sync_all()) return RT_FAILURE;
+    set_chunk_log2(log2);
+    return RT_SUCCESS;
+}
+
 int rt_gpu_last_stats(rt_render_stats* st) {
     if (!st) return RT_INVALID_ARG;
     std::memset(st, 0, sizeof *st);
@@ -930,6 +983,7 @@ const char* rt_gpu_last_error(void) { return g_err; }
 namespace {
 void destroy_comms();
 void release_multi();
+void release_multi_ctx(int k);
 
 void shutdown_ctx() {
     if (!g.inited) return;
@@ -1053,16 +1107,23 @@ void destroy_comms() {
     g_multi.n = 0;
 }
 
+// Context k's split buffers and event, released on the device they live on
+// (before the context moves to another device, or at shutdown). The
+// communicator of a device set that included k is destroyed too.
+void release_multi_ctx(int k) {
+    if (!g_ctx[k].inited) return;
+    if (k < g_multi.n) destroy_comms();
+    (void)hipSetDevice(g_ctx[k].device);
+    (void)hipDeviceSynchronize();
+    for (DevBuf* b : {&g_multi.row_calls[k], &g_multi.gathered[k], &g_multi.base[k], &g_multi.tile[k]}) release(*b);
+    if (g_multi.ready[k]) (void)hipEventDestroy(g_multi.ready[k]);
+    g_multi.ready[k] = nullptr;
+    g_multi.scene_of[k] = 0;
+}
+
 void release_multi() {
     destroy_comms();
-    for (int k = 0; k < kMaxCtx; k++) {
-        if (!g_ctx[k].inited) continue;
-        (void)hipSetDevice(g_ctx[k].device);
-        for (DevBuf* b : {&g_multi.row_calls[k], &g_multi.gathered[k], &g_multi.base[k], &g_multi.tile[k]}) release(*b);
-        if (g_multi.ready[k]) (void)hipEventDestroy(g_multi.ready[k]);
-        g_multi.ready[k] = nullptr;
-        g_multi.scene_of[k] = 0;
-    }
+    for (int k = 0; k < kMaxCtx; k++) release_multi_ctx(k);
     if (g_ctx[0].inited) {
         (void)hipSetDevice(g_ctx[0].device);
         release(g_multi.root_tiles);
@@ -1191,16 +1252,19 @@ int multi_render(const rt_render_params* p, int16_t* fb_out, int n, const int* d
     const State& c0 = g_ctx[0];
     for (int k = 1; k < n; k++) {
         g_cur = k;
-        if (g.inited && g.device != devs[k]) {
+        if (g.inited && g.device != devs[k]) {  // this context moves to another device
+            release_multi_ctx(k);
             shutdown_ctx();
-            g_multi.scene_of[k] = 0;
         }
         if (!g.inited && rt_gpu_init(devs[k])) return RT_FAILURE;
         g.accel = c0.accel;
         g.pipeline = c0.pipeline;
+        if (g.chunk_log2 != c0.chunk_log2) {
+            if (sync_all()) return RT_FAILURE;
+            set_chunk_log2(c0.chunk_log2);
+        }
         if (g_multi.scene_of[k] != c0.scene_gen) {
-            const rt_scene_soa v = g_host_scene.view();
-            if (rt_gpu_upload_scene(&v)) return RT_FAILURE;
+            if (clone_scene(0)) return RT_FAILURE;
             g_multi.scene_of[k] = c0.scene_gen;
         }
     }

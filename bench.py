@@ -3,24 +3,34 @@
 "Mrays/sec + ms/frame at 1920x1080, depth=4, 64 AO samples; 1/2/4/8 GPU").
 
 A step = one frame of BASELINE config 2 (simpleSphereScene.json, 1920x1080,
-depth 4, 64 AO samples; the reference's own scene file) rendered from scratch:
-trace of the recursion tree, AO-call count + RNG-offset scan, AO kernel,
-resolve (+ for N > 1 the all-gather of per-row AO counts and the RCCL gather of
-the row tiles to rank 0). The scene is resident in HBM; the framebuffer stays
-in HBM (device throughput, frames pipelined on two streams). The blocking
-Render() latency (framebuffer copied to the host) is reported beside it.
+depth 4, 64 AO samples; the reference's own scene file) rendered from scratch
+by the reference's Render() loop (Raytracer.cpp:916-935): trace of the
+recursion tree, AO-call count + RNG-offset scan, AO kernel, resolve (+ for
+N > 1 the all-gather of per-row AO counts and the gather of the row tiles).
+The scene is resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    python bench.py [--gpus N [--rehearse]] [--steps K] [--warmup W]
                     [--workload config2|cornell10k|field100k_1080p|field100k|field1m]
+                    [--no-cpu-baseline] [--no-north-star] [--no-check]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
---workload selects another BASELINE configuration (synthetic scenes from
-tools/gen_scenes.py, generated on first use under tests/_scenes); config2 is
-the headline. Synthetic workloads default to 2 steps after 1 warm-up.
+Parallel modes (the row split of SURVEY §8e, byte-identical frames for every N):
+  * N = 1: rt_gpu_render_device, two frames in flight, framebuffer left in HBM
+    (device throughput); the blocking Render() latency is reported beside it.
+  * --gpus N without a launcher: rt_gpu_render_multi over devices 0..N-1 in this
+    process (what the drop-in Render() calls: single-process RCCL, framebuffer
+    on the host every step). N above the visible devices is an error;
+    --rehearse runs the same split on device 0 N times (device copies instead
+    of RCCL) to rehearse it on a one-GPU box.
+  * under torch.distributed.run: one process per GPU (rt580_dist.DistFrame:
+    RCCL all-gather of the counts, async gather of the u8 tiles to rank 0).
+    --gpus must equal WORLD_SIZE.
 
-Rank 0 prints ONE JSON line on stdout (metric, value = whole-job Mrays/s,
-ms_per_step, roofline of the AO ray kernel, cpu_baseline = the repository's
-CPU restatement in ref-faithful mode on this host, 1 core and all cores).
+Rank 0 prints ONE JSON line on stdout: metric, value = whole-job Mrays/s,
+ms_per_step, roofline of the AO ray kernel, cpu_baseline (N = 1), the frame
+check of the last timed frame (config 2: the reference's sha256), and the
+north_star sub-record: the 100k-triangle 1920x1080 depth-4 AO-64 frame that
+BASELINE's target names, measured the same way in the same run.
 """
 import argparse
 import contextlib
@@ -37,37 +47,22 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 # every 2 cycles, 2.4 GHz; HBM3E 8.0 TB/s.
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0   # 1228.8 G wave-instructions/s
 HBM_PEAK_GBS = 8000.0
+PROFILE_ROUNDS = ("r03", "r02")         # newest committed counter profiles first
 
-# name -> (scene, synthetic?, width, height, depth, AO samples,
-#          CPU-baseline sample, label)
-# CPU sample (~10-30 s for the ref-faithful restatement on one core):
-#   (w, h, depth, ao)  a downscaled frame of the same scene (config 2: exact bytes);
-#   ("pixels", P[, A]) P pixels of the workload's own full-resolution frame on a
-#                      stratified grid, at its depth and AO count (A: a smaller AO
-#                      count, config 5 only: one 1M-triangle pixel at AO 256 is
-#                      minutes of CPU; the reference's IntersectScene loops over every
-#                      primitive for every ray, Raytracer.cpp:476-521, so its cost
-#                      per ray does not depend on the ray's kind).
+# name -> (scene, synthetic?, width, height, depth, AO samples, label)
 WORKLOADS = {
-    "config2": ("simpleSphereScene.json", False, 1920, 1080, 4, 64, (640, 360, 4, 64),
+    "config2": ("simpleSphereScene.json", False, 1920, 1080, 4, 64,
                 "BASELINE config 2: simpleSphereScene.json 1920x1080 depth=4 AO=64"),
-    "cornell10k": ("cornell10k.json", True, 1920, 1080, 4, 64, ("pixels", 64),
+    "cornell10k": ("cornell10k.json", True, 1920, 1080, 4, 64,
                    "BASELINE config 3: 10k-triangle Cornell box 1920x1080 depth=4 AO=64"),
-    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64, ("pixels", 32),
+    "field100k_1080p": ("field100k.json", True, 1920, 1080, 4, 64,
                         "north_star target: 100k-triangle field 1920x1080 depth=4 AO=64"),
-    "field100k": ("field100k.json", True, 3840, 2160, 6, 256, ("pixels", 2),
+    "field100k": ("field100k.json", True, 3840, 2160, 6, 256,
                   "BASELINE config 4: 100k-triangle field 3840x2160 depth=6 AO=256"),
-    "field1m": ("field1m.json", True, 7680, 4320, 8, 256, ("pixels", 1, 8),
+    "field1m": ("field1m.json", True, 7680, 4320, 8, 256,
                 "BASELINE config 5: 1M-triangle field 7680x4320 depth=8 AO=256"),
 }
-
-
-def stratified_pixels(n, w, h):
-    """n pixel centres of a gx x gy (>= n cells) grid over the w x h frame (raster order)."""
-    gx = max(1, int(round((n * w / h) ** 0.5)))
-    gy = (n + gx - 1) // gx
-    pts = [(int((i + 0.5) * w / gx), int((j + 0.5) * h / gy)) for j in range(gy) for i in range(gx)]
-    return [pts[k * len(pts) // n] for k in range(n)]  # n cells spread over the whole grid
+CPU_BUDGET_S = 15.0  # one core, per workload (the all-cores leg renders the same pixels)
 
 
 def env_int(k, d):
@@ -75,6 +70,10 @@ def env_int(k, d):
         return int(os.environ.get(k, d))
     except ValueError:
         return d
+
+
+def log(msg):
+    print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
 
 
 @contextlib.contextmanager
@@ -93,154 +92,167 @@ def stdout_to_stderr():
         os.close(saved)
 
 
-def main():
-    # stdout carries exactly one JSON line: everything else written to fd 1 (the
-    # drop-in's "Scene parsing completed!", RCCL's version banner at communicator
-    # init) goes to stderr; the JSON line goes to the saved original stdout
-    sys.stdout.flush()
-    json_out = os.fdopen(os.dup(1), "w")
-    os.dup2(2, 1)
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="default 20 (config2), 2 (synthetic)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 3 (config2), 1 (synthetic)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
-    ap.add_argument("--dist", action="store_true",
-                    help="the multi-rank path (torch.distributed + DistFrame) even with one rank: rehearses the "
-                         "RCCL all-gather/gather and the per-frame host overhead of N>1 on one GPU")
-    ap.add_argument("--check", action="store_true", help="verify the frame against the golden sha256 (config2)")
-    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
-    ap.add_argument("--row-sample", type=int, default=1,
-                    help="N=1 only: time rows r = 0 mod K of the frame (rank 0's exact share of a K-way "
-                         "interleaved split; RNG bases from an untimed full-frame count), for huge frames")
-    args = ap.parse_args()
-    global SCENE, WIDTH, HEIGHT, DEPTH, AO, CPU_SAMPLE, LABEL, SYNTH
-    SCENE, SYNTH, WIDTH, HEIGHT, DEPTH, AO, CPU_SAMPLE, LABEL = WORKLOADS[args.workload]
-    if args.steps is None:
-        args.steps = 2 if SYNTH else 20
-    if args.warmup is None:
-        args.warmup = 1 if SYNTH else 3
+class Ctx:
+    """What every workload run shares: torch, the library, the parallel mode."""
 
-    import torch
-    import torch.distributed as dist
-    import helpers
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        import helpers
+        self.torch, self.dist, self.helpers = torch, dist, helpers
+        self.args = args
+        self.rank, self.world = env_int("RANK", 0), env_int("WORLD_SIZE", 1)
+        self.launched = "WORLD_SIZE" in os.environ
+        n_dev = torch.cuda.device_count()
+        if self.launched and args.gpus != self.world:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, self.world))
+        self.dist_on = self.world > 1 or args.dist
+        self.multi = 0 if self.dist_on else (args.gpus if args.gpus > 1 else 0)
+        if self.multi and not args.rehearse and self.multi > n_dev:
+            raise SystemExit("bench.py: --gpus %d but %d visible device(s); --rehearse splits the frame over "
+                             "device 0 instead" % (self.multi, n_dev))
+        self.devices = ([0] * self.multi if args.rehearse else list(range(self.multi))) if self.multi else None
+        # one GPU per rank; on a box with fewer GPUs than ranks (rehearsal of the
+        # multi-rank path with --backend gloo) ranks share devices round-robin
+        self.local_rank = env_int("LOCAL_RANK", 0) % max(n_dev, 1)
+        torch.cuda.set_device(self.local_rank)
+        self.device = torch.device("cuda", self.local_rank)
+        if self.dist_on:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29581")
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", rank=self.rank, world_size=self.world, device_id=self.device)
+            else:
+                dist.init_process_group(args.backend, rank=self.rank, world_size=self.world)
+        self.rt580 = helpers.rt580()
+        self.lib = self.rt580.load()
+        self.rt580.check(self.lib.rt_gpu_init(self.local_rank), "rt_gpu_init")
+        self.stream = torch.cuda.current_stream(self.device)
+        self.rt580.check(self.lib.rt_gpu_set_stream(ctypes.c_void_p(self.stream.cuda_stream)), "rt_gpu_set_stream")
+        self.n_gpus = self.world if self.dist_on else max(self.multi, 1)
+        self.row_sample = args.row_sample if self.n_gpus == 1 and not self.dist_on else 1
+        self.row_rank = args.row_rank if self.row_sample > 1 else 0
 
-    rank, world = env_int("RANK", 0), env_int("WORLD_SIZE", 1)
-    # one GPU per rank; on a box with fewer GPUs than ranks (rehearsal of the
-    # multi-rank path with --backend gloo) ranks share devices round-robin
-    local_rank = env_int("LOCAL_RANK", 0) % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
-    dist_on = world > 1 or args.dist
-    if dist_on:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29581")
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
-        else:
-            dist.init_process_group(args.backend, rank=rank, world_size=world)
+    def barrier(self):
+        if self.dist_on:
+            self.dist.barrier()
 
-    rt580 = helpers.rt580()
-    lib = rt580.load()
-    rt580.check(lib.rt_gpu_init(local_rank), "rt_gpu_init")
-    stream = torch.cuda.current_stream(device)
-    rt580.check(lib.rt_gpu_set_stream(ctypes.c_void_p(stream.cuda_stream)), "rt_gpu_set_stream")
+    def parallelism(self):
+        if self.dist_on:
+            return "interleaved rows x%d, one process per GPU, %s all_gather/gather" % (
+                self.world, "RCCL" if self.args.backend == "nccl" else self.args.backend)
+        if self.multi:
+            if self.args.rehearse:
+                return ("interleaved rows x%d on device 0 (rehearsal: device copies instead of RCCL; "
+                        "not a multi-GPU measurement)" % self.multi)
+            return "interleaved rows x%d, one process (rt_gpu_render_multi, RCCL)" % self.multi
+        return "1 GPU"
 
-    root = helpers.synthetic_root(SCENE[:-5]) if SYNTH else helpers.ASSETS_ROOT
-    rt = rt580.Raytracer(WIDTH, HEIGHT, root)
+
+def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
+    """Render `name` warmup + steps times in ctx's parallel mode; returns the
+    bench record (rank 0) or None."""
+    torch, lib, rt580, helpers = ctx.torch, ctx.lib, ctx.rt580, ctx.helpers
+    scene, synth, W, H, depth, ao, label = WORKLOADS[name]
+    root = helpers.synthetic_root(scene[:-5]) if synth else helpers.ASSETS_ROOT
+    rt = rt580.Raytracer(W, H, root)
     with stdout_to_stderr():
-        assert rt.LoadSceneJSON(SCENE) == 0, "LoadSceneJSON failed"
-    rt.set_depth(DEPTH)
-    rt.set_ao(AO, True)
+        assert rt.LoadSceneJSON(scene) == 0, "LoadSceneJSON failed"
+    rt.set_depth(depth)
+    rt.set_ao(ao, True)
     assert rt.InitializeRenderer() == 0
     params = rt.render_params()
-    scene = rt.scene()
-    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(scene)), "rt_gpu_upload_scene")
-    prims = [scene.prims[i] for i in range(scene.n_prims)]
-    n_tri = sum(1 for p in prims if p.kind == 0)
+    sc = rt.scene()
+    t_up = time.perf_counter()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(sc)), "rt_gpu_upload_scene")
+    upload_s = time.perf_counter() - t_up
+    n_tri = sum(1 for i in range(sc.n_prims) if sc.prims[i].kind == 0)
+    log("%s: scene uploaded (%d primitives, %.1f s incl. acceleration build)" % (name, sc.n_prims, upload_s))
 
     fbp = ctypes.c_void_p()
-    K = max(args.row_sample, 1) if not dist_on else 1
-    dist_mod = helpers.rt580_dist() if (dist_on or K > 1) else None
-    backend = dist_mod.GpuRows(rt580, params, torch, device) if (dist_on or K > 1) else None
-    sample_base = None
-    if K > 1:
-        # exact global RNG bases: every row's AO-call count, once, outside the timed region
-        log("row sample 1/%d: full-frame count pass" % K)
-        cnt = backend.count(0, 1)[:HEIGHT].to(torch.int64)
-        base = torch.cumsum(cnt, 0) - cnt
-        n_loc = dist_mod.n_local_rows(HEIGHT, 0, K)
-        sample_base = torch.zeros(dist_mod.n_max_rows(HEIGHT, K), dtype=torch.int64, device=device)
-        sample_base[:n_loc] = base[0::K][:n_loc]
-
-    # steady-state multi-rank frames (RCCL): persistent buffers, async gather
-    # overlapped with the next frame; gloo (rehearsal) uses the plain form
-    dframe = dist_mod.DistFrame(backend, dist, torch, HEIGHT, WIDTH, rank, world, device) \
-        if (dist_on and args.backend == "nccl") else None
+    host = None
+    dframe = None
+    dist_mod = helpers.rt580_dist() if ctx.dist_on else None
+    if ctx.dist_on:
+        backend = dist_mod.GpuRows(rt580, params, torch, ctx.device)
+        if ctx.args.backend == "nccl":
+            dframe = dist_mod.DistFrame(backend, ctx.dist, torch, H, W, ctx.rank, ctx.world, ctx.device)
+    import numpy as np
+    if ctx.multi:
+        host = np.zeros(W * H * 3, dtype=np.int16)
+        devs = (ctypes.c_int * ctx.multi)(*ctx.devices)
 
     def step():
         if K > 1:
-            backend.count(0, K)
-            return backend.shade(0, K, sample_base)
-        if not dist_on:
-            rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(fbp)), "rt_gpu_render_device")
+            rows.count(R, K)
+            rows.shade(R, K, sample_base)
             return None
-        if dframe is not None:
-            dframe.render()
+        if ctx.dist_on:
+            if dframe is not None:
+                dframe.render()
+                return None
+            return dist_mod.render_frame(backend, ctx.dist, torch, H, W, ctx.rank, ctx.world)
+        if ctx.multi:
+            rt580.check(lib.rt_gpu_render_multi(ctypes.byref(params), host.ctypes.data, ctx.multi, devs),
+                        "rt_gpu_render_multi")
             return None
-        return dist_mod.render_frame(backend, dist, torch, HEIGHT, WIDTH, rank, world)
+        rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(fbp)), "rt_gpu_render_device")
+        return None
 
     def finish():
         return dframe.finish() if dframe is not None else None
 
-    def barrier():
-        if dist_on:
-            dist.barrier()
+    # rank r's exact share of a K-way interleaved split (--row-sample K
+    # --row-rank r, one GPU): RNG bases from a full-frame count, untimed
+    K, R = ctx.row_sample, ctx.row_rank
+    sample_base = None
+    if K > 1:
+        rows = helpers.rt580_dist().GpuRows(rt580, params, torch, ctx.device)
+        log("%s: row sample %d/%d: full-frame count pass" % (name, R, K))
+        cnt = rows.count(0, 1)[:H].to(torch.int64)
+        base = torch.cumsum(cnt, 0) - cnt
+        n_loc = helpers.rt580_dist().n_local_rows(H, R, K)
+        sample_base = torch.zeros(helpers.rt580_dist().n_max_rows(H, K), dtype=torch.int64, device=ctx.device)
+        sample_base[:n_loc] = base[R::K][:n_loc]
 
-    frame = None
-    for i in range(max(args.warmup, 1 if args.check else 0)):
-        frame = step()
-        if dframe is not None:
-            frame = finish()
-        if SYNTH:
+    # a split frame (N > 1 in this process): the frame's rays, and the frame to
+    # compare with, from one untimed single-device render (rt_gpu_last_stats
+    # of a split frame covers context 0's rows only)
+    single = None
+    if ctx.multi:
+        single = np.zeros(W * H * 3, dtype=np.int16)
+        rt580.check(lib.rt_gpu_render(ctypes.byref(params), single.ctypes.data), "rt_gpu_render")
+        st = rt580.RenderStats()
+        rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "rt_gpu_last_stats")
+        rays_single = int(st.rays_total)
+
+    for i in range(warmup):
+        step()
+        finish()
+        if synth:
             torch.cuda.synchronize()
-            log("warmup step %d done" % i)
+            log("%s: warmup step %d done" % (name, i))
     torch.cuda.synchronize()
-    check_ok = None
-    if args.check and rank == 0:
-        # the frame of the (last warm-up) step vs the reference's config-2 hash
-        import numpy as np
-        if not dist_on:
-            host = np.zeros(WIDTH * HEIGHT * 3, dtype=np.int16)
-            rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
-            frame_np = host.reshape(HEIGHT, WIDTH, 3)
-        else:
-            frame_np = frame.cpu().numpy()
-        want = next(e for e in helpers.golden_entries(False) if e["name"] == "config2_1080p_d4_ao64")["sha256"]
-        if frame_np.dtype == np.uint8:  # DistFrame(u8=True): already the PPM body
-            ppm = b"P6\n%d %d\n255\n" % (WIDTH, HEIGHT) + frame_np.tobytes()
-        else:
-            ppm = rt580.ppm_bytes(frame_np)
-        check_ok = helpers.sha256(ppm) == want
     rt580.check(lib.rt_gpu_profile(1), "rt_gpu_profile")
-    barrier()
+    ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     host_s = 0.0  # host time inside step(): the enqueue cost of a frame (its kernels run asynchronously)
-    for i in range(args.steps):
+    last = None
+    for i in range(steps):
         th = time.perf_counter()
         step()
         host_s += time.perf_counter() - th
-        if i == args.steps - 1:
-            finish()  # the last frame's gather + de-interleave belong to the timed region
-        if SYNTH:  # long frames: keep a progress line per step (sync costs microseconds)
+        if i == steps - 1:
+            last = finish()  # the last frame's gather + de-interleave belong to the timed region
+        if synth:  # long frames: keep a progress line per step (sync costs microseconds)
             torch.cuda.synchronize()
-            if rank == 0:
-                log("step %d done" % i)
-    barrier()
+            if ctx.rank == 0:
+                log("%s: step %d done" % (name, i))
+    ctx.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+
     ms = [ctypes.c_double() for _ in range(4)]
     frames = ctypes.c_int()
     rt580.check(lib.rt_gpu_profile_read(*[ctypes.byref(m) for m in ms], ctypes.byref(frames)), "rt_gpu_profile_read")
@@ -249,86 +261,113 @@ def main():
     k_ms, k_launches, k_rays = ctypes.c_double(), ctypes.c_int(), ctypes.c_uint64()
     rt580.check(lib.rt_gpu_profile_ao_kernel(ctypes.byref(k_ms), ctypes.byref(k_launches), ctypes.byref(k_rays)),
                 "rt_gpu_profile_ao_kernel")
-    # rays of one frame (this rank's rows), from the count pass of the last frame
     st = rt580.RenderStats()
     rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "rt_gpu_last_stats")
     local = st.as_dict()
 
-    rays_local = int(local["rays_total"])
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    # the last timed frame, on rank 0's host (int16 Pixel frame, or the u8 PPM body of DistFrame)
+    frame_np = None
+    if ctx.rank == 0 and K == 1:
+        if ctx.dist_on:
+            frame_np = last.cpu().numpy() if last is not None else None
+        elif ctx.multi:
+            frame_np = host.reshape(H, W, 3)
+        else:
+            frame_np = rt580.copy_to_host(fbp.value, W * H * 6, np.int16).reshape(H, W, 3)
+
+    if ctx.dist_on:
+        t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
+        ctx.dist.all_reduce(t, op=ctx.dist.ReduceOp.MAX)
         dt = float(t.item())
-        r = torch.tensor([rays_local], dtype=torch.int64, device=device)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        r = torch.tensor([int(local["rays_total"])], dtype=torch.int64, device=ctx.device)
+        ctx.dist.all_reduce(r, op=ctx.dist.ReduceOp.SUM)
         rays_frame = int(r.item())
+    elif ctx.multi:
+        rays_frame = rays_single
     else:
-        rays_frame = rays_local
+        rays_frame = int(local["rays_total"])  # this call's rows (all of them, or the row sample)
+    if ctx.rank != 0:
+        return None
 
-    if rank == 0:
-        value = rays_frame * args.steps / dt / 1e6
-        out = {
-            "metric": "Mrays/sec (+ ms/frame) at %dx%d, depth=%d, %d AO samples" % (WIDTH, HEIGHT, DEPTH, AO),
-            "value": round(value, 3),
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": ("synthetic scene (tools/gen_scenes.py, seed 580, %d triangles)" % n_tri) if SYNTH else
-                    "reference scene file Assets/%s (no dataset needed)" % SCENE,
-            "config": {
-                "workload": LABEL,
-                "scene": SCENE, "width": WIDTH, "height": HEIGHT, "depth": DEPTH, "ao_samples": AO,
-                "rng": "minstd_rand0 (libstdc++ default_random_engine)",
-                "rays_per_frame": rays_frame,
-                "parallelism": ("interleaved rows x%d + %s all_gather/gather" % (world, "RCCL" if args.backend == "nccl"
-                                else args.backend)) if dist_on else "1 GPU",
-                "row_sample": ("rows r = 0 mod %d only (the exact pixels of rank 0 in a %d-way interleaved split; "
-                               "RNG bases from a full-frame count outside the timed region); value and "
-                               "rays_per_frame refer to the sample" % (K, K)) if K > 1 else None,
-                "scene_query": "exact BVH + plane tree (rt_bvh.h)" if lib.rt_gpu_accel_active() else
-                               "brute force (every primitive per ray, as the reference)",
-            },
-            "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4),
-            "kernel_ms_per_frame": {
-                "trace": round(per_frame[0], 4),
-                "rank": round(per_frame[1], 4),
-                "ao": round(per_frame[2], 4),
-                "resolve": round(per_frame[3], 4),
-            },
-        }
-        if check_ok is not None:
-            out["frame_matches_reference"] = check_ok
-        # AO rays per timed launch: the chunked BVH launches report theirs; a
-        # small-scene frame is one launch over all of its AO rays
-        k_units = k_rays.value if k_rays.value else int(local["rays_ao"]) * max(frames.value, 1)
-        out["roofline"] = roofline(args.workload, k_ms.value, k_launches.value, k_units, int(local["rays_ao"]))
-        if not dist_on and K == 1:
-            out["render_call_ms"] = render_latency(lib, rt580, params, torch)
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(lib, rt580, helpers, root)
-        print(json.dumps(out), file=json_out, flush=True)
-    if dist_on:
-        dist.barrier()
-        dist.destroy_process_group()
-
-
-def log(msg):
-    print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
+    value = rays_frame * steps / dt / 1e6
+    out = {
+        "metric": "Mrays/sec (+ ms/frame) at %dx%d, depth=%d, %d AO samples" % (W, H, depth, ao),
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": ctx.n_gpus,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": ("synthetic scene (tools/gen_scenes.py, seed 580, %d triangles)" % n_tri) if synth else
+                "reference scene file Assets/%s (no dataset needed)" % scene,
+        "config": {
+            "workload": label,
+            "scene": scene, "width": W, "height": H, "depth": depth, "ao_samples": ao,
+            "rng": "minstd_rand0 (libstdc++ default_random_engine)",
+            "rays_per_frame": rays_frame,
+            "parallelism": ctx.parallelism(),
+            "row_sample": ("rows r = %d mod %d only (the exact pixels of rank %d in a %d-way interleaved split; "
+                           "RNG bases from a full-frame count outside the timed region); value and "
+                           "rays_per_frame refer to the sample" % (R, K, R, K)) if K > 1 else None,
+            "scene_query": "exact BVH + plane tree (rt_bvh.h)" if lib.rt_gpu_accel_active() else
+                           "brute force (every primitive per ray, as the reference)",
+        },
+        "step": ("one frame; framebuffer left in HBM, two frames in flight (device throughput)" if not
+                 (ctx.dist_on or ctx.multi) else
+                 "one frame, whole Render(): framebuffer on device 0's host copy" if ctx.multi else
+                 "one frame on every rank; rank 0 holds the gathered u8 frame"),
+        "scene_upload_s": round(upload_s, 3),
+        "host_enqueue_ms_per_step": round(host_s / steps * 1e3, 4),
+        "kernel_ms_per_frame" + ("" if not (ctx.dist_on or ctx.multi) else "_rank0"): {
+            "trace": round(per_frame[0], 4), "rank": round(per_frame[1], 4),
+            "ao": round(per_frame[2], 4), "resolve": round(per_frame[3], 4)},
+    }
+    # AO rays per timed launch: the chunked BVH launches report theirs; a
+    # small-scene frame is one launch over all of its (this context's) AO rays
+    k_units = k_rays.value if k_rays.value else int(local["rays_ao"]) * max(frames.value, 1)
+    out["roofline"] = roofline(name, k_ms.value, k_launches.value, k_units)
+    if frame_np is not None:
+        out["frame_check"] = frame_check(ctx, name, frame_np, single, W, H, check)
+    if not ctx.dist_on and not ctx.multi and K == 1:
+        out["render_call_ms"] = render_latency(lib, rt580, params, torch)
+    if cpu_baseline_on and ctx.n_gpus == 1 and not ctx.dist_on:
+        gpu_px = frame_np.reshape(-1, 3) if frame_np is not None and frame_np.dtype == np.int16 else None
+        out["cpu_baseline"] = cpu_baseline(ctx, name, root, params, gpu_px)
+    return out
 
 
-def roofline(workload, k_ms, k_launches, k_rays, rays_ao_frame):
+def frame_check(ctx, name, frame_np, single, W, H, check):
+    """The last timed frame against the reference's hash (config 2: the sha256 of
+    the reference's own 1080p render, tests/golden/manifest.json) and, for a
+    split frame, against the single-device render of the same frame."""
+    import numpy as np
+    rt580, helpers = ctx.rt580, ctx.helpers
+    res = {"frame": "last timed step"}
+    if frame_np.dtype == np.uint8:  # DistFrame(u8=True): already the PPM body
+        ppm = b"P6\n%d %d\n255\n" % (W, H) + frame_np.tobytes()
+    else:
+        ppm = rt580.ppm_bytes(frame_np)
+    res["sha256"] = helpers.sha256(ppm)
+    if check and name == "config2":
+        want = next(e for e in helpers.golden_entries(False) if e["name"] == "config2_1080p_d4_ao64")["sha256"]
+        res["reference_sha256"] = want
+        res["matches_reference"] = res["sha256"] == want
+    if single is not None and (ctx.multi or ctx.dist_on):
+        res["matches_single_gpu"] = bool(np.array_equal(frame_np.reshape(-1), single))
+    return res
+
+
+def roofline(workload, k_ms, k_launches, k_rays):
     """Roofline of the AO ray kernel (the scene query of every AO sample; 95 %
     of the frame's rays). Neither MFMA nor HBM bounds it (no dense
     contraction; the scene is re-read from L2/MALL, see `traffic`): it is
     bound by VALU instruction issue. achieved = VALU wave-instructions per AO
     ray (rocprofv3 SQ_INSTS_VALU per dispatch / AO rays per dispatch, from the
-    committed profile summary profiles/r02/roofline_<workload>.json) x the AO
+    committed profile summary profiles/<round>/roofline_<workload>.json) x the AO
     rays of one launch / that launch's mean duration, measured here with HIP
     events around every launch on its own stream (rt_gpu_profile_ao_kernel).
     peak = 1024 SIMDs x one wave64 VALU instruction per 2 cycles x 2.4 GHz."""
@@ -341,15 +380,17 @@ def roofline(workload, k_ms, k_launches, k_rays, rays_ao_frame):
     rays_launch = k_rays / k_launches
     res["launch_ms"] = round(launch_s * 1e3, 4)
     res["ao_rays_per_launch"] = int(rays_launch)
-    path = os.path.join(REPO, "profiles", "r02", "roofline_%s.json" % workload)
-    prof = None
-    if os.path.exists(path):
-        try:
-            prof = json.load(open(path))
-        except (ValueError, OSError):
-            prof = None
+    prof, path = None, None
+    for rnd in PROFILE_ROUNDS:
+        p = os.path.join(REPO, "profiles", rnd, "roofline_%s.json" % workload)
+        if os.path.exists(p):
+            try:
+                prof, path = json.load(open(p)), p
+                break
+            except (ValueError, OSError):
+                pass
     if not prof or not prof.get("valu_per_ao_ray"):
-        res["note"] = "no committed counter profile for this workload (%s)" % os.path.relpath(path, REPO)
+        res["note"] = "no committed counter profile for this workload (profiles/*/roofline_%s.json)" % workload
         return res
     res["kernel"] = prof["kernel"]
     achieved = prof["valu_per_ao_ray"] * rays_launch / launch_s / 1e9
@@ -388,64 +429,120 @@ def render_latency(lib, rt580, params, torch, n=3):
     return round(sum(times) / len(times), 4)
 
 
-def cpu_baseline(lib, rt580, helpers, root):
-    """The repository's CPU restatement (oracle/) in ref-faithful mode (the
-    reference's per-call work: string mesh lookup and ComputeModelMatrix per
-    shape per IntersectScene call, the unused Matrix::Inverse + TransformPoint
-    per triangle test; oracle_set_mode(1)) on a bounded sample of the same
-    workload (CPU_SAMPLE), on 1 core and on all of this host's cores (threads).
-    The reference itself does not travel to this box."""
-    threads = env_int("OMP_NUM_THREADS", os.cpu_count() or 1)
-    if CPU_SAMPLE[0] == "pixels":
-        pts = stratified_pixels(CPU_SAMPLE[1], WIDTH, HEIGHT)
-        ao = CPU_SAMPLE[2] if len(CPU_SAMPLE) > 2 else AO
-        threads = min(threads, len(pts))
-
-        def run(nt):
-            return helpers.oracle_time_pixels(SCENE, WIDTH, HEIGHT, DEPTH, ao, pts, threads=nt, root=root,
-                                              faithful=True)
-        sample = ("%s %dx%d depth=%d AO=%d: %d pixel(s) of the full-resolution frame on a stratified grid "
-                  "(RNG at an estimated draw offset: same work per pixel, not the frame's exact bytes)%s"
-                  % (SCENE, WIDTH, HEIGHT, DEPTH, ao, len(pts),
-                     "" if ao == AO else "; AO %d instead of %d (CPU cost per ray is independent of the ray's "
-                     "kind: the reference tests every primitive per ray)" % (ao, AO)))
-    else:
-        w, h, depth, ao = CPU_SAMPLE
-
-        def run(nt):
-            return helpers.oracle_render(SCENE, w, h, depth, ao, True, threads=nt, root=root, faithful=True)[1]
-        sample = ("%s %dx%d depth=%d AO=%d (a downscaled frame of the workload, %.4g%% of its pixels)"
-                  % (SCENE, w, h, depth, ao, 100.0 * w * h / (WIDTH * HEIGHT)))
-    t0 = time.perf_counter()
-    cnt = run(1)
-    secs1 = time.perf_counter() - t0
-    rays = cnt["rays_total"]
-    secsn = secs1
-    if threads > 1:
-        t0 = time.perf_counter()
-        run(threads)
-        secsn = time.perf_counter() - t0
-    cpu = ""
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {
-        "value": float("%.4g" % (rays / secs1 / 1e6)),
+    return ""
+
+
+def cpu_baseline(ctx, name, root, params, gpu_px):
+    """The repository's CPU restatement (oracle/) in ref-faithful mode (the
+    reference's per-call work: string mesh lookup and ComputeModelMatrix per
+    shape per IntersectScene call, the unused Matrix::Inverse + TransformPoint
+    per triangle test) running the reference's own raster loop
+    (Raytracer.cpp:921-932) over an exact range of the workload's full frame:
+    from the first row with geometry (the rows above are sky, with no AO call,
+    so the RNG starts at draw 0 exactly as in the full frame), one serial
+    stream on one core for ~CPU_BUDGET_S seconds; then the same pixels on all
+    of this host's cores (count pass, scan, pixels as work items). Both are
+    compared with the GPU's last timed frame (parity). The reference itself
+    does not travel to this box: profiles/r03/cpu_calibration.json holds the
+    port-to-reference cost ratio measured in the build container."""
+    helpers, torch = ctx.helpers, ctx.torch
+    scene, _, W, H, depth, ao, _ = WORKLOADS[name]
+    # first row with an AO call, from the GPU's count pass (untimed)
+    rows = ctx.helpers.rt580_dist().GpuRows(ctx.rt580, params, torch, ctx.device)
+    counts = rows.count(0, 1)[:H].cpu().numpy()
+    nz = counts.nonzero()[0]
+    y0 = int(nz[0]) if len(nz) else 0
+    p0 = y0 * W
+    threads = env_int("OMP_NUM_THREADS", os.cpu_count() or 1)
+    fb1, cnt, secs1 = helpers.oracle_time_prefix(scene, W, H, depth, ao, p0, W * H - p0, budget_s=CPU_BUDGET_S,
+                                                 threads=1, root=root, faithful=True)
+    n = len(fb1)
+    res = {
+        "value": float("%.4g" % (cnt["rays_total"] / secs1 / 1e6)),
         "unit": "Mrays/s",
         "cores": 1,
         "kind": "port",
         "seconds": round(secs1, 3),
-        "rays": rays,
-        "all_cores": {"value": float("%.4g" % (rays / secsn / 1e6)), "cores": threads, "seconds": round(secsn, 3)},
-        "cpu": cpu,
-        "sample": sample + ", oracle/rt_oracle.cpp in ref-faithful mode (the reference's arithmetic and "
-                  "per-call work; its cost model checked against the reference binary in the build container, "
-                  "DESIGN.md)",
+        "rays": cnt["rays_total"],
+        "cpu": cpu_model(),
+        "sample": ("%s %dx%d depth=%d AO=%d: exact raster range of the full frame, %d pixel(s) from (0, %d) "
+                   "(rows 0-%d are sky: no AO call precedes, the RNG starts at draw 0 as in the frame); "
+                   "oracle/rt_oracle.cpp in ref-faithful mode (the reference's arithmetic and per-call work)"
+                   % (scene, W, H, depth, ao, n, y0, max(y0 - 1, 0))),
     }
+    parity = None if gpu_px is None else bool((fb1 == gpu_px[p0:p0 + n]).all())
+    if threads > 1 and n > 1:
+        fbn, cntn, secsn = helpers.oracle_time_prefix(scene, W, H, depth, ao, p0, n, threads=threads, root=root,
+                                                      faithful=True)
+        res["all_cores"] = {"value": float("%.4g" % (cntn["rays_total"] / secsn / 1e6)), "cores": threads,
+                            "seconds": round(secsn, 3),
+                            "note": "same pixels; includes the count pass that splitting the serial RNG stream needs"}
+        res["all_cores"]["matches_one_core"] = bool((fbn == fb1).all())
+    res["matches_gpu_frame"] = parity
+    cal = os.path.join(REPO, "profiles", "r03", "cpu_calibration.json")
+    if os.path.exists(cal):
+        c = json.load(open(cal))
+        row = c["scenes"].get(scene[:-5])
+        if row:
+            res["calibration"] = {"port_over_reference": row["port_over_reference"], "cpu": c["cpu"],
+                                  "frame": row["frame"], "file": os.path.relpath(cal, REPO),
+                                  "reference_equiv_value": float("%.4g" % (res["value"] * row["port_over_reference"]))}
+    return res
+
+
+def main():
+    # stdout carries exactly one JSON line: everything else written to fd 1 (the
+    # drop-in's "Scene parsing completed!", RCCL's version banner at communicator
+    # init) goes to stderr; the JSON line goes to the saved original stdout
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--rehearse", action="store_true",
+                    help="--gpus N on a box with fewer GPUs: split the frame N ways on device 0 (device copies)")
+    ap.add_argument("--steps", type=int, default=None, help="default 20 (config2), 2 (synthetic)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 3 (config2), 1 (synthetic)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true", help="skip the north_star sub-record (config2)")
+    ap.add_argument("--no-check", action="store_true", help="skip the reference-hash check of the last frame")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--dist", action="store_true",
+                    help="the multi-rank path (torch.distributed + DistFrame) even with one rank: rehearses the "
+                         "RCCL all-gather/gather and the per-frame host overhead of N>1 on one GPU")
+    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
+    ap.add_argument("--row-sample", type=int, default=1,
+                    help="N=1 only: time rows r = R mod K of the frame (rank R's exact share of a K-way "
+                         "interleaved split; RNG bases from an untimed full-frame count), for huge frames and "
+                         "the per-rank shares of a split")
+    ap.add_argument("--row-rank", type=int, default=0, help="R of --row-sample")
+    args = ap.parse_args()
+    if args.row_sample < 1 or not 0 <= args.row_rank < args.row_sample:
+        raise SystemExit("bench.py: need --row-sample K >= 1 and 0 <= --row-rank < K")
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    synth = WORKLOADS[args.workload][1]
+    steps = args.steps if args.steps is not None else (2 if synth else 20)
+    warmup = args.warmup if args.warmup is not None else (1 if synth else 3)
+
+    ctx = Ctx(args)
+    out = run_workload(ctx, args.workload, steps, warmup, not args.no_cpu_baseline, not args.no_check)
+    if args.workload == "config2" and not args.no_north_star:
+        ns = run_workload(ctx, "field100k_1080p", 5, 2, not args.no_cpu_baseline, False)
+        if out is not None:
+            out["north_star"] = ns
+    if out is not None:
+        print(json.dumps(out), file=json_out, flush=True)
+    if ctx.dist_on:
+        ctx.dist.barrier()
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

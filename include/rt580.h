@@ -221,6 +221,12 @@ int rt580_eval_powf(const float* x_device, float y, float* out_device, uint64_t 
 #define RT_ACCEL_AUTO 1
 int rt_gpu_set_accel(int mode);
 int rt_gpu_accel_active(void);
+/* Largest chunk of the chunked passes of BVH frames (far-hit queue, AO ray
+ * records): 2^log2 rays, log2 in [6, 26] (default 26, or $RT580_CHUNK_LOG2 read
+ * by rt_gpu_init). Larger frames run in several chunks with identical results;
+ * small chunks let the tests reach the multi-chunk paths on small frames.
+ * Synchronizes; applies to the following renders. Test hook. */
+int rt580_set_chunk_log2(int log2);
 /* Counters and HIP-event timings of the last render. */
 int rt_gpu_last_stats(rt_render_stats* stats);
 /* Bench profiling: with enable=1 every following frame records its own HIP
@@ -259,7 +265,7 @@ int rt580_set_ao(rt580_raytracer* rt, int samples, int enabled);
 int rt580_set_rng(rt580_raytracer* rt, int engine);
 int rt580_set_rows(rt580_raytracer* rt, int row_begin, int row_end);
 /* GPUs Render() shards whole frames across (rt_gpu_render_multi); 0 (default):
- * $RT580_GPUS if set, else every visible device. */
+ * $RT580_GPUS if set (an integer in [1, 16], else Render fails), else 1. */
 int rt580_set_gpus(rt580_raytracer* rt, int n);
 const int16_t* rt580_framebuffer(rt580_raytracer* rt); /* Pixel[w*h] */
 int rt580_get_render_params(rt580_raytracer* rt, rt_render_params* out);

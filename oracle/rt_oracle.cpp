@@ -4,6 +4,8 @@
 #include "rt_oracle.h"
 
 #include <atomic>
+#include <chrono>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -841,18 +843,28 @@ extern "C" int oracle_render(const char* assets_root, const char* scene, int w, 
     return 0;
 }
 
-// CPU-baseline timing (bench.py cpu_baseline): Raycast of n listed pixels of the
-// FULL-resolution w x h frame (xy = x0, y0, x1, y1, ...), the reference's per-pixel
-// work (Raytracer.cpp:916-935) on a stratified sample of the workload's own rays.
-// The RNG is positioned at draw 2*ao_n*(y*w + x) (one AO call per earlier pixel):
-// the exact offset would need the whole frame's count pass, and only the position
-// in the draw stream differs (the sample's cost, not its bytes, is measured).
-// Pixels are work items over `threads` threads; counters as oracle_render.
-extern "C" int oracle_time_pixels(const char* assets_root, const char* scene, int w, int h, int depth,
-                                  int ao_samples, int threads, int n, const int32_t* xy, uint64_t* counters) {
-    if (w <= 0 || h <= 0 || depth < 0 || ao_samples <= 0 || n < 0) return 2;
-    for (int i = 0; i < n; i++)
-        if (xy[2 * i] < 0 || xy[2 * i] >= w || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= h) return 2;
+// CPU baseline (bench.py cpu_baseline): the reference's Render loop
+// (Raytracer.cpp:921-932) over an exact raster range of the FULL-resolution
+// w x h frame, pixels [p0, p0 + n), with the serial RNG stream positioned at
+// the absolute AO-call index call_base (draw 2 * ao_n * call_base; 0 for a
+// range that no AO call precedes, e.g. one starting below the sky rows).
+//  threads == 1: one serial stream, pixel after pixel, as the reference does;
+//    stops after max_pixels pixels or once budget_s seconds have passed (checked
+//    after each pixel) -> *n_done.
+//  threads > 1: exactly max_pixels pixels on `threads` threads: a count pass
+//    (AO calls per pixel, the work the serial stream needs to be split), the
+//    exclusive scan, then the pixels as work items.
+// fb receives the range's int16 pixels (n_done x 3); counters as oracle_render
+// (the count pass's rays are not counted: they are overhead of the split);
+// *seconds the render time (scene load excluded, as Render() excludes it).
+extern "C" int oracle_time_prefix(const char* assets_root, const char* scene, int w, int h, int depth,
+                                  int ao_samples, int threads, int64_t p0, int64_t max_pixels, double budget_s,
+                                  uint64_t call_base, int16_t* fb, uint64_t* counters, int64_t* n_done,
+                                  double* seconds) {
+    const int64_t npix = (int64_t)w * h;
+    if (w <= 0 || h <= 0 || depth < 0 || ao_samples <= 0 || p0 < 0 || max_pixels < 0 || p0 + max_pixels > npix ||
+        threads < 1 || !fb || !n_done)
+        return 2;
     Scene sc;
     if (load_scene(sc, assets_root, scene) != 0) return 1;
     for (const Shape& s : sc.shapes)
@@ -866,32 +878,69 @@ extern "C" int oracle_time_pixels(const char* assets_root, const char* scene, in
     tr.ao_bmax = (float)(2 * kPI);
     tr.n_amb = 0;
     for (auto& l : sc.lights) tr.n_amb += l.type == LAMB;
-    if (threads <= 0) threads = default_threads();
     DrawSource src;
     src.engine = 0;
-    std::vector<Counters> pc((size_t)n);
-    std::atomic<int> next{0};
-    auto work = [&] {
-        RngCursor rng;
-        rng.src = &src;
-        for (;;) {
-            const int i = next.fetch_add(1);
-            if (i >= n) break;
-            const int x = xy[2 * i], y = xy[2 * i + 1];
-            rng.seek(2ull * (uint64_t)ao_samples * ((uint64_t)y * w + x));
-            Counters& c = pc[(size_t)i];
-            c.primary++;
-            (void)tr.raycast(generate_ray(cam, x, y), depth, &rng, c, false);
-        }
-    };
-    std::vector<std::thread> th;
-    for (int t = 0; t < threads; t++) th.emplace_back(work);
-    for (auto& t : th) t.join();
+    const uint64_t per_call = 2ull * (uint64_t)ao_samples;
     Counters tot;
-    for (const Counters& c : pc) {
+    auto add = [&tot](const Counters& c) {
         tot.primary += c.primary; tot.secondary += c.secondary; tot.shadow += c.shadow;
         tot.ao += c.ao; tot.ao_calls += c.ao_calls;
+    };
+    auto put = [fb, p0](int64_t i, const Pix& p) {
+        int16_t* o = fb + (size_t)(i - p0) * 3;
+        o[0] = p.r; o[1] = p.g; o[2] = p.b;
+    };
+    int64_t done = 0;
+    const auto t_start = std::chrono::steady_clock::now();
+    if (threads == 1) {
+        RngCursor rng;
+        rng.src = &src;
+        rng.seek(call_base * per_call);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int64_t i = p0; i < p0 + max_pixels; i++) {
+            Counters c;
+            c.primary++;
+            put(i, tr.raycast(generate_ray(cam, (int)(i % w), (int)(i / w)), depth, &rng, c, false));
+            add(c);
+            done++;
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >= budget_s) break;
+        }
+    } else {
+        std::vector<uint64_t> base((size_t)max_pixels + 1, 0);
+        std::vector<Counters> pc((size_t)max_pixels);
+        std::atomic<int64_t> next{0};
+        auto count = [&] {
+            for (int64_t k; (k = next.fetch_add(1)) < max_pixels;) {
+                Counters c;
+                tr.raycast(generate_ray(cam, (int)((p0 + k) % w), (int)((p0 + k) / w)), depth, nullptr, c, true);
+                base[(size_t)k + 1] = c.ao_calls;
+            }
+        };
+        auto shade = [&] {
+            RngCursor rng;
+            rng.src = &src;
+            for (int64_t k; (k = next.fetch_add(1)) < max_pixels;) {
+                rng.seek((call_base + base[(size_t)k]) * per_call);
+                Counters& c = pc[(size_t)k];
+                c.primary++;
+                put(p0 + k, tr.raycast(generate_ray(cam, (int)((p0 + k) % w), (int)((p0 + k) / w)), depth, &rng, c,
+                                       false));
+            }
+        };
+        auto run = [&](const std::function<void()>& fn) {
+            next = 0;
+            std::vector<std::thread> th;
+            for (int t = 0; t < threads; t++) th.emplace_back(fn);
+            for (auto& t : th) t.join();
+        };
+        run(count);
+        for (size_t k = 0; k < (size_t)max_pixels; k++) base[k + 1] += base[k];
+        run(shade);
+        for (const Counters& c : pc) add(c);
+        done = max_pixels;
     }
+    *n_done = done;
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     if (counters) {
         counters[0] = tot.primary + tot.secondary + tot.shadow + tot.ao;
         counters[1] = tot.primary; counters[2] = tot.secondary; counters[3] = tot.shadow;

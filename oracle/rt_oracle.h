@@ -46,6 +46,15 @@ int oracle_shade_rows(const char* assets_root, const char* scene, int w, int h, 
                       int ao_enabled, int row_begin, int row_step, int n_rows, const uint64_t* row_base,
                       int16_t* fb);
 
+// CPU baseline: the reference's raster loop over pixels [p0, p0 + n) of the
+// full w x h frame with the RNG at AO-call index call_base; threads == 1: one
+// serial stream, stopping after max_pixels or budget_s seconds (*n_done);
+// threads > 1: exactly max_pixels pixels (count pass, scan, shade). fb:
+// n_done * 3 int16; *seconds: render time, load excluded. See rt_oracle.cpp.
+int oracle_time_prefix(const char* assets_root, const char* scene, int w, int h, int depth, int ao_samples,
+                       int threads, int64_t p0, int64_t max_pixels, double budget_s, uint64_t call_base,
+                       int16_t* fb, uint64_t* counters, int64_t* n_done, double* seconds);
+
 // 0 = hoisted (default), 1 = ref-faithful cost model (see above). Process-global.
 int oracle_set_mode(int faithful);
 

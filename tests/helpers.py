@@ -149,22 +149,30 @@ def oracle_render(scene, w, h, depth, ao_samples=128, ao_enabled=True, engine=0,
     return fb, dict(zip(keys, (int(x) for x in cnt)))
 
 
-def oracle_time_pixels(scene, w, h, depth, ao_samples, pixels, threads=0, root=ASSETS_ROOT, faithful=True):
-    """CPU-baseline timing: Raycast of the listed (x, y) pixels of the full w x h
-    frame (oracle_time_pixels; RNG at an estimated offset) -> counters dict."""
+def oracle_time_prefix(scene, w, h, depth, ao_samples, p0, max_pixels, budget_s=1e30, threads=1, call_base=0,
+                       root=ASSETS_ROOT, faithful=True):
+    """CPU baseline: the reference's raster loop over pixels [p0, p0 + n) of the
+    full w x h frame, RNG at AO-call index call_base (oracle_time_prefix).
+    threads == 1: serial, stops after max_pixels or budget_s seconds;
+    threads > 1: exactly max_pixels pixels. -> (int16 (n, 3) pixels, counters, render seconds
+    without the scene load)."""
     lib = oracle_lib()
-    lib.oracle_time_pixels.restype = ctypes.c_int
-    lib.oracle_time_pixels.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 6 + \
-        [ctypes.c_void_p, ctypes.c_void_p]
-    xy = np.asarray(pixels, dtype=np.int32).reshape(-1)
+    f = lib.oracle_time_prefix
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 5 + \
+        [ctypes.c_int64, ctypes.c_int64, ctypes.c_double, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p]
+    fb = np.zeros((max_pixels, 3), dtype=np.int16)
     cnt = np.zeros(6, dtype=np.uint64)
+    done = ctypes.c_int64(0)
+    secs = ctypes.c_double(0)
     lib.oracle_set_mode(1 if faithful else 0)
-    st = lib.oracle_time_pixels(os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples, threads,
-                                len(xy) // 2, xy.ctypes.data, cnt.ctypes.data)
+    st = f(os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples, threads, p0, max_pixels, budget_s,
+           call_base, fb.ctypes.data, cnt.ctypes.data, ctypes.byref(done), ctypes.byref(secs))
     lib.oracle_set_mode(0)
-    assert st == 0, "oracle_time_pixels failed"
+    assert st == 0, "oracle_time_prefix failed"
     keys = ["rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"]
-    return dict(zip(keys, (int(x) for x in cnt)))
+    return fb[:done.value], dict(zip(keys, (int(x) for x in cnt))), secs.value
 
 
 @functools.lru_cache(None)

@@ -105,3 +105,17 @@ def test_reference_main_with_two_gpus(tmp_path):
     assert p.returncode == 0, p.stderr
     want = next(e for e in helpers.golden_entries(False) if e["name"] == "main_500_d4_ao128")["sha256"]
     assert helpers.sha256(open(os.path.join(cwd, "output.ppm"), "rb").read()) == want
+
+
+def test_render_multi_follows_scene_and_device_set():
+    """Consecutive split frames with different device sets (G = 3, 2, 3) and a
+    new scene in between: the other contexts are refreshed from context 0 (the
+    scene is replicated by device copies, never rebuilt) and every frame equals
+    the single-GPU render of its scene."""
+    root = helpers.synthetic_root("cornell10k")
+    a = ("cornell10k.json", 40, 24, 3, 8, root)
+    b = ("scene.json", 40, 30, 2, 8, helpers.ASSETS_ROOT)
+    for (scene, w, h, depth, ao, r), G in ((a, 3), (a, 2), (b, 3), (a, 3)):
+        full, _ = render_gpu(scene, w, h, depth, ao, True, root=r)
+        got = _multi(scene, w, h, depth, ao, G, root=r)
+        assert np.array_equal(got, full), (scene, G)

@@ -66,13 +66,30 @@ def test_scene_fixtures_are_the_reference_assets():
         assert filecmp.cmp(os.path.join(ref, f), os.path.join(helpers.GOLDEN, "Assets", f), shallow=False), f
 
 
-def test_time_pixels_counts_the_frames_rays():
-    """bench.py's CPU-baseline sampler (oracle_time_pixels: listed pixels of the
-    full frame) traces exactly the rays oracle_render traces for those pixels,
-    in both cost modes (only the RNG position differs, not the work)."""
-    w, h = 24, 18
-    _, want = helpers.oracle_render("simpleSphereScene.json", w, h, 4, 8, True)
-    pts = [(x, y) for y in range(h) for x in range(w)]
-    for faithful in (False, True):
-        got = helpers.oracle_time_pixels("simpleSphereScene.json", w, h, 4, 8, pts, threads=4, faithful=faithful)
-        assert got == want
+@pytest.mark.parametrize("p0,n", [(0, 24 * 18), (24 * 5 + 7, 100)])
+def test_time_prefix_is_the_frames_pixels(p0, n):
+    """bench.py's CPU-baseline timer (oracle_time_prefix: an exact raster range of
+    the full frame with the RNG at the range's AO-call base) gives exactly the
+    frame's pixels and rays, serially (the reference's loop, ref-faithful cost
+    model) and split over threads (count pass, scan, shade)."""
+    w, h, d, ao = 24, 18, 4, 8
+    full, _ = helpers.oracle_render("simpleSphereScene.json", w, h, d, ao, True)
+    calls = []
+    for y in range(h):  # AO calls per pixel of the frame (raster order)
+        cnt = helpers.oracle_render("simpleSphereScene.json", w, h, d, ao, True, rows=(y, y + 1))[1]
+        calls.append(cnt["ao_calls"])
+    # the base of p0 from per-row counts + the pixels of p0's row before it
+    y0, x0 = divmod(p0, w)
+    base = sum(calls[:y0])
+    if x0:
+        part = helpers.oracle_time_prefix("simpleSphereScene.json", w, h, d, ao, y0 * w, x0, faithful=False)[1]
+        base += part["ao_calls"]
+    want = full.reshape(-1, 3)[p0:p0 + n]
+    for faithful, threads in ((True, 1), (False, 1), (False, 4)):
+        fb, cnt, _ = helpers.oracle_time_prefix("simpleSphereScene.json", w, h, d, ao, p0, n, threads=threads,
+                                                call_base=base, faithful=faithful)
+        assert fb.shape == want.shape and (fb == want).all(), (faithful, threads)
+        assert cnt["rays_primary"] == n
+    # the serial timer stops at its budget
+    fb, cnt, _ = helpers.oracle_time_prefix("simpleSphereScene.json", w, h, d, ao, 0, w * h, budget_s=0.0)
+    assert len(fb) == 1 and cnt["rays_primary"] == 1

@@ -9,7 +9,7 @@ shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="python3 bench.py --no-cpu-baseline $*"
+BENCH="python3 bench.py --no-cpu-baseline --no-north-star $*"
 case "$*" in *--steps*) ;; *) BENCH="$BENCH --steps 3 --warmup 1";; esac
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o trace -- $BENCH > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 1; }
 i=0
