@@ -94,7 +94,14 @@ struct DevWork {
     uint32_t* far_keys_alt;
     uint32_t* far_vals;    // [far_cap] x2 (ray index, sorted)
     uint32_t* far_vals_alt;
-    uint32_t* far_count;   // [1]
+    uint32_t* far_count;   // [2]: queued rays, of which far-origin (brute scan)
+    // the sorted queue in segments of one key (run-length encoding into
+    // far_keys / far_vals, then offsets): far_seg_off[k] = first sorted ray of
+    // segment k; work items = chunks of <= 64 rays of one segment
+    uint32_t* far_seg_off; // [far_cap]
+    uint32_t* far_seg_n;   // [2]: segments, work items (chunks of <= 64 rays of one segment)
+    uint32_t* far_wofs;    // [far_cap] first work item of each segment
+    uint4* far_work;       // [far_cap + far_cap / 64 + 64] work items: sorted rays [x, y), cell list at z, w entries
     uint32_t* far_count_host;  // pinned
     void* sort_tmp;
     size_t sort_tmp_bytes;
@@ -137,7 +144,7 @@ hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, c
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s);
 // The launcher step that ran last (for error messages).
 const char* launch_where();
-// Temporary storage of the far-queue radix sort for `cap` rays.
+// Temporary storage of the far-queue radix sort / run-length encoding / scan for `cap` rays.
 size_t far_sort_tmp_bytes(uint32_t cap);
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s);
 hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* out,

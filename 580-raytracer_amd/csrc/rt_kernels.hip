@@ -357,10 +357,13 @@ __device__ __forceinline__ void block_alloc2(uint32_t* counter, bool fa, bool fb
     sb = base + na + (uint32_t)__popcll(mb & lt);
 }
 
-// Octahedral direction key (12 + 12 bits): groups rays of similar direction
-// for the far-hit passes (grouping only; never affects a result).
-#define RT_DIR_KEY_BITS 25
-#define RT_KEY_BRUTE (1u << 24)  // far-origin rays: brute-force scan, sorted after every direction key
+// Sort keys of the far-hit queues (grouping only; never affects a result):
+// grid-origin rays: their direction-grid cell (< 2^24, rt_isect.h grid_cell,
+// scaled to 24 bits); plane-tree rays: RT_KEY_TREE | a 12 + 12-bit octahedral
+// direction key; far-origin rays (brute scan): RT_KEY_BRUTE, sorted last.
+#define RT_DIR_KEY_BITS 26
+#define RT_KEY_TREE (1u << 24)
+#define RT_KEY_BRUTE (1u << 25)
 
 // Rays whose origin is so far out (a child of one of the reference's far hits)
 // that a typical triangle cannot be culled (T <= 0) or the fat-ray margin
@@ -373,11 +376,11 @@ __device__ __forceinline__ bool far_origin(const DevScene& S, rv3 o) {
 }
 __device__ __forceinline__ uint32_t dir_key(rv3 d);
 // Sort key of a far-pass ray: its direction-grid cell (rays of one cell are
-// then contiguous: waves share a cell list) when the origin uses the grid,
-// else the 4096^2 direction key. Below RT_KEY_BRUTE.
+// then contiguous: one candidate list serves them all) when the origin uses
+// the grid, else RT_KEY_TREE | the 4096^2 direction key. Below RT_KEY_BRUTE.
 __device__ __forceinline__ uint32_t far_key(const BvhView& V, rv3 o, rv3 d) {
     if (grid_origin(V, o)) return grid_cell(d, V.grid_log2) << (24 - 2 * V.grid_log2);
-    return dir_key(d);
+    return RT_KEY_TREE | dir_key(d);
 }
 __device__ __forceinline__ uint32_t dir_key(rv3 d) {
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
@@ -1430,6 +1433,17 @@ static int near_wpe() {
 // after the other instead: field1m AO 2.26 -> 5.54 s -- waves hold many.)
 // Each candidate gets far_candidate + the full reference test. Must be called
 // by the whole wave.
+#ifdef RT580_DIAGNOSTICS
+// DIAGNOSTIC build only: far_any_kernel statistics -- rays, grid rays, uniform
+// waves, per-lane waves, lanes' list entries, lock-step list steps (per wave:
+// the longest lane list / U), plane-tree rays, candidates passing
+// far_candidate, full tests that hit
+__device__ unsigned long long g_far_stats[9];
+#define RT_FAR_STAT(k, v) atomicAdd(&g_far_stats[k], (unsigned long long)(v))
+#else
+#define RT_FAR_STAT(k, v) ((void)0)
+#endif
+
 template <bool CLOSEST, int U = 1>
 __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o, rv3 d, const FarRay& fr, Hit& h,
                                               bool& found, FarTri* tile) {
@@ -1439,6 +1453,7 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
     auto test = [&](bool on, const FarTri& ft) {
         if (!(on && !(CLOSEST ? false : hit))) return;
         if (!far_candidate(ft, fr, o, d)) return;
+        if (!CLOSEST) RT_FAR_STAT(7, 1);
         const rt_prim P = load_prim_scalar(S.prims, (int)__builtin_amdgcn_readfirstlane(ft.id));
         if (CLOSEST) {
             float t, a, b, g;
@@ -1460,6 +1475,16 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
         c0 = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)cell, __ffsll((unsigned long long)glm) - 1));
         uniform = __ballot(gl && cell != c0) == 0;
     }
+#ifdef RT580_DIAGNOSTICS
+    if (!CLOSEST && glm && lane == (uint32_t)(__ffsll((unsigned long long)glm) - 1)) RT_FAR_STAT(uniform ? 2 : 3, 1);
+    if (!CLOSEST && gl) {
+        const uint32_t len = V.grid_start[cell + 1] - V.grid_start[cell];
+        RT_FAR_STAT(4, len);
+        uint32_t mx = len;
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+        if (lane == (uint32_t)(__ffsll((unsigned long long)glm) - 1)) RT_FAR_STAT(5, uniform ? (mx + 63) / 64 : (mx + U - 1) / U);
+    }
+#endif
     if (uniform) {
         const bool mine = gl;
         const uint32_t b = V.grid_start[c0], e = V.grid_start[c0 + 1];
@@ -1495,6 +1520,7 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
             if (k0 + u >= e || !(CLOSEST || !hit)) continue;
             const FarTri& ft = fts[u];
             if (!far_candidate(ft, fr, o, d)) continue;
+            if (!CLOSEST) RT_FAR_STAT(7, 1);
             const rt_prim P = S.prims[ft.id];
             if (CLOSEST) {
                 float t, a, bb, g;
@@ -1526,6 +1552,135 @@ __device__ __forceinline__ void any_hit_out(const DevWork& W, uint8_t* flag, uin
     else atomicAdd(&W.occ[tag], 1u);
 }
 
+// The plane-tree far search of the live lanes (bvh_any's far part): the wave
+// walks the tree once for all of them (a node is entered if any live lane may
+// have a far hit below it; node index wave-uniform), each lane evaluating the
+// exact tests for its own ray. stk: the wave's LDS stack. Whole wave.
+__device__ __forceinline__ bool far_tree_any_wave(const DevScene& S, bool live, rv3 o, rv3 d, const FarRay& fr,
+                                                  int32_t* stk) {
+    bool hit = false;
+    int sp = 0;
+    stk[sp++] = 0;  // every lane writes the same value: no cross-lane ordering needed
+    while (sp > 0) {
+        if (__ballot(live) == 0) break;
+        const int node = __builtin_amdgcn_readfirstlane(stk[--sp]);
+        const FarNode fn = load_far_node(S.bv.far_nodes, node);
+        float T;
+        const bool may = live && far_node_may(fn, fr, o, d, T);
+        if (__ballot(may) == 0) continue;
+        if (fn.count == 0) {
+            stk[sp++] = fn.first + 1;
+            stk[sp++] = fn.first;
+            continue;
+        }
+        for (int k = fn.first; k < fn.first + fn.count; k++) {
+            const FarTri ft = load_far_tri(S.bv.far_tris, k);
+            bool cand = may && live && far_candidate(ft, fr, o, d);
+            if (__ballot(cand) == 0) continue;
+            const rt_prim P = load_prim_scalar(S.prims, (int)ft.id);
+            if (cand && prim_test_any(P, o, d)) {
+                hit = true;
+                live = false;
+            }
+        }
+    }
+    return hit;
+}
+
+// Cell-major any-hit far pass over the sorted queue [0, n) (far-origin rays
+// excluded), cut into segments of one sort key (far_seg_off / far_keys, see
+// launch_far_cells). A wave takes a segment: a grid cell's rays share one
+// candidate list (rt_bvh.h build_dir_grid), so the list is read once per
+// segment, not once per ray. The wave stages up to 64 of the segment's rays in
+// LDS; the lanes hold candidates (the "always" entries, then the cell's list;
+// lists shorter than 64 are replicated 64 / Lp times, Lp = the list length
+// rounded up to a power of two, so each step tests 64 / Lp rays) and step
+// through the staged rays: far_candidate, then the full reference test
+// (prim_test_any) -- the tests far_any / far_grid_lane make, on the same pairs.
+// A plane-tree segment (RT_KEY_TREE keys) runs far_tree_any_wave over its
+// staged rays instead. Hit rays: any_hit_out. A wave's work item is one chunk
+// of <= 64 rays of one segment (a directional light's shadow rays all share a
+// cell); grid-stride over the work items (their count is read on the device).
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
+far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
+    __shared__ float4 sray[TB / 64][64][2];
+    __shared__ uint32_t shit[TB / 64][64];
+    __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
+    const BvhView& V = S.bv;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t nwork = W.far_seg_n[1];
+    for (uint32_t w = blockIdx.x * (TB / 64) + wave; w < nwork; w += gridDim.x * (TB / 64)) {
+        // the work item: sorted rays [r0, r1) of one segment and its cell's candidate list
+        const uint4 wd = W.far_work[w];
+        const uint32_t r0 = __builtin_amdgcn_readfirstlane(wd.x), r1 = __builtin_amdgcn_readfirstlane(wd.y);
+        const uint32_t lb = __builtin_amdgcn_readfirstlane(wd.z), lw = __builtin_amdgcn_readfirstlane(wd.w);
+        const bool tree = lw == 0xffffffffu;
+        const uint32_t n_list = tree ? 0u : lw;
+        const int n_cand = V.n_always + (int)n_list;
+        if (!tree && n_cand == 0) continue;  // no candidate: no far hit in this cell
+        {
+            const uint32_t rc = r0;
+            const uint32_t nr = r1 - rc < 64u ? r1 - rc : 64u;
+            rv3 o = v3(0, 0, 0), d = v3(1, 0, 0);
+            FarRay fr;
+            fr.R = 0.0f;
+            uint32_t call = 0;
+            // the previous chunk's LDS reads are done before it is overwritten
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if ((uint32_t)lane < nr) {
+                const uint32_t q = W.far_vals_alt[rc + lane];
+                float4 a = W.far_rays[2 * (size_t)q], b = W.far_rays[2 * (size_t)q + 1];
+                o = v3(a.x, a.y, a.z);
+                d = v3(b.x, b.y, b.z);
+                call = __float_as_uint(a.w);
+                fr = far_ray(V, o);
+                b.w = fr.R;
+                sray[wave][lane][0] = a;
+                sray[wave][lane][1] = b;
+                shit[wave][lane] = 0u;
+            }
+            bool hit = false;
+            if (tree) {
+                hit = far_tree_any_wave(S, (uint32_t)lane < nr, o, d, fr, stk[wave]);
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                for (int kc = 0; kc < n_cand; kc += 64) {
+                    const int lt = n_cand - kc < 64 ? n_cand - kc : 64;
+                    const int lg = lt > 32 ? 6 : lt > 16 ? 5 : lt > 8 ? 4 : lt > 4 ? 3 : lt > 2 ? 2 : lt > 1 ? 1 : 0;
+                    const int kk = lane & ((1 << lg) - 1), g = lane >> lg;
+                    const bool has = kk < lt;
+                    FarTri ft;
+                    if (has) {
+                        const int k = kc + kk - V.n_always;
+                        ft = V.far_tris[k < 0 ? V.grid_always[k + V.n_always] : V.grid_items[lb + (uint32_t)k]];
+                    }
+                    const uint32_t step = 64u >> lg;
+                    for (uint32_t j0 = 0; j0 < nr; j0 += step) {
+                        const uint32_t j = j0 + (uint32_t)g;
+                        if (!has || j >= nr || shit[wave][j] != 0u) continue;
+                        const float4 a = sray[wave][j][0], b = sray[wave][j][1];
+                        const rv3 oj = v3(a.x, a.y, a.z), dj = v3(b.x, b.y, b.z);
+                        FarRay fj;
+                        fj.R = b.w;
+                        if (far_candidate(ft, fj, oj, dj) && prim_test_any(S.prims[ft.id], oj, dj)) shit[wave][j] = 1u;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                hit = (uint32_t)lane < nr && shit[wave][lane] != 0u;
+            }
+            RT_FAR_STAT(0, (uint32_t)lane < nr ? 1 : 0);
+            RT_FAR_STAT(8, hit ? 1 : 0);
+            if (hit) any_hit_out(W, flag, call);
+        }
+    }
+}
+
 template <int U = 1>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
 far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
@@ -1549,37 +1704,17 @@ far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
         bool hit = false;
         {
             const bool gl = live && grid_origin(S.bv, o);
+            RT_FAR_STAT(0, live ? 1 : 0);
+            RT_FAR_STAT(1, gl ? 1 : 0);
+            RT_FAR_STAT(6, live && !gl ? 1 : 0);
             Hit hd;
             bool fd = false;
             if (far_grid_lane<false, U>(S, gl, o, d, fr, hd, fd, ftile[wave])) hit = true;
             if (gl) live = false;  // done: the tree walk below serves the other lanes
         }
-        int sp = 0;
-        stk[wave][sp++] = 0;  // every lane writes the same value: no cross-lane ordering needed
-        while (sp > 0) {
-            if (__ballot(live) == 0) break;
-            const int node = __builtin_amdgcn_readfirstlane(stk[wave][--sp]);
-            const FarNode fn = load_far_node(S.bv.far_nodes, node);
-            float T;
-            const bool may = live && far_node_may(fn, fr, o, d, T);
-            if (__ballot(may) == 0) continue;
-            if (fn.count == 0) {
-                stk[wave][sp++] = fn.first + 1;
-                stk[wave][sp++] = fn.first;
-                continue;
-            }
-            for (int k = fn.first; k < fn.first + fn.count; k++) {
-                const FarTri ft = load_far_tri(S.bv.far_tris, k);
-                bool cand = may && live && far_candidate(ft, fr, o, d);
-                if (__ballot(cand) == 0) continue;
-                const rt_prim P = load_prim_scalar(S.prims, (int)ft.id);
-                if (cand && prim_test_any(P, o, d)) {
-                    hit = true;
-                    live = false;
-                }
-            }
-        }
+        if (far_tree_any_wave(S, live, o, d, fr, stk[wave])) hit = true;
         if (hit) any_hit_out(W, flag, call);
+        RT_FAR_STAT(8, hit ? 1 : 0);
     }
 }
 
@@ -1820,16 +1955,17 @@ static int brute_split() {
     return v;
 }
 
-// Far-pass flavour for a queue of nq rays: 1 = wave union (sorted, dense
-// queues), 2 = per lane, 3 = scan. RT580_FAR_MODE overrides the size rule (A/B only).
+// Far-pass flavour for a queue of nq rays: 4 = cell-major segments (any-hit
+// passes), 1 = wave union per 64 sorted rays, 2 = per lane, 3 = scan.
+// RT580_FAR_MODE overrides (A/B only; the closest-hit passes use 1 for 4).
 static int far_mode(uint32_t nq) {
     static int forced = -1;
     if (forced < 0) {
         const char* e = getenv("RT580_FAR_MODE");
-        forced = e ? atoi(e) : 0;
+        forced = e ? atoi(e) : 4;
     }
-    if (forced >= 1 && forced <= 3) return forced;
-    return 1;
+    if (forced >= 1 && forced <= 4) return forced;
+    return 4;
 }
 
 // Queued tree rays of a BVH trace level (sorted by direction key): the far part
@@ -2098,6 +2234,98 @@ static void launch_far_any(const DevScene& S, const DevWork& W, uint32_t n, uint
 }
 
 
+// RT580_PROGRESS=1: a stderr line per trace level / AO chunk of the BVH path
+// (those already synchronize), so multi-minute frames show progress.
+static void progress(const char* fmt, ...) {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("RT580_PROGRESS");
+        on = e && atoi(e) > 0;
+    }
+    if (!on) return;
+    va_list ap;
+    va_start(ap, fmt);
+    fprintf(stderr, "[rt580] ");
+    vfprintf(stderr, fmt, ap);
+    fprintf(stderr, "\n");
+    fflush(stderr);
+    va_end(ap);
+}
+
+// Which launcher step failed last (error messages of the shim).
+static const char* g_where = "";
+const char* launch_where() { return g_where; }
+#define RT_STEP(what) (g_where = (what))
+
+// Work items of the cell pass: segment k (W.far_vals[k] rays) is cut into
+// ceil(count / 64) chunks; chunk counts first (into far_keys_alt, free after
+// the run-length encoding), then, after their scan into far_wofs, one entry
+// per chunk naming its segment, and the total.
+__global__ void far_chunk_count_kernel(DevWork W, uint32_t nseg) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nseg; k += gridDim.x * blockDim.x)
+        W.far_keys_alt[k] = (W.far_vals[k] + 63u) / 64u;
+}
+// One descriptor per work item (sorted rays [x, y), the cell list's first
+// entry z and length w; w = ~0: a plane-tree segment), so the cell pass reads
+// one record per item instead of a chain of lookups.
+__global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    const int shift = 24 - 2 * S.bv.grid_log2;
+    for (uint32_t k = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < nseg;
+         k += gridDim.x * (blockDim.x / 64)) {
+        const uint32_t b = W.far_wofs[k], c = W.far_keys_alt[k], key = W.far_keys[k];
+        const uint32_t s0 = W.far_seg_off[k], s1 = k + 1 < nseg ? W.far_seg_off[k + 1] : n;
+        uint32_t lb = 0, lw = 0xffffffffu;
+        if (key < RT_KEY_TREE) {
+            const uint32_t cell = key >> shift;
+            lb = S.bv.grid_start[cell];
+            lw = S.bv.grid_start[cell + 1] - lb;
+        }
+        for (uint32_t j = lane; j < c; j += 64) {
+            const uint32_t r0 = s0 + 64u * j;
+            W.far_work[b + j] = make_uint4(r0, s1 - r0 < 64u ? s1 : r0 + 64u, lb, lw);
+        }
+        if (k == nseg - 1 && lane == 0) W.far_seg_n[1] = b + c;
+    }
+}
+
+// The any-hit far pass over the sorted queue [0, n) (far-origin rays
+// excluded): segments of one key (run-length encoding of the sorted keys into
+// far_keys / far_vals -- the sort's inputs, free now -- and the exclusive scan
+// of the run lengths), their chunks of <= 64 rays as work items, then
+// far_cell_any_kernel. One host read (the segment count).
+static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s) {
+    size_t tmp = W.sort_tmp_bytes;
+    RT_STEP("far queue segments");
+    hipError_t e = hipcub::DeviceRunLengthEncode::Encode(W.sort_tmp, tmp, W.far_keys_alt, W.far_keys, W.far_vals,
+                                                         W.far_seg_n, (int)n, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(W.far_count_host + 2, W.far_seg_n, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    const uint32_t nseg = W.far_count_host[2];
+    if (nseg == 0) return hipSuccess;
+    tmp = W.sort_tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(W.sort_tmp, tmp, W.far_vals, W.far_seg_off, (int)nseg, s)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(far_chunk_count_kernel, dim3(grid_for(nseg, 4096)), dim3(TB), 0, s, W, nseg);
+    tmp = W.sort_tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(W.sort_tmp, tmp, W.far_keys_alt, W.far_wofs, (int)nseg, s)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(far_chunk_expand_kernel, dim3(grid_for((uint64_t)nseg * 64, 16384)), dim3(TB), 0, s, S, W, nseg,
+                       n);
+    RT_STEP("far cell pass");
+    hipLaunchKernelGGL(far_cell_any_kernel, dim3(grid_for((uint64_t)(n / 64 + nseg) * 64, 16384)), dim3(TB), 0, s, S,
+                       W, n, flag);
+#ifdef RT580_DIAGNOSTICS
+    {
+        uint32_t nw[2] = {0, 0};
+        if (hipMemcpyAsync(nw, W.far_seg_n, 8, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess)
+            progress("far cell pass: rays %u segments %u work items %u", n, nw[0], nw[1]);
+    }
+#endif
+    return hipGetLastError();
+}
+
 __constant__ uint8_t c_gamma_lut[256];
 
 __global__ void gamma_u8_kernel(const int16_t* __restrict__ fb, uint64_t n, uint8_t* __restrict__ out) {
@@ -2307,28 +2535,6 @@ void kernel_timer_release() {
     g_kt = KernelTimer();
 }
 
-// Which launcher step failed last (error messages of the shim).
-static const char* g_where = "";
-const char* launch_where() { return g_where; }
-#define RT_STEP(what) (g_where = (what))
-
-// RT580_PROGRESS=1: a stderr line per trace level / AO chunk of the BVH path
-// (those already synchronize), so multi-minute frames show progress.
-static void progress(const char* fmt, ...) {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("RT580_PROGRESS");
-        on = e && atoi(e) > 0;
-    }
-    if (!on) return;
-    va_list ap;
-    va_start(ap, fmt);
-    fprintf(stderr, "[rt580] ");
-    vfprintf(stderr, fmt, ap);
-    fprintf(stderr, "\n");
-    fflush(stderr);
-    va_end(ap);
-}
 
 // Sort the far queue (W.far_count entries) by direction key; returns its length.
 static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
@@ -2433,7 +2639,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 if (nq) {
                     RT_STEP("trace far pass");
                     const int fm = far_mode(nq);
-                    if (fm == 1)
+                    if (fm == 1 || fm == 4)
                         hipLaunchKernelGGL(far_closest_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
                     else if (fm == 2)
                         hipLaunchKernelGGL(far_closest_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
@@ -2464,7 +2670,11 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         }
                         if (sq) {
                             RT_STEP("trace shadow far pass");
-                            launch_far_any(S, W, sq, flags, s);
+                            if (far_mode(sq) == 4) {
+                                if ((e = launch_far_cells(S, W, sq, flags, s)) != hipSuccess) return e;
+                            } else {
+                                launch_far_any(S, W, sq, flags, s);
+                            }
                             if ((e = hipGetLastError()) != hipSuccess) return e;
                         }
                     }
@@ -2503,10 +2713,13 @@ hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, c
 }
 
 size_t far_sort_tmp_bytes(uint32_t cap) {
-    size_t bytes = 0;
+    size_t bytes = 0, rle = 0, scan = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, 0, RT_DIR_KEY_BITS);
-    return bytes;
+    (void)hipcub::DeviceRunLengthEncode::Encode(nullptr, rle, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap);
+    return std::max(bytes, std::max(rle, scan));
 }
 
 static int ao_variant() {
@@ -2656,7 +2869,9 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
 #endif
             if (nq == 0) continue;
             const int fm = far_mode(nq);
-            if (fm == 1)
+            if (fm == 4) {
+                if ((e = launch_far_cells(S, W, nq, (uint8_t*)nullptr, s)) != hipSuccess) return e;
+            } else if (fm == 1)
                 launch_far_any(S, W, nq, (uint8_t*)nullptr, s);
             else if (fm == 2)
                 hipLaunchKernelGGL(far_any_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq,
@@ -2664,6 +2879,17 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             else
                 hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nq * 64, 16384)), dim3(TB), 0, s, S, W,
                                    0u, nq, 0, (int)S.bv.n_far, 0, (uint8_t*)nullptr);
+#ifdef RT580_DIAGNOSTICS
+            {
+                unsigned long long st[9];
+                if (hipMemcpyFromSymbolAsync(st, HIP_SYMBOL(g_far_stats), sizeof st, 0, hipMemcpyDeviceToHost, s) ==
+                        hipSuccess &&
+                    hipStreamSynchronize(s) == hipSuccess)
+                    progress("far_any so far: rays %llu grid %llu uniform waves %llu lane waves %llu list entries %llu "
+                             "lock-step steps %llu tree rays %llu candidates %llu hits %llu",
+                             st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8]);
+            }
+#endif
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         return hipSuccess;

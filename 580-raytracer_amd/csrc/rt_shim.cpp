@@ -80,7 +80,8 @@ struct State {
     bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
     // BVH far-queue buffers (BVH frames always run serialized on slot 0)
     DevBuf ao_rays, ao_late, ao_late_count;
-    DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim, shadow;
+    DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim, shadow,
+        far_seg_off, far_seg_n, far_wofs, far_work;
     uint32_t* far_count_host = nullptr;  // pinned
     uint32_t far_cap = 0;
     uint32_t ao_cap = 0;
@@ -328,6 +329,10 @@ DevWork dev_work() {
     w.far_vals = (uint32_t*)g.far_vals.p;
     w.far_vals_alt = (uint32_t*)g.far_vals_alt.p;
     w.far_count = (uint32_t*)g.far_count.p;
+    w.far_seg_off = (uint32_t*)g.far_seg_off.p;
+    w.far_seg_n = (uint32_t*)g.far_seg_n.p;
+    w.far_wofs = (uint32_t*)g.far_wofs.p;
+    w.far_work = (uint4*)g.far_work.p;
     w.far_count_host = g.far_count_host;
     w.sort_tmp = g.sort_tmp.p;
     w.sort_tmp_bytes = g.sort_tmp.bytes;
@@ -381,6 +386,7 @@ void set_chunk_log2(int log2) {
     if (g.chunk_log2 == log2) return;
     g.chunk_log2 = log2;
     for (DevBuf* b : {&g.far_rays, &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.sort_tmp, &g.ao_rays,
+                      &g.far_seg_off, &g.far_wofs, &g.far_work,
                       &g.ao_late, &g.shadow})
         release(*b);
     g.far_cap = g.ao_cap = 0;
@@ -426,6 +432,8 @@ int ensure_work(const rt_render_params* p, int n_rows) {
         if (ensure(g.far_rays, (size_t)fc * 32) || ensure(g.far_keys, (size_t)fc * 4) ||
             ensure(g.far_keys_alt, (size_t)fc * 4) || ensure(g.far_vals, (size_t)fc * 4) ||
             ensure(g.far_vals_alt, (size_t)fc * 4) || ensure(g.far_count, 64) ||
+            ensure(g.far_seg_off, (size_t)fc * 4) || ensure(g.far_seg_n, 64) || ensure(g.far_wofs, (size_t)fc * 4) ||
+            ensure(g.far_work, ((size_t)fc + fc / 64 + 64) * 16) ||
             ensure(g.sort_tmp, far_sort_tmp_bytes(fc) + 256))
             return RT_FAILURE;
         g.far_cap = fc;
@@ -993,6 +1001,7 @@ void shutdown_ctx() {
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
                       &g.ao_rays, &g.ao_late, &g.ao_late_count, &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
+                      &g.far_seg_off, &g.far_wofs, &g.far_work, &g.far_seg_n,
                       &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.shadow})
         release(*b);
     for (Slot& sl : g.slot) {
