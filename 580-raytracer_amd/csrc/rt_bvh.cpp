@@ -442,14 +442,71 @@ int32_t collapse4(const std::vector<BvhNode>& bin, int32_t b, std::vector<Bvh4No
 }
 }  // namespace
 
+// One node of nodes4 quantized (Bvh4QNode). Per axis: origin = the smallest
+// child lo, scale = 2^e with 255 * scale >= the children's extent; q_lo the
+// largest and q_hi the smallest code whose decoded plane fmaf(q, scale, origin)
+// (the device's exact arithmetic: q * scale is exact, one rounding) lies
+// outside the float plane; a larger scale when q_hi would not fit 8 bits.
+static Bvh4QNode quantize4(const Bvh4Node& nd) {
+    Bvh4QNode q;
+    std::memset(&q, 0, sizeof q);
+    bool any = false;
+    for (int j = 0; j < 4; j++) any = any || nd.n[j] >= 0;
+    for (int a = 0; a < 3; a++) {
+        float o = INFINITY, top = -INFINITY;
+        for (int j = 0; j < 4; j++)
+            if (nd.n[j] >= 0) {
+                o = std::min(o, nd.lo[a][j]);
+                top = std::max(top, nd.hi[a][j]);
+            }
+        if (!any) o = top = 0.0f;
+        int e;
+        (void)std::frexp(((double)top - (double)o) / 255.0, &e);  // 2^e >= extent / 255
+        e = std::max(e, -126);                                   // a normal scale
+        for (;; e++) {
+            const float scale = std::ldexp(1.0f, e);
+            bool fit = true;
+            for (int j = 0; j < 4 && fit; j++) {
+                if (nd.n[j] < 0) continue;
+                long lo = (long)std::floor(((double)nd.lo[a][j] - o) / scale);
+                lo = std::max(0L, std::min(255L, lo));
+                while (lo > 0 && std::fma((float)lo, scale, o) > nd.lo[a][j]) lo--;
+                while (lo < 255 && std::fma((float)(lo + 1), scale, o) <= nd.lo[a][j]) lo++;
+                long hi = (long)std::ceil(((double)nd.hi[a][j] - o) / scale);
+                hi = std::max(lo, std::min(256L, hi));
+                while (hi <= 255 && std::fma((float)hi, scale, o) < nd.hi[a][j]) hi++;
+                while (hi > lo && hi <= 255 && std::fma((float)(hi - 1), scale, o) >= nd.hi[a][j]) hi--;
+                if (hi > 255 || std::fma((float)lo, scale, o) > nd.lo[a][j]) {
+                    fit = false;
+                    break;
+                }
+                q.qlo[a][j] = (uint8_t)lo;
+                q.qhi[a][j] = (uint8_t)hi;
+            }
+            if (fit) break;
+        }
+        q.origin[a] = o;
+        q.exps |= (uint32_t)(e + 127) << (8 * a);
+    }
+    for (int j = 0; j < 4; j++)
+        q.link[j] = nd.n[j] < 0 ? 0xffffffffu : (((uint32_t)nd.n[j] << 27) | (uint32_t)nd.c[j]);
+    return q;
+}
+
 void collapse_bvh4(BvhBuild& out) {
     out.nodes4.clear();
+    out.nodes4q.clear();
     if (out.nodes.empty()) return;
     out.nodes4.reserve(out.nodes.size() / 2 + 8);
     int depth = 0;
     collapse4(out.nodes, 0, out.nodes4, 1, depth);
     // a traversal stacks at most 3 entries per level
-    if (3 * depth + 1 > RT_BVH_STACK) out.nodes4.clear();
+    if (3 * depth + 1 > RT_BVH_STACK) {
+        out.nodes4.clear();
+        return;
+    }
+    out.nodes4q.reserve(out.nodes4.size());
+    for (const Bvh4Node& nd : out.nodes4) out.nodes4q.push_back(quantize4(nd));
 }
 
 }  // namespace rt580

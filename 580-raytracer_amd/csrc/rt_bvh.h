@@ -67,6 +67,24 @@ struct alignas(16) Bvh4Node {
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node is two 64-byte lines");
 
+// The 4-wide node as the device reads it: the four child boxes quantized to
+// 8 bits per plane against the node's own frame (origin = the children's
+// smallest corner, per-axis power-of-two scale), rounded outward so that the
+// decoded box fmaf(q, scale, origin) contains the child's float box -- the
+// same culling decisions or more conservative ones (more boxes entered, never
+// fewer), hence the same answers. Child link as a stack entry: n << 27 | c
+// (n == 0: node c; n > 0: leaf slots [c, c + n)); 0xffffffff: empty. 64 bytes:
+// half the bytes and registers of Bvh4Node per traversal step.
+struct alignas(16) Bvh4QNode {
+    float origin[3];
+    uint32_t exps;      // biased float exponents of the three scales, bits 0-7, 8-15, 16-23
+    uint8_t qlo[3][4];  // [axis][child]
+    uint8_t qhi[3][4];
+    uint32_t link[4];
+    uint32_t pad[2];
+};
+static_assert(sizeof(Bvh4QNode) == 64, "Bvh4QNode is one 64-byte line");
+
 // Plane-tree node (own bounds): normals in [nlo, nhi], plane offsets D in
 // [dlo, dhi], and the subtree minima of D_hi and delta (for its T bound).
 // count > 0: leaf of far_tris [first, first + count); else children first, first + 1.
@@ -94,6 +112,7 @@ static_assert(sizeof(FarTri) == 32, "FarTri layout");
 struct BvhBuild {
     std::vector<BvhNode> nodes;     // node 0 is the root
     std::vector<Bvh4Node> nodes4;   // the same tree 4-wide (collapse_bvh4); node 0 is the root
+    std::vector<Bvh4QNode> nodes4q; // nodes4 quantized (collapse_bvh4): what the traversal reads
     std::vector<rt_prim> prims;     // near-set triangles in leaf order (copies of the scene records)
     std::vector<uint32_t> ids;      // scene index of each slot (tie-break + shading lookups)
     std::vector<FarNode> far_nodes; // node 0 is the root (empty when no far-set triangle)
@@ -122,7 +141,7 @@ struct BvhBuild {
 // would exceed the device stack (the caller then keeps brute force).
 bool build_bvh(const rt_prim* prims, int n, BvhBuild& out);
 
-// The 4-wide form of out.nodes (after build_bvh).
+// The 4-wide form of out.nodes (after build_bvh), float and quantized.
 void collapse_bvh4(BvhBuild& out);
 
 // Build the far-search direction grid over out.far_tris (after build_bvh; the

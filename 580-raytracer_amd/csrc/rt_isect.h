@@ -110,7 +110,7 @@ RTM_HD bool prim_test_any(const rt_prim& P, rv3 o, rv3 d) {
 struct BvhView {
     const rt_prim* all;         // scene primitives by index
     const BvhNode* nodes;
-    const Bvh4Node* nodes4;     // the same tree 4-wide (any-hit queries); null: binary only
+    const Bvh4QNode* nodes4;    // the same tree 4-wide, quantized boxes (rt_bvh.h); null: binary only
     const rt_prim* prims;       // spatial leaf order
     const uint32_t* ids;
     const FarNode* far_nodes;
@@ -517,16 +517,36 @@ RTM_HD bool bvh_any(const BvhView& V, rv3 o, rv3 d, bool with_far = true, float 
 
 // Whole-record loads (one batch of 16-byte loads per node / primitive on the
 // device, so a traversal step waits for memory once, not once per field).
-RTM_HD void load_node4(const Bvh4Node* p, Bvh4Node& out) {
+// A quantized 4-wide node (rt_bvh.h Bvh4QNode) decoded: child boxes
+// lo/hi[axis][child] = fmaf(q, scale, origin) (exact product, one rounding, as
+// the host's quantizer assumed) and the child links.
+struct Node4 {
+    float lo[3][4], hi[3][4];
+    uint32_t link[4];
+};
+RTM_HD void load_node4(const Bvh4QNode* p, Node4& out) {
+    Bvh4QNode q;
 #ifdef __HIP_DEVICE_COMPILE__
     const float4* s = reinterpret_cast<const float4*>(p);
-    float4* d = reinterpret_cast<float4*>(&out);
+    float4* d = reinterpret_cast<float4*>(&q);
 #pragma unroll
-    for (int i = 0; i < 8; i++) d[i] = s[i];
+    for (int i = 0; i < 4; i++) d[i] = s[i];
 #else
-    out = *p;
+    q = *p;
 #endif
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float scale = rt_bits_f32(((q.exps >> (8 * a)) & 255u) << 23);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            out.lo[a][j] = fmaf((float)q.qlo[a][j], scale, q.origin[a]);
+            out.hi[a][j] = fmaf((float)q.qhi[a][j], scale, q.origin[a]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) out.link[j] = q.link[j];
 }
+
 RTM_HD void load_prim(const rt_prim* p, rt_prim& out) {
 #ifdef __HIP_DEVICE_COMPILE__
     const float4* s = reinterpret_cast<const float4*>(p);
@@ -581,7 +601,7 @@ RTM_HD bool bvh4_descend(const BvhView& V, const SlabRay& sr, float tmax, const 
                          int32_t& n) {
     while (n == 0) {
         RT_CNT(nodes, 1);
-        Bvh4Node nd;
+        Node4 nd;
         load_node4(V.nodes4 + c, nd);
         float t[4];
         bool ok[4];
@@ -590,7 +610,7 @@ RTM_HD bool bvh4_descend(const BvhView& V, const SlabRay& sr, float tmax, const 
             const float lo[3] = {nd.lo[0][j], nd.lo[1][j], nd.lo[2][j]};
             const float hi[3] = {nd.hi[0][j], nd.hi[1][j], nd.hi[2][j]};
             const bool in = slab(lo, hi, sr, t[j]);
-            ok[j] = (nd.n[j] >= 0) & in & !(t[j] > tmax);
+            ok[j] = (nd.link[j] != 0xffffffffu) & in & !(t[j] > tmax);
         }
         int best = -1;
         float bt = INFINITY;
@@ -602,12 +622,13 @@ RTM_HD bool bvh4_descend(const BvhView& V, const SlabRay& sr, float tmax, const 
             }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            stk.put(sp, ((uint32_t)nd.n[j] << 27) | (uint32_t)nd.c[j]);
+            stk.put(sp, nd.link[j]);
             sp += (ok[j] & (j != best)) ? 1 : 0;
         }
         if (best >= 0) {
-            c = best == 0 ? nd.c[0] : best == 1 ? nd.c[1] : best == 2 ? nd.c[2] : nd.c[3];
-            n = best == 0 ? nd.n[0] : best == 1 ? nd.n[1] : best == 2 ? nd.n[2] : nd.n[3];
+            const uint32_t e = best == 0 ? nd.link[0] : best == 1 ? nd.link[1] : best == 2 ? nd.link[2] : nd.link[3];
+            c = (int32_t)(e & 0x7ffffffu);
+            n = (int32_t)(e >> 27);
         } else if (!bvh4_pop(stk, sp, c, n)) {
             return false;
         }
@@ -707,7 +728,7 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
         bool have = true;
         while (n == 0) {
             RT_CNT(nodes, 1);
-            Bvh4Node nd;
+            Node4 nd;
             load_node4(V.nodes4 + c, nd);
             float t[4];
             bool ok[4];
@@ -716,7 +737,7 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
                 const float lo[3] = {nd.lo[0][j], nd.lo[1][j], nd.lo[2][j]};
                 const float hi[3] = {nd.hi[0][j], nd.hi[1][j], nd.hi[2][j]};
                 const bool in = slab(lo, hi, sr, t[j]);
-                ok[j] = (nd.n[j] >= 0) & in & (!found || t[j] <= h.t);
+                ok[j] = (nd.link[j] != 0xffffffffu) & in & (!found || t[j] <= h.t);
             }
             int best = -1;
             float bt = INFINITY;
@@ -728,13 +749,14 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
                 }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                stk[sp] = ((uint32_t)nd.n[j] << 27) | (uint32_t)nd.c[j];
+                stk[sp] = nd.link[j];
                 tstk[sp] = t[j];
                 sp += (ok[j] & (j != best)) ? 1 : 0;
             }
             if (best >= 0) {
-                c = best == 0 ? nd.c[0] : best == 1 ? nd.c[1] : best == 2 ? nd.c[2] : nd.c[3];
-                n = best == 0 ? nd.n[0] : best == 1 ? nd.n[1] : best == 2 ? nd.n[2] : nd.n[3];
+                const uint32_t e = best == 0 ? nd.link[0] : best == 1 ? nd.link[1] : best == 2 ? nd.link[2] : nd.link[3];
+                c = (int32_t)(e & 0x7ffffffu);
+                n = (int32_t)(e >> 27);
                 continue;
             }
             have = false;

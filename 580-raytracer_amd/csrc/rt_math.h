@@ -21,6 +21,17 @@ struct rv3 {
     float x, y, z;
 };
 
+// The float with these bits.
+RTM_HD float rt_bits_f32(uint32_t u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __uint_as_float(u);
+#else
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+#endif
+}
+
 RTM_HD rv3 v3(float x, float y, float z) { rv3 r; r.x = x; r.y = y; r.z = z; return r; }
 RTM_HD rv3 v3_add(rv3 a, rv3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 RTM_HD rv3 v3_sub(rv3 a, rv3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }

@@ -243,7 +243,7 @@ DevScene dev_scene(const rt_render_params* p) {
     BvhView& v = s.bv;
     v.all = s.prims;
     v.nodes = (const BvhNode*)g.bvh_nodes.p;
-    v.nodes4 = g.bvh.nodes4.empty() ? nullptr : (const Bvh4Node*)g.bvh_nodes4.p;
+    v.nodes4 = g.bvh.nodes4q.empty() ? nullptr : (const Bvh4QNode*)g.bvh_nodes4.p;
     v.prims = (const rt_prim*)g.bvh_prims.p;
     v.ids = (const uint32_t*)g.bvh_ids.p;
     v.far_nodes = (const FarNode*)g.far_nodes.p;
@@ -688,7 +688,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         // the 4-wide form for the any-hit queries (AO, shadows); RT580_BVH4=0: binary only
         const char* b4 = std::getenv("RT580_BVH4");
         if (g.bvh_ok && !(b4 && std::atoi(b4) == 0)) collapse_bvh4(g.bvh);
-        if (g.bvh_ok && (upload_vec(g.bvh_nodes, g.bvh.nodes) || upload_vec(g.bvh_nodes4, g.bvh.nodes4) || upload_vec(g.bvh_prims, g.bvh.prims) ||
+        if (g.bvh_ok && (upload_vec(g.bvh_nodes, g.bvh.nodes) || upload_vec(g.bvh_nodes4, g.bvh.nodes4q) || upload_vec(g.bvh_prims, g.bvh.prims) ||
                          upload_vec(g.bvh_ids, g.bvh.ids) || upload_vec(g.far_nodes, g.bvh.far_nodes) ||
                          upload_vec(g.far_tris, g.bvh.far_tris) || upload_vec(g.brute, g.bvh.brute) ||
                          upload_vec(g.grid_start, g.bvh.grid_start) || upload_vec(g.grid_items, g.bvh.grid_items) ||
@@ -710,6 +710,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         g.grid_n_always = (int)g.bvh.grid_always.size();
         // the device needs only the arrays; keep the host copy small
         g.bvh.prims = std::vector<rt_prim>();
+        g.bvh.nodes4 = std::vector<Bvh4Node>();
         g.bvh.ids = std::vector<uint32_t>();
         g.bvh.n_far = (int)g.bvh.far_tris.size();
         g.bvh.far_tris = std::vector<FarTri>();

@@ -82,7 +82,7 @@ int main(int argc, char** argv) {
     BvhView V;
     V.all = P.data();
     V.nodes = B.nodes.data();
-    V.nodes4 = B.nodes4.empty() ? nullptr : B.nodes4.data();
+    V.nodes4 = B.nodes4q.empty() ? nullptr : B.nodes4q.data();
     V.prims = B.prims.data();
     V.ids = B.ids.data();
     V.far_nodes = B.far_nodes.empty() ? nullptr : B.far_nodes.data();

@@ -43,25 +43,26 @@ static bool trace(const BvhView& V, rv3 o, rv3 d, std::vector<Step>& steps) {
             int sp0 = sp;
             int32_t c0 = c, n0 = n;
             // one node iteration of bvh4_descend
-            Bvh4Node nd = V.nodes4[c0];
+            Node4 nd;
+            load_node4(V.nodes4 + c0, nd);
             float t[4];
             bool ok[4];
             for (int j = 0; j < 4; j++) {
                 const float lo[3] = {nd.lo[0][j], nd.lo[1][j], nd.lo[2][j]};
                 const float hi[3] = {nd.hi[0][j], nd.hi[1][j], nd.hi[2][j]};
                 const bool in = slab(lo, hi, sr, t[j]);
-                ok[j] = (nd.n[j] >= 0) & in;
+                ok[j] = (nd.link[j] != 0xffffffffu) & in;
             }
             int best = -1;
             float bt = INFINITY;
             for (int j = 0; j < 4; j++)
                 if (ok[j] && (best < 0 || t[j] < bt)) { best = j; bt = t[j]; }
             for (int j = 0; j < 4; j++) {
-                stk[sp] = ((uint32_t)nd.n[j] << 27) | (uint32_t)nd.c[j];
+                stk[sp] = nd.link[j];
                 sp += (ok[j] && j != best) ? 1 : 0;
             }
             (void)sp0; (void)n0;
-            if (best >= 0) { c = nd.c[best]; n = nd.n[best]; }
+            if (best >= 0) { c = (int32_t)(nd.link[best] & 0x7ffffffu); n = (int32_t)(nd.link[best] >> 27); }
             else if (!bvh4_pop(ArrStack{stk}, sp, c, n)) { leaf = false; break; }
         }
         if (!leaf) { steps.push_back(s); return false; }
@@ -89,7 +90,7 @@ int main(int argc, char** argv) {
     if (!build_bvh(P.data(), (int)P.size(), B)) { std::printf("no bvh\n"); return 0; }
     collapse_bvh4(B);
     BvhView V{};
-    V.all = P.data(); V.nodes = B.nodes.data(); V.nodes4 = B.nodes4.data(); V.prims = B.prims.data();
+    V.all = P.data(); V.nodes = B.nodes.data(); V.nodes4 = B.nodes4q.data(); V.prims = B.prims.data();
     V.ids = B.ids.data(); V.has_tree = 1; V.scale = B.scale;
     const long waves = std::atol(argv[3]);
     std::mt19937 rng(argc > 4 ? std::atoi(argv[4]) : 580);
