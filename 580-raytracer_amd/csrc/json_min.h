@@ -43,6 +43,7 @@ struct Value {
     bool is_array() const { return kind == Array; }
     bool is_object() const { return kind == Object; }
     bool is_string() const { return kind == String; }
+    bool is_null() const { return kind == Null; }
 
     // json::get<float>() / implicit float conversion
     float as_float() const {

@@ -14,7 +14,9 @@ Raytracer::Raytracer(int width, int height) : mWidth(width), mHeight(height) {
     std::memset(&mParams, 0, sizeof mParams);
 }
 
-Raytracer::~Raytracer() {}
+Raytracer::~Raytracer() {
+    if (mFbRegistered) (void)rt_gpu_host_unregister(mFrameBuffer.data());
+}
 
 int Raytracer::LoadSceneJSON(const std::string scenePath) {
     std::string err;
@@ -103,6 +105,10 @@ int Raytracer::Render(const std::string outputName) {
     // a whole frame lands in mFrameBuffer directly; selected rows through a row buffer
     std::vector<int16_t> rows(whole ? 0 : (size_t)(nsel > 0 ? nsel : 0) * mWidth * 3);
     int16_t* dst = whole ? reinterpret_cast<int16_t*>(mFrameBuffer.data()) : rows.data();
+    // The framebuffer lives as long as this instance: page-lock it once, so
+    // every frame lands in it with one DMA (no staging copy)
+    if (whole && !mFbRegistered && !mFrameBuffer.empty())
+        mFbRegistered = rt_gpu_host_register(mFrameBuffer.data(), mFrameBuffer.size() * sizeof(Pixel)) == RT_SUCCESS;
     // Whole frames can shard across the node's GPUs (interleaved rows, RCCL
     // exchange + gather, rt_gpu_render_multi) when SetGpuCount or $RT580_GPUS
     // asks for more than one; the default is the one device of rt_gpu_init

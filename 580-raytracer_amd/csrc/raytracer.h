@@ -58,4 +58,5 @@ class Raytracer {
     int mDepth = 4, mAoSamples = 128, mAoOn = 1, mEngine = RT_RNG_MINSTD_RAND0;
     int mRowBegin = 0, mRowEnd = -1, mRowStep = 1;
     int mGpus = 0;
+    bool mFbRegistered = false;  // mFrameBuffer page-locked for the GPU (rt_gpu_host_register)
 };

@@ -41,6 +41,9 @@ struct DevFrame {
     float cam_from[3];
     float ao_angle_max;
     double ndc_kx, ndc_ky;
+    // minstd_rand0: step = 16807^(2 * ao_samples) mod (2^31 - 1), the state
+    // advance of one AO call; step_pow2[i] = step^(2^i)
+    uint32_t step_pow2[32];
 };
 
 // One node of the reflect/refract recursion tree (a Raycast call). 64 bytes.
@@ -147,6 +150,15 @@ const char* launch_where();
 // Temporary storage of the far-queue radix sort / run-length encoding / scan for `cap` rays.
 size_t far_sort_tmp_bytes(uint32_t cap);
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s);
+// Latency path of small-scene frames (a frame split by rows so that the first
+// part's resolve and copy overlap the second part's AO): AO of the calls
+// [*call_lo, *call_hi) (device values; null: from the first / to the last),
+// and the resolve of the local pixels [p_lo, p_hi).
+bool ao_calls_supported(const DevScene& S, const DevFrame& F);
+hipError_t launch_ao_calls(const DevScene& S, const DevFrame& F, const DevWork& W, const uint64_t* call_lo,
+                           const uint64_t* call_hi, hipStream_t s);
+hipError_t launch_resolve_range(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, uint32_t p_lo,
+                                uint32_t p_hi, hipStream_t s);
 hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* out,
                             hipStream_t s);
 hipError_t upload_gamma_lut(const uint8_t* lut, hipStream_t s);

@@ -57,16 +57,8 @@ __device__ __forceinline__ uint32_t mersenne31_mul(uint32_t a, uint32_t b) {
     return v >= 0x7fffffffu ? v - 0x7fffffffu : v;
 }
 
-__constant__ uint32_t c_minstd_pow2[32];   // 16807^(2^i) mod m
 __constant__ uint32_t c_minstd_j1[512];    // 16807^(2s+1) mod m: state offset of sample s's first draw
 
-__device__ __forceinline__ uint32_t minstd_pow(uint32_t state, uint64_t k) {
-    k %= 2147483646ull;  // period: 16807 is a primitive root mod 2^31-1
-    uint32_t s = state;
-    for (int i = 0; i < 31; i++)
-        if ((k >> i) & 1ull) s = mersenne31_mul(s, c_minstd_pow2[i]);
-    return s;
-}
 
 // generate_canonical<float,24> (libstdc++ random.tcc:3348-3378) for one draw.
 __device__ __forceinline__ float canon_minstd(uint32_t x) {  // r = 2^31-2 -> tmp = 2^31 (float)
@@ -787,42 +779,56 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
 
 // ---------------------------------------------------------------- AO-call bookkeeping
 // One workgroup per local row: AO calls per pixel (hits x ambient lights), their
-// in-row exclusive prefix, and the row's totals.
-__global__ void __launch_bounds__(1024) row_counts_kernel(DevScene S, DevFrame F, DevWork W) {
-    __shared__ uint32_t part[1024];
-    __shared__ uint32_t carry, hsum, nsum;
+// in-row exclusive prefix, and the row's totals. Each thread takes a run of
+// consecutive pixels; the runs' sums are scanned across the wave (shuffles)
+// and the workgroup's four waves (LDS), then each run writes its prefixes.
+__global__ void __launch_bounds__(TB) row_counts_kernel(DevScene S, DevFrame F, DevWork W) {
+    __shared__ uint32_t wsum[TB / 64][3];
     const int lr = blockIdx.x;
     const uint32_t off = (uint32_t)lr * (uint32_t)F.width;
-    if (threadIdx.x == 0) { carry = 0; hsum = 0; nsum = 0; }
-    __syncthreads();
-    uint32_t my_h = 0, my_n = 0;
-    for (int x0 = 0; x0 < F.width; x0 += 1024) {
-        const int x = x0 + threadIdx.x;
-        uint32_t hits = 0, nodes = 0;
-        if (x < F.width) { hits = W.pix_hits[off + x]; nodes = W.pix_nodes[off + x]; }
-        my_h += hits;
-        my_n += nodes;
-        const uint32_t v = hits * (uint32_t)S.n_ambient;
-        part[threadIdx.x] = v;
-        __syncthreads();
-        for (int s = 1; s < 1024; s <<= 1) {
-            uint32_t add = threadIdx.x >= s ? part[threadIdx.x - s] : 0;
-            __syncthreads();
-            part[threadIdx.x] += add;
-            __syncthreads();
-        }
-        if (x < F.width) W.pix_prefix[off + x] = carry + part[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += part[1023];
-        __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int per = (F.width + TB - 1) / TB;
+    const int x0 = threadIdx.x * per, x1 = min(x0 + per, F.width);
+    const uint32_t na = (uint32_t)S.n_ambient;
+    uint32_t calls = 0, hits = 0, nodes = 0;
+    for (int x = x0; x < x1; x++) {
+        const uint32_t h = W.pix_hits[off + x];
+        hits += h;
+        calls += h * na;
+        nodes += W.pix_nodes[off + x];
     }
-    atomicAdd(&hsum, my_h);
-    atomicAdd(&nsum, my_n);
+    // inclusive scan of calls over the wave; sums of hits and nodes
+    uint32_t inc = calls, hs = hits, ns = nodes;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)inc, k);
+        if (lane >= k) inc += v;
+        hs += (uint32_t)__shfl_xor((int)hs, k);
+        ns += (uint32_t)__shfl_xor((int)ns, k);
+    }
+    if (lane == 63) {
+        wsum[wave][0] = inc;
+        wsum[wave][1] = hs;
+        wsum[wave][2] = ns;
+    }
     __syncthreads();
+    uint32_t base = 0, tot = 0, th = 0, tn = 0;
+#pragma unroll
+    for (int w = 0; w < TB / 64; w++) {
+        if (w < wave) base += wsum[w][0];
+        tot += wsum[w][0];
+        th += wsum[w][1];
+        tn += wsum[w][2];
+    }
+    uint32_t acc = base + inc - calls;
+    for (int x = x0; x < x1; x++) {
+        W.pix_prefix[off + x] = acc;
+        acc += W.pix_hits[off + x] * na;
+    }
     if (threadIdx.x == 0) {
-        W.row_calls[lr] = carry;
-        W.row_hits[lr] = hsum;
-        W.row_nodes[lr] = nsum;
+        W.row_calls[lr] = tot;
+        W.row_hits[lr] = th;
+        W.row_nodes[lr] = tn;
     }
 }
 
@@ -862,12 +868,15 @@ __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWor
     const int lr = (int)(p / (uint32_t)F.width);
     const uint64_t lbase = W.row_base_local[lr] + W.pix_prefix[p];
     const uint64_t gbase = (row_base_global ? row_base_global[lr] : W.row_base_local[lr]) + W.pix_prefix[p];
-    const uint64_t draws_per_call = 2ull * (uint64_t)F.ao_samples;
     uint64_t rng = 0;
-    uint32_t step = 1;
+    const uint32_t step = F.step_pow2[0];
     if (F.rng_engine == RT_RNG_MINSTD_RAND0) {
-        rng = minstd_pow(F.rng_seed, gbase * draws_per_call);
-        step = minstd_pow(1u, draws_per_call);
+        // seed * step^gbase (the order of step divides the period 2^31 - 2)
+        uint64_t k = gbase < 2147483646ull ? gbase : gbase % 2147483646ull;
+        uint32_t st = F.rng_seed;
+        for (int i = 0; k; i++, k >>= 1)
+            if (k & 1) st = mersenne31_mul(st, F.step_pow2[i]);
+        rng = st;
     } else {
         rng = gbase;
     }
@@ -1142,7 +1151,10 @@ __device__ void ao_fix_item(const DevScene& S, const DevFrame& F, const DevWork&
 
 // The queued items; if the queue overflowed (more failing samples than slots),
 // every item of [b, e) is re-tested and the failing ones recomputed instead.
-__global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
+__global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e,
+                                                    const uint64_t* call_lo, const uint64_t* call_hi) {
+    if (call_lo) b = *call_lo * (uint64_t)F.ao_samples;
+    if (call_hi) e = *call_hi * (uint64_t)F.ao_samples;
     const uint32_t n = *W.aofix_count;
     if (n == 0) return;
     if (n <= W.aofix_cap) {
@@ -2035,10 +2047,13 @@ __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, 
 
 // Same kernel with the register budget capped for 8 waves per SIMD (SGPR <= 80
 // admits 8 workgroups per CU instead of 6).
+// call_lo / call_hi (device, may be null): only the items of AO calls
+// [*call_lo, *call_hi) (a row range of the frame: its calls are contiguous).
 template <int VARIANT>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(8, 8)))
-ao_kernel_occ8(DevScene S, DevFrame F, DevWork W) {
-    ao_body<VARIANT>(S, F, W);
+ao_kernel_occ8(DevScene S, DevFrame F, DevWork W, const uint64_t* call_lo, const uint64_t* call_hi) {
+    const uint64_t N = (uint64_t)F.ao_samples;
+    ao_body<VARIANT>(S, F, W, call_lo ? *call_lo * N : 0ull, call_hi ? *call_hi * N : ~0ull);
 }
 
 // ---------------------------------------------------------------- resolve
@@ -2132,17 +2147,23 @@ __device__ __forceinline__ rpix node_val_load(const DevWork& W, int32_t id) {
     return px((int16_t)(v.x & 0xffff), (int16_t)(v.x >> 16), (int16_t)(v.y & 0xffff));
 }
 
+// Only the nodes of pixels [p_lo, p_hi) (local pixel index; level 0 nodes are
+// the pixels, deeper ones name theirs in W.rays).
 __global__ void __launch_bounds__(TB) resolve_level_kernel(DevScene S, DevFrame F, DevWork W, int level,
-                                                           int16_t* __restrict__ fb) {
-    const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
-    uint32_t base = 0, count = npix;
+                                                           int16_t* __restrict__ fb, uint32_t p_lo, uint32_t p_hi) {
+    uint32_t base = p_lo, count = p_hi - p_lo;
     if (level > 0) {  // the trace's own clamp to the node capacity
         base = W.lvl[LVL_BASE + level];
         const uint32_t room = W.node_cap > base ? W.node_cap - base : 0u;
         count = W.lvl[level] < room ? W.lvl[level] : room;
     }
+    const bool all = p_lo == 0 && p_hi == (uint32_t)F.n_rows * (uint32_t)F.width;
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < count; i += gridDim.x * TB) {
         const uint32_t node = base + i;
+        if (level > 0 && !all) {
+            const uint32_t px = (uint32_t)W.rays[node].pixel;
+            if (px < p_lo || px >= p_hi) continue;
+        }
         const NodeRec nd = W.nodes[node];
         const int flags = nd.local_b_flags >> 16;
         rpix v;
@@ -2458,23 +2479,14 @@ hipError_t launch_deinterleave(const int16_t* tiles, int world, int n_max, int w
 // ---------------------------------------------------------------- launchers
 
 hipError_t upload_minstd_table(hipStream_t s) {
-    uint32_t pw[32];
-    uint64_t a = 16807;
-    for (int i = 0; i < 32; i++) { pw[i] = (uint32_t)a; a = (a * a) % 2147483647ull; }
-    static uint32_t j1[512];
+    static uint32_t j1[512];  // async copies read host memory later: keep it alive
     uint64_t x = 16807;  // a^(2s+1)
     for (int i = 0; i < 512; i++) {
         j1[i] = (uint32_t)x;
         x = (x * 16807ull) % 2147483647ull;
         x = (x * 16807ull) % 2147483647ull;
     }
-    static uint32_t pw_keep[32];  // async copies read host memory later: keep it alive
-    std::memcpy(pw_keep, pw, sizeof pw);
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_pow2), pw_keep, sizeof pw_keep, 0,
-                                          hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-        e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
-    return e;
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
 }
 
 // ---------------------------------------------------------------- kernel timer
@@ -2699,7 +2711,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
 
 hipError_t launch_row_counts(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     if (F.n_rows == 0) return hipSuccess;
-    hipLaunchKernelGGL(row_counts_kernel, dim3(F.n_rows), dim3(1024), 0, s, S, F, W);
+    hipLaunchKernelGGL(row_counts_kernel, dim3(F.n_rows), dim3(TB), 0, s, S, F, W);
     hipLaunchKernelGGL(row_scan_kernel, dim3(1), dim3(1024), 0, s, F, W);
     return hipGetLastError();
 }
@@ -2745,8 +2757,9 @@ static unsigned ao_grid() {
 }
 
 hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t b, uint64_t e,
-                         hipStream_t s);
-hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v);
+                         hipStream_t s, const uint64_t* call_lo = nullptr, const uint64_t* call_hi = nullptr);
+hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v,
+                           const uint64_t* call_lo = nullptr, const uint64_t* call_hi = nullptr);
 
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     (void)hipGetLastError();  // launch checks below must not see a stale error
@@ -2902,18 +2915,36 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
     return launch_ao_fix(S, F, W, 0, ~0ull, s);
 }
 
+bool ao_calls_supported(const DevScene& S, const DevFrame& F) {
+    return !S.use_bvh && F.ao_enabled && S.n_ambient > 0 && (ao_variant() & (16 | 4096)) == (16 | 4096);
+}
+
+hipError_t launch_ao_calls(const DevScene& S, const DevFrame& F, const DevWork& W, const uint64_t* call_lo,
+                           const uint64_t* call_hi, hipStream_t s) {
+    (void)hipGetLastError();
+    if (!ao_calls_supported(S, F)) return hipErrorInvalidValue;
+    // a fresh fix-up queue for this range (frame_init_kernel zeroed it for the first)
+    hipError_t e = hipMemsetAsync(W.aofix_count, 0, 4, s);
+    if (e != hipSuccess) return e;
+    if ((e = launch_ao_small(S, F, W, s, ao_variant(), call_lo, call_hi)) != hipSuccess) return e;
+    return launch_ao_fix(S, F, W, 0, ~0ull, s, call_lo, call_hi);
+}
+
 // Exact recompute of the samples the fast pass queued (or, on queue overflow,
 // of every failing sample of items [b, e)); exits at once with nothing to do.
 hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t b, uint64_t e,
-                         hipStream_t s) {
-    hipLaunchKernelGGL(ao_fix_kernel, dim3(2048), dim3(TB), 0, s, S, F, W, b, e);
+                         hipStream_t s, const uint64_t* call_lo, const uint64_t* call_hi) {
+    // a few hundred samples per frame at most (the queue; its overflow case
+    // re-tests every item of [b, e) grid-stride): a small grid exits at once
+    hipLaunchKernelGGL(ao_fix_kernel, dim3(64), dim3(TB), 0, s, S, F, W, b, e, call_lo, call_hi);
     return hipGetLastError();
 }
 
-hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v) {
+hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v,
+                           const uint64_t* call_lo, const uint64_t* call_hi) {
     if (v & 16) {
         switch (v & ~16) {
-#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(ao_grid()), dim3(TB), 0, s, S, F, W); break;
+#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(ao_grid()), dim3(TB), 0, s, S, F, W, call_lo, call_hi); break;
             RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8) RT_AO_CASE(1032) RT_AO_CASE(2056) RT_AO_CASE(3080)
             RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128) RT_AO_CASE(7180) RT_AO_CASE(7182)
 #undef RT_AO_CASE
@@ -2961,9 +2992,15 @@ hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W
         hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)((npix + TB - 1) / TB)), dim3(TB), 0, s, S, F, W, fb);
         return hipGetLastError();
     }
+    return launch_resolve_range(S, F, W, fb, 0, (uint32_t)npix, s);
+}
+
+hipError_t launch_resolve_range(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, uint32_t p_lo,
+                                uint32_t p_hi, hipStream_t s) {
+    const uint64_t npix = (uint64_t)F.n_rows * F.width;
     for (int level = F.depth; level >= 0; level--) {
-        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, deep_grid());
-        hipLaunchKernelGGL(resolve_level_kernel, dim3(grid), dim3(TB), 0, s, S, F, W, level, fb);
+        const int grid = level == 0 ? grid_for(p_hi - p_lo, 1 << 20) : grid_for(2 * npix, deep_grid());
+        hipLaunchKernelGGL(resolve_level_kernel, dim3(grid), dim3(TB), 0, s, S, F, W, level, fb, p_lo, p_hi);
     }
     return hipGetLastError();
 }

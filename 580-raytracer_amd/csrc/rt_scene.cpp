@@ -76,10 +76,14 @@ int load_scene_json(const std::string& root, const std::string& scene_path, Scen
     int status = RT_SUCCESS;
     try {
         json_min::Value j = json_min::parse(text);
-        // jsonData["scene"] (Raytracer.cpp:667): a document without "scene"
-        // (or with a non-object there) has no shapes, camera or lights and
-        // still loads; a document that is not an object is a type error.
-        if (!j.is_object()) throw json_min::error("type_error: cannot use operator[] with a string argument");
+        // jsonData["scene"] (Raytracer.cpp:667) on the non-const document: a
+        // document without "scene" (or with a non-object there) has no shapes,
+        // camera or lights and still loads -- so does the document `null`,
+        // which operator[] turns into an object; any other non-object
+        // document is a type error (tests/golden/loader: null_document,
+        // array_document, number_document).
+        if (!j.is_object() && !j.is_null())
+            throw json_min::error("type_error: cannot use operator[] with a string argument");
         static const json_min::Value kNull;
         const json_min::Value& s = j.contains("scene") ? j.at("scene") : kNull;
         if (s.contains("shapes")) {

@@ -22,6 +22,7 @@
 #include "../../include/rt580.h"
 #include "rt_bvh.h"
 #include "rt_kernels.h"
+#include "rt_knobs.h"
 
 using namespace rt580;
 
@@ -78,6 +79,14 @@ struct State {
     size_t stage_bytes = 0;
     std::array<hipEvent_t, 16> stage_ev{};
     bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
+    // rt_gpu_render's latency path: a second stream for the first part's
+    // resolve + copy, and the hand-off events
+    hipStream_t aux = nullptr;
+    hipEvent_t aux_go = nullptr, aux_done = nullptr;
+    // its split row for a (params, scene): read once, deterministic afterwards
+    rt_render_params lat_params{};
+    uint64_t lat_gen = ~0ull;
+    int lat_row = -1;
     // BVH far-queue buffers (BVH frames always run serialized on slot 0)
     DevBuf ao_rays, ao_late, ao_late_count;
     DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim, shadow,
@@ -300,6 +309,13 @@ DevFrame dev_frame(const rt_render_params* p, int row_begin, int row_step, int n
     f.ao_angle_max = p->ao_angle_max;
     f.ndc_kx = p->ndc_kx;
     f.ndc_ky = p->ndc_ky;
+    {   // 16807^(2 N) mod (2^31 - 1), then its repeated squares
+        const uint64_t m = 2147483647ull;
+        uint64_t b = 16807, st = 1;
+        for (uint64_t e = 2ull * (uint64_t)p->ao_samples; e; e >>= 1, b = b * b % m)
+            if (e & 1) st = st * b % m;
+        for (int i = 0; i < 32; i++, st = st * st % m) f.step_pow2[i] = (uint32_t)st;
+    }
     return f;
 }
 
@@ -589,6 +605,10 @@ extern "C" {
 
 int rt_gpu_init(int device) {
     if (g.inited) return RT_SUCCESS;
+    {   // every RT580_* switch known and valid (rt_knobs.cpp), before anything reads one
+        char why[256];
+        if (!knobs_check(why, sizeof why)) return fail("%s", why);
+    }
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= 0) return fail("no HIP device available (%s)", hipGetErrorString(e));
@@ -618,6 +638,9 @@ int rt_gpu_init(int device) {
         HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
     }
     for (auto& ev : g.user_mark) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_TRY(hipStreamCreateWithFlags(&g.aux, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&g.aux_go, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&g.aux_done, hipEventDisableTiming));
     g.ev = g.ev_default.data();
     HIP_TRY(hipHostMalloc((void**)&g.needed_host, 64, hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void**)&g.far_count_host, 64, hipHostMallocDefault));
@@ -774,9 +797,31 @@ int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     return fail("node capacity could not be sized");
 }
 
-// The framebuffer to the caller's (pageable) memory: device -> pinned staging in
-// up to 16 chunks, each chunk's host copy overlapping the next chunks' DMA.
-int copy_out(const int16_t* dev, int16_t* fb_out, size_t bytes) {
+// Host ranges page-locked by rt_gpu_host_register (process-wide).
+struct HostRange {
+    const char* p;
+    size_t bytes;
+};
+static std::vector<HostRange> g_host_ranges;
+
+static bool host_registered(const void* p, size_t bytes) {
+    const char* c = (const char*)p;
+    for (const HostRange& r : g_host_ranges)
+        if (c >= r.p && c + bytes <= r.p + r.bytes) return true;
+    return false;
+}
+
+// The framebuffer to the caller's memory: one DMA into a registered range;
+// else device -> pinned staging in up to 16 chunks, each chunk's host copy
+// overlapping the next chunks' DMA.
+static int copy_out(const int16_t* dev, int16_t* fb_out, size_t bytes, hipStream_t stream = nullptr) {
+    if (host_registered(fb_out, bytes)) {
+        // on the stream that produced the frame when given (no cross-stream hand-off)
+        const hipStream_t cs = stream ? stream : g.stream;
+        HIP_TRY(hipMemcpyAsync(fb_out, dev, bytes, hipMemcpyDeviceToHost, cs));
+        HIP_TRY(hipStreamSynchronize(cs));
+        return RT_SUCCESS;
+    }
     if (g.stage_bytes < bytes) {
         if (g.stage) (void)hipHostFree(g.stage);
         g.stage = nullptr;
@@ -806,13 +851,126 @@ int copy_out(const int16_t* dev, int16_t* fb_out, size_t bytes) {
     return RT_SUCCESS;
 }
 
+// rt_gpu_render's latency path for small-scene whole frames into a registered
+// host framebuffer: after the trace and the AO-call numbering, the frame's
+// rows split in two at row r (the calls of rows [0, r) are the first ones of
+// the serial RNG stream, so the split needs no other change): AO of the first
+// part, then -- on a second stream -- its resolve and copy to the host while
+// the second part's AO runs. Same kernels, same bytes. done = false when the
+// frame does not qualify (the caller takes the plain path).
+static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) {
+    done = false;
+    const int H = p->height, W = p->width;
+    const size_t bytes = (size_t)H * W * 6;
+    if (!g.pipeline || H < 2 || p->row_begin != 0 || p->row_step != 1 || p->row_end != H ||
+        !host_registered(fb_out, bytes) || frame_uses_bvh(p))
+        return RT_SUCCESS;
+    DevFrame f = dev_frame(p, 0, 1, H);
+    const DevScene sc = dev_scene(p);
+    if (!ao_calls_supported(sc, f)) return RT_SUCCESS;
+    // only a (params, scene) whose node capacity is verified (no retry here)
+    g.traced_rows[0] = 0;
+    g.traced_rows[1] = 1;
+    g.traced_rows[2] = H;
+    if (!(g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0 &&
+          std::memcmp(g.verified_rows, g.traced_rows, sizeof g.traced_rows) == 0))
+        return RT_SUCCESS;
+    if (begin_slot(false) || begin_frame()) return RT_FAILURE;
+    const hipStream_t s = fs();
+    HIP_TRY(hipEventRecord(g.ev[EV_START], s));
+    if (trace_rows(p, 0, 1, H)) return RT_FAILURE;
+    if (ensure(SL.fb, bytes)) return RT_FAILURE;
+    int16_t* out = (int16_t*)SL.fb.p;
+    DevWork w = dev_work();
+    HIP_TRY(launch_rank(sc, f, w, nullptr, s));
+    HIP_TRY(hipEventRecord(g.ev[EV_RANK], s));
+    if (prepare_mt_stream(p, nullptr, H)) return RT_FAILURE;
+    w = dev_work();
+    // The split row: the last part should hold few rows (its resolve and copy
+    // are the tail of the call) and enough AO calls that its AO covers the
+    // first part's resolve and copy: the largest row r with at least 35 % of
+    // the frame's calls in rows [r, H). Taken from this frame's per-row counts
+    // once per (params, scene) -- they do not change between calls.
+    if (!(g.lat_gen == g.scene_gen && std::memcmp(&g.lat_params, p, sizeof *p) == 0)) {
+        std::vector<uint32_t> rc((size_t)H);
+        HIP_TRY(hipMemcpyAsync(rc.data(), SL.row_calls.p, (size_t)H * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        uint64_t tot = 0, tail = 0;
+        for (uint32_t v : rc) tot += v;
+        int r = H;
+        while (r > 1 && (tail < (tot * 35 + 99) / 100 || r > H - 1)) tail += rc[(size_t)--r];
+        g.lat_params = *p;
+        g.lat_gen = g.scene_gen;
+        g.lat_row = r;
+    }
+    const int h0 = g.lat_row;
+    const uint32_t p0 = (uint32_t)h0 * (uint32_t)W, np = (uint32_t)H * (uint32_t)W;
+    const uint64_t* split = w.row_base_local + h0;  // calls before row h0
+    HIP_TRY(launch_ao_calls(sc, f, w, nullptr, split, s));
+    HIP_TRY(hipEventRecord(g.aux_go, s));
+    // first half: resolve + copy on the second stream
+    HIP_TRY(hipStreamWaitEvent(g.aux, g.aux_go, 0));
+    HIP_TRY(launch_resolve_range(sc, f, w, out, 0, p0, g.aux));
+    HIP_TRY(hipMemcpyAsync(fb_out, out, (size_t)p0 * 6, hipMemcpyDeviceToHost, g.aux));
+    HIP_TRY(hipEventRecord(g.aux_done, g.aux));
+    // second half
+    HIP_TRY(launch_ao_calls(sc, f, w, split, w.totals, s));
+    HIP_TRY(hipEventRecord(g.ev[EV_AO], s));
+    HIP_TRY(launch_resolve_range(sc, f, w, out, p0, np, s));
+    HIP_TRY(hipEventRecord(g.ev[EV_RESOLVE], s));
+    HIP_TRY(hipMemcpyAsync(fb_out + (size_t)p0 * 3, out + (size_t)p0 * 3, (size_t)(np - p0) * 6,
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamWaitEvent(s, g.aux_done, 0));  // the slot is free once both halves are done
+    if (end_slot()) return RT_FAILURE;
+    HIP_TRY(hipStreamSynchronize(s));
+    done = true;
+    return RT_SUCCESS;
+}
+
 int rt_gpu_render(const rt_render_params* p, int16_t* fb_out) {
+    if (check_params(p)) return RT_FAILURE;
+    HIP_TRY(hipSetDevice(g.device));
+    if (fb_out) {
+        bool done = false;
+        if (render_split(p, fb_out, done)) return RT_FAILURE;
+        if (done) {
+            HIP_TRY(hipStreamSynchronize(g.stream));
+            return RT_SUCCESS;
+        }
+    }
     int16_t* dev = nullptr;
     if (rt_gpu_render_device(p, &dev)) return RT_FAILURE;
     const size_t bytes = (size_t)n_selected_rows(p) * p->width * 6;
-    if (bytes && fb_out && copy_out(dev, fb_out, bytes)) return RT_FAILURE;
+    if (bytes && fb_out && copy_out(dev, fb_out, bytes, fs())) return RT_FAILURE;
     HIP_TRY(hipStreamSynchronize(g.stream));
     return RT_SUCCESS;
+}
+
+int rt_gpu_host_register(void* host_ptr, uint64_t bytes) {
+    if (!host_ptr || bytes == 0) return fail("rt_gpu_host_register: empty range");
+    if (host_registered(host_ptr, bytes)) return RT_SUCCESS;
+    if (!g.inited && rt_gpu_init(-1) != RT_SUCCESS) return RT_FAILURE;
+    HIP_TRY(hipHostRegister(host_ptr, bytes, hipHostRegisterPortable));
+    g_host_ranges.push_back({(const char*)host_ptr, (size_t)bytes});
+    return RT_SUCCESS;
+}
+
+int rt_gpu_host_unregister(void* host_ptr) {
+    for (size_t i = 0; i < g_host_ranges.size(); i++)
+        if (g_host_ranges[i].p == (const char*)host_ptr) {
+            for (int k = 0; k < kMaxCtx; k++)  // no copy into it may still be in flight
+                if (g_ctx[k].inited) {
+                    const int cur = g_cur;
+                    g_cur = k;
+                    (void)hipSetDevice(g.device);
+                    (void)sync_all();
+                    g_cur = cur;
+                }
+            g_host_ranges.erase(g_host_ranges.begin() + (long)i);
+            HIP_TRY(hipHostUnregister(host_ptr));
+            return RT_SUCCESS;
+        }
+    return fail("rt_gpu_host_unregister: %p was not registered", host_ptr);
 }
 
 int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
@@ -1016,6 +1174,9 @@ void shutdown_ctx() {
     }
     for (auto& ev : g.user_mark)
         if (ev) (void)hipEventDestroy(ev);
+    if (g.aux) (void)hipStreamDestroy(g.aux);
+    if (g.aux_go) (void)hipEventDestroy(g.aux_go);
+    if (g.aux_done) (void)hipEventDestroy(g.aux_done);
     for (auto& ev : g.ev_default)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& q : g.prof_pool)

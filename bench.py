@@ -415,17 +415,23 @@ def roofline(workload, k_ms, k_launches, k_rays):
 def render_latency(lib, rt580, params, torch, n=3):
     """Blocking rt_gpu_render (what Render() calls): first launch -> int16
     framebuffer on the host (SURVEY §8d ms/frame), excluding scene load/upload
-    and the PPM write. Mean of n calls after the timed region, after one untimed
-    call (the first sizes the pinned staging buffer of the host copy)."""
+    and the PPM write. The host framebuffer is page-locked once
+    (rt_gpu_host_register), as the class surface does with its own, so the
+    frame lands in it with one DMA. Mean of n calls after the timed region,
+    after one untimed call."""
     import numpy as np
     host = np.zeros(params.width * params.height * 3, dtype=np.int16)
-    rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
-    times = []
-    for _ in range(n):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
+    rt580.check(lib.rt_gpu_host_register(host.ctypes.data, host.nbytes), "rt_gpu_host_register")
+    try:
         rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
-        times.append((time.perf_counter() - t0) * 1e3)
+        times = []
+        for _ in range(n):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
+            times.append((time.perf_counter() - t0) * 1e3)
+    finally:
+        rt580.check(lib.rt_gpu_host_unregister(host.ctypes.data), "rt_gpu_host_unregister")
     return round(sum(times) / len(times), 4)
 
 

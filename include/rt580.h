@@ -163,6 +163,13 @@ int rt_gpu_render(const rt_render_params* params, int16_t* fb_out);
 /* Same, leaving the framebuffer in HBM (device pointer valid until the next
  * call); asynchronous on the shim's stream. */
 int rt_gpu_render_device(const rt_render_params* params, int16_t** fb_device);
+/* Page-lock a host buffer that will receive frames (rt_gpu_render's fb_out):
+ * a frame copied into a registered range lands there with one DMA instead of
+ * through the shim's pinned staging buffer. The caller keeps the buffer alive
+ * until rt_gpu_host_unregister (the class surface registers its framebuffer on
+ * its first Render and unregisters it in its destructor). */
+int rt_gpu_host_register(void* host_ptr, uint64_t bytes);
+int rt_gpu_host_unregister(void* host_ptr);
 /* Multi-rank split of rt_gpu_render_device. Buffers are
  * caller-owned device memory (e.g. torch tensors on this device); the work is
  * queued on the shim's stream (see rt_gpu_set_stream).

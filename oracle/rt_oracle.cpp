@@ -293,8 +293,10 @@ static int load_scene(Scene& sc, const std::string& root, const std::string& pat
         auto doc = ora_json::read(text);
         const ora_json::Node& j = *doc;
         // jsonData["scene"] on the non-const document (:667): absent -> null, so
-        // no shapes, camera or lights; a non-object document is a type error
-        if (j.t != ora_json::Node::OBJ) throw std::runtime_error("document is not an object");
+        // no shapes, camera or lights; a null document becomes an object there,
+        // any other non-object document is a type error
+        if (j.t != ora_json::Node::OBJ && j.t != ora_json::Node::NUL)
+            throw std::runtime_error("document is not an object");
         static const ora_json::Node kNull;
         const ora_json::Node& s = j.has("scene") ? j["scene"] : kNull;
         std::map<std::string, int> cache;

@@ -88,6 +88,10 @@ CASES = {
                              '"Ka": 0.5, "Kd": 0.5, "Ks": 0, "Kt": 0, "n": 2}, "transforms": []}]'),
     "truncated": BASE[:len(BASE) // 2],
     "empty_file": "",
+    "null_document": "null",
+    "array_document": "[]",
+    "number_document": "5",
+    "scene_null": '{"scene": null}',
 }
 MESHES = {
     "lsphere.json": SPHERE_MESH,

@@ -90,7 +90,7 @@ def _shade_with_bases(scene, w, h, depth, ao, offset_calls, root=helpers.ASSETS_
 @pytest.mark.parametrize("ao,periods", [(64, 1), (256, 1), (256, 23)])
 def test_rng_stream_wraps_past_the_minstd_period(ao, periods):
     """Draw indices cross k * (2^31 - 2) inside the frame: the device's
-    modular skip-ahead (minstd_pow) and per-sample table must agree with the
+    modular skip-ahead (rank_kernel: seed * step^call, step = 16807^(2N)) and per-sample table must agree with the
     oracle's serial-stream semantics on both sides of the wrap. periods=23 puts
     the frame near draw 4.9e10, where BASELINE config 5's last rows are."""
     scene, w, h, depth = "simpleSphereScene.json", 40, 30, 4
