@@ -18,7 +18,12 @@
 // would not reproduce the reference's bits. Tables come from this image's libm
 // (tools/gen_glibc_tables.py -> glibc_tables.inc). Equality with the host glibc
 // is checked EXHAUSTIVELY over the input domains the path uses
-// (tests/native/libm_check.cpp, tests/test_libm_port.py; GPU leg in tests/test_gpu_parity.py).
+// (tests/native/libm_check.cpp driven by tests/test_native_checks.py; the device
+// leg, the device powf against the host's glibc, in tests/test_gpu_libm.py).
+//
+// Licence: the algorithms and tables restated here are glibc's (GNU LGPL 2.1
+// or later; the powf tables come from ARM's optimized-routines, MIT/Apache-2.0
+// in that project). INTEGRATION.md records this.
 //
 // Every floating-point expression below must be compiled WITHOUT contraction
 // (-ffp-contract=off): the FMA points of __powf_fma are the explicit fma() calls.
