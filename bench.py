@@ -241,10 +241,11 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     last = None
     for i in range(steps):
         th = time.perf_counter()
-        step()
+        r = step()
         host_s += time.perf_counter() - th
         if i == steps - 1:
-            last = finish()  # the last frame's gather + de-interleave belong to the timed region
+            # the last frame's gather + de-interleave belong to the timed region
+            last = finish() if dframe is not None else r
         if synth:  # long frames: keep a progress line per step (sync costs microseconds)
             torch.cuda.synchronize()
             if ctx.rank == 0:
