@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/rt580.h"
 #include "rt_isect.h"
 
@@ -135,6 +137,26 @@ struct DevWork {
     uint32_t* call_hint;
     uint32_t aofix_cap;
 };
+
+// Host reads of device counts during a frame's enqueue (trace-level ray
+// counts, far-queue lengths and segment counts, the AO-call total) go through
+// the current count schedule. RECORD reads each count (a D2H copy and a sync
+// of the frame's stream) and appends it; REPLAY takes the counts from the
+// recorded list instead -- the frame then enqueues without a host sync, so
+// consecutive frames overlap on the two frame slots -- and enqueues a device
+// check per count that sets *bad when the frame's own count differs. The
+// counts are a function of (scene, params, rows, chunk size); the shim
+// replays only a verified repeat of the frame that recorded them, and fails
+// the frame when *bad is set (rt_shim.cpp begin_slot).
+struct CountSchedule {
+    enum Mode { OFF, RECORD, REPLAY };
+    Mode mode = OFF;
+    std::vector<uint32_t> vals;
+    size_t pos = 0;
+    uint32_t* bad = nullptr;  // device word (REPLAY)
+    bool broken = false;      // REPLAY asked for more counts than were recorded
+};
+void set_count_schedule(CountSchedule* cs);  // null: plain reads
 
 hipError_t upload_minstd_table(hipStream_t s);
 // Breadth-first trace of all levels: nodes, shading except AO, per-pixel counters.

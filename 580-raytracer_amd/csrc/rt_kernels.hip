@@ -2278,6 +2278,42 @@ static const char* g_where = "";
 const char* launch_where() { return g_where; }
 #define RT_STEP(what) (g_where = (what))
 
+static thread_local CountSchedule* g_cs = nullptr;
+void set_count_schedule(CountSchedule* cs) { g_cs = cs; }
+
+__global__ void count_check_kernel(const uint32_t* dev, uint32_t e0, uint32_t e1, int n, uint32_t* bad) {
+    if (threadIdx.x == 0 && (dev[0] != e0 || (n > 1 && dev[1] != e1))) *bad = 1u;
+}
+
+// n (1 or 2) device words -> out (pinned), through the count schedule.
+static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStream_t s) {
+    if (g_cs && g_cs->mode == CountSchedule::REPLAY) {
+        if (g_cs->pos + (size_t)n > g_cs->vals.size()) {
+            g_cs->broken = true;
+            return hipErrorInvalidValue;
+        }
+        for (int i = 0; i < n; i++) out[i] = g_cs->vals[g_cs->pos++];
+        uint32_t e0 = out[0];
+#ifdef RT580_DIAGNOSTICS
+        {   // DIAGNOSTIC build only: RT580_REPLAY_CORRUPT=1 makes every check fail (tests the detection)
+            static int corrupt = -1;
+            if (corrupt < 0) {
+                const char* ev = getenv("RT580_REPLAY_CORRUPT");
+                corrupt = ev ? atoi(ev) : 0;
+            }
+            if (corrupt) e0 ^= 1u;
+        }
+#endif
+        hipLaunchKernelGGL(count_check_kernel, dim3(1), dim3(64), 0, s, dev, e0, n > 1 ? out[1] : 0u, n, g_cs->bad);
+        return hipGetLastError();
+    }
+    hipError_t e = hipMemcpyAsync(out, dev, (size_t)n * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess && g_cs && g_cs->mode == CountSchedule::RECORD)
+        for (int i = 0; i < n; i++) g_cs->vals.push_back(out[i]);
+    return e;
+}
+
 // Work items of the cell pass: segment k (W.far_vals[k] rays) is cut into
 // ceil(count / 64) chunks; chunk counts first (into far_keys_alt, free after
 // the run-length encoding), then, after their scan into far_wofs, one entry
@@ -2320,8 +2356,7 @@ static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t
     RT_STEP("far queue segments");
     hipError_t e = hipcub::DeviceRunLengthEncode::Encode(W.sort_tmp, tmp, W.far_keys_alt, W.far_keys, W.far_vals,
                                                          W.far_seg_n, (int)n, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(W.far_count_host + 2, W.far_seg_n, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = read_counts(W.far_seg_n, 1, W.far_count_host + 2, s);
     if (e != hipSuccess) return e;
     const uint32_t nseg = W.far_count_host[2];
     if (nseg == 0) return hipSuccess;
@@ -2551,8 +2586,7 @@ void kernel_timer_release() {
 // Sort the far queue (W.far_count entries) by direction key; returns its length.
 static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
     RT_STEP("far queue count D2H");
-    hipError_t e = hipMemcpyAsync(W.far_count_host, W.far_count, 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipError_t e = read_counts(W.far_count, 2, W.far_count_host, s);
     if (e != hipSuccess) return e;
     nq = W.far_count_host[0];
     nb = W.far_count_host[1];  // far-origin rays: keyed to sort last
@@ -2596,9 +2630,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
             uint32_t count = (uint32_t)npix;
             if (level > 0) {
                 RT_STEP("level count D2H");
-                if ((e = hipMemcpyAsync(W.far_count_host, W.lvl + level, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-                    (e = hipStreamSynchronize(s)) != hipSuccess)
-                    return e;
+                if ((e = read_counts(W.lvl + level, 1, W.far_count_host, s)) != hipSuccess) return e;
                 count = *W.far_count_host;
             }
             if (count == 0) {  // still publish the next level's base
@@ -2767,10 +2799,9 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
     if (S.use_bvh) {
         // chunks of the AO items: near pass + queue, sort the misses by
         // direction, wave-cooperative far pass
-        uint64_t calls = 0;
-        hipError_t e = hipMemcpyAsync(&calls, W.totals, 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        hipError_t e = read_counts(reinterpret_cast<const uint32_t*>(W.totals), 2, W.far_count_host + 4, s);
         if (e != hipSuccess) return e;
+        const uint64_t calls = (uint64_t)W.far_count_host[4] | ((uint64_t)W.far_count_host[5] << 32);
         const uint64_t items = calls * (uint64_t)F.ao_samples;
         const bool split = ao_split() != 0 && W.ao_rays && S.bv.nodes4 && !near_wave();
         if (W.call_hint && S.bv.has_far && calls &&

@@ -56,6 +56,7 @@ const Knob kKnobs[] = {
     {"RT580_CALL_HINT", INT_SET, 0, 0, k01, nullptr},
     {"RT580_MULTI_TRANSPORT", STRING_SET, 0, 0, nullptr, kTransport},
     {"RT580_GPUS", INT_RANGE, 1, 16, nullptr, nullptr},
+    {"RT580_REPLAY", INT_SET, 0, 0, k01, nullptr},
     // rt_bvh.cpp
     {"RT580_LEAF_MAX", INT_RANGE, 1, 8, nullptr, nullptr},
     {"RT580_BVH_INFLATE", FLOAT_NONNEG, 0, 0, nullptr, nullptr},
@@ -81,6 +82,7 @@ const Knob kKnobs[] = {
     // diagnostic builds (make diag) only
     {"RT580_BVH_DIAG", DIAG_ONLY, 0, 0, nullptr, nullptr},
     {"RT580_DUMP_FAR", DIAG_ONLY, 0, 0, nullptr, nullptr},
+    {"RT580_REPLAY_CORRUPT", DIAG_ONLY, 0, 0, nullptr, nullptr},
     // read by the Python binding and the tests, not by the library
     {"RT580_LIB", NOT_LIBRARY, 0, 0, nullptr, nullptr},
     {"RT580_EXHAUSTIVE", NOT_LIBRARY, 0, 0, nullptr, nullptr},

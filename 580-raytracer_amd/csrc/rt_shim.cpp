@@ -41,6 +41,25 @@ struct Slot {
     DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
         row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream, aofix_items, aofix_count,
         call_hint;
+    // BVH frames: the far queue, the AO ray records and the split trace's
+    // provisional hits -- per slot, so that consecutive BVH frames overlap
+    // like the others (count schedule replay, see trace_rows)
+    DevBuf ao_rays, ao_late, ao_late_count, far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count,
+        far_seg_off, far_seg_n, far_wofs, far_work, sort_tmp, hit4, hit_prim, shadow;
+    uint32_t far_cap = 0, ao_cap = 0;
+    // replayed count schedules: the device checks' flag, its host copy (read
+    // when the slot is next used), and whether a replayed frame is unchecked
+    DevBuf bad;
+    uint32_t* bad_host = nullptr;  // pinned
+    bool check_pending = false;
+};
+
+// Key of a recorded count schedule: the frame it was recorded on.
+struct SchedKey {
+    rt_render_params p;
+    uint64_t gen;
+    int rows[3];
+    uint32_t far_chunk, ao_chunk;  // the frame's chunk sizes (they set the passes' sequence)
 };
 
 struct State {
@@ -87,13 +106,14 @@ struct State {
     rt_render_params lat_params{};
     uint64_t lat_gen = ~0ull;
     int lat_row = -1;
-    // BVH far-queue buffers (BVH frames always run serialized on slot 0)
-    DevBuf ao_rays, ao_late, ao_late_count;
-    DevBuf far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count, sort_tmp, hit4, hit_prim, shadow,
-        far_seg_off, far_seg_n, far_wofs, far_work;
-    uint32_t* far_count_host = nullptr;  // pinned
-    uint32_t far_cap = 0;
-    uint32_t ao_cap = 0;
+    uint32_t* far_count_host = nullptr;  // pinned: counts read on the host (rt_kernels.hip read_counts)
+    // count schedules of the trace phase and of the AO phase (rt_kernels.h
+    // CountSchedule), each valid for the frame of its key
+    CountSchedule sched_trace, sched_ao;
+    SchedKey key_trace{}, key_ao{};
+    bool trace_valid = false, ao_valid = false;
+    bool replayed = false;  // the frame being enqueued replays a schedule (its check is pending)
+    uint32_t frame_fc = 0, frame_ac = 0;  // chunk sizes of the frame being enqueued (<= the slot's buffers)
     int chunk_log2 = 26;  // largest far-queue / AO-ray chunk: 2^chunk_log2 rays (RT580_CHUNK_LOG2)
     uint32_t node_cap = 0, call_cap = 0;
     double node_factor = 4.0;         // node capacity per pixel (grown on overflow)
@@ -143,21 +163,26 @@ int fail(const char* fmt, ...) {
 
 // Frame pipelining. Consecutive frame calls alternate between two slots (own
 // stream and workspace), so frame k+1's latency-bound trace overlaps frame k's
-// AO kernel. Ordering:
+// AO kernels. BVH frames too: their host reads (trace-level counts, the AO-call
+// total) synchronize their own slot's stream only, and their AO chunks enqueue
+// without one (binned far queue), so the host returns while frame k's AO runs
+// and frame k+1's trace levels run beside it. Ordering:
 //  - a frame on the slot the PREVIOUS call did not use waits on the caller's
 //    stream as it was at the start of the previous call (user_mark): that
 //    covers whatever the caller queued against this slot's last framebuffer
 //    before it made that call;
-//  - a frame on the same slot as the previous call (a BVH frame after a slot-0
-//    frame; see below) waits on the caller's stream as it is now, so work the
-//    caller queued against the previous frame's framebuffer completes first;
+//  - a frame on the same slot as the previous call (serialize) waits on the
+//    caller's stream as it is now, so work the caller queued against the
+//    previous frame's framebuffer completes first;
 //  - the caller's stream waits for the frame (end_slot), so work the caller
 //    queues after the call sees its results ("asynchronous on the shim's stream").
-// BVH frames (host syncs inside, shared far-queue buffers) always run on slot 0.
+int check_replay(Slot& sl);
+int post_replay_check();
+
 int begin_slot(bool serialize) {
     if (!g.pipeline) {
         g.cur = 0;
-        return RT_SUCCESS;
+        return check_replay(SL);
     }
     const int k = (int)(g.frames & 1);
     HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));  // this call's start
@@ -165,6 +190,7 @@ int begin_slot(bool serialize) {
     const hipEvent_t wait = (g.frames == 0 || slot == g.last_slot) ? g.user_mark[k] : g.user_mark[k ^ 1];
     g.cur = slot;
     g.last_slot = slot;
+    if (check_replay(SL)) return RT_FAILURE;
     HIP_TRY(hipStreamWaitEvent(SL.stream, wait, 0));
     g.frames++;
     return RT_SUCCESS;
@@ -172,6 +198,7 @@ int begin_slot(bool serialize) {
 
 // The caller's stream waits for what the current slot has enqueued.
 int end_slot() {
+    if (post_replay_check()) return RT_FAILURE;
     if (!g.pipeline) return RT_SUCCESS;
     HIP_TRY(hipEventRecord(SL.done, SL.stream));
     HIP_TRY(hipStreamWaitEvent(g.stream, SL.done, 0));
@@ -339,30 +366,30 @@ DevWork dev_work() {
     w.mt_stream = (const uint32_t*)SL.mt_stream.p;
     w.node_cap = g.node_cap;
     w.call_cap = g.call_cap;
-    w.far_rays = (float4*)g.far_rays.p;
-    w.far_keys = (uint32_t*)g.far_keys.p;
-    w.far_keys_alt = (uint32_t*)g.far_keys_alt.p;
-    w.far_vals = (uint32_t*)g.far_vals.p;
-    w.far_vals_alt = (uint32_t*)g.far_vals_alt.p;
-    w.far_count = (uint32_t*)g.far_count.p;
-    w.far_seg_off = (uint32_t*)g.far_seg_off.p;
-    w.far_seg_n = (uint32_t*)g.far_seg_n.p;
-    w.far_wofs = (uint32_t*)g.far_wofs.p;
-    w.far_work = (uint4*)g.far_work.p;
+    w.far_rays = (float4*)SL.far_rays.p;
+    w.far_keys = (uint32_t*)SL.far_keys.p;
+    w.far_keys_alt = (uint32_t*)SL.far_keys_alt.p;
+    w.far_vals = (uint32_t*)SL.far_vals.p;
+    w.far_vals_alt = (uint32_t*)SL.far_vals_alt.p;
+    w.far_count = (uint32_t*)SL.far_count.p;
+    w.far_seg_off = (uint32_t*)SL.far_seg_off.p;
+    w.far_seg_n = (uint32_t*)SL.far_seg_n.p;
+    w.far_wofs = (uint32_t*)SL.far_wofs.p;
+    w.far_work = (uint4*)SL.far_work.p;
     w.far_count_host = g.far_count_host;
-    w.sort_tmp = g.sort_tmp.p;
-    w.sort_tmp_bytes = g.sort_tmp.bytes;
-    w.far_cap = g.far_cap;
-    w.ao_rays = g.ao_cap ? (float4*)g.ao_rays.p : nullptr;
-    w.ao_cap = g.ao_cap;
-    w.ao_late = g.ao_cap ? (uint32_t*)g.ao_late.p : nullptr;
-    w.ao_late_count = g.ao_cap ? (uint32_t*)g.ao_late_count.p : nullptr;
+    w.sort_tmp = SL.sort_tmp.p;
+    w.sort_tmp_bytes = SL.sort_tmp.bytes;
+    w.far_cap = std::min(SL.far_cap, g.frame_fc);
+    w.ao_cap = std::min(SL.ao_cap, g.frame_ac);
+    w.ao_rays = w.ao_cap ? (float4*)SL.ao_rays.p : nullptr;
+    w.ao_late = w.ao_cap ? (uint32_t*)SL.ao_late.p : nullptr;
+    w.ao_late_count = w.ao_cap ? (uint32_t*)SL.ao_late_count.p : nullptr;
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
-    w.hit4 = split ? (float4*)g.hit4.p : nullptr;
-    w.hit_prim = split ? (int32_t*)g.hit_prim.p : nullptr;
+    w.hit4 = split ? (float4*)SL.hit4.p : nullptr;
+    w.hit_prim = split ? (int32_t*)SL.hit_prim.p : nullptr;
     // shadow flags of the split trace's lights (more than 8: decided in the shading phase)
-    w.shadow = (split && g.shadow.p && !g.shadow_lights.empty() && g.shadow_lights.size() <= 8) ? (uint8_t*)g.shadow.p
-                                                                                                    : nullptr;
+    w.shadow = (split && SL.shadow.p && !g.shadow_lights.empty() && g.shadow_lights.size() <= 8) ? (uint8_t*)SL.shadow.p
+                                                                                                      : nullptr;
     w.aofix_items = (uint64_t*)SL.aofix_items.p;
     w.aofix_count = (uint32_t*)SL.aofix_count.p;
     {   // RT580_CALL_HINT=0 (A/B): no per-call acceptor hints
@@ -401,11 +428,12 @@ int begin_frame() {
 void set_chunk_log2(int log2) {
     if (g.chunk_log2 == log2) return;
     g.chunk_log2 = log2;
-    for (DevBuf* b : {&g.far_rays, &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.sort_tmp, &g.ao_rays,
-                      &g.far_seg_off, &g.far_wofs, &g.far_work,
-                      &g.ao_late, &g.shadow})
-        release(*b);
-    g.far_cap = g.ao_cap = 0;
+    for (Slot& sl : g.slot) {
+        for (DevBuf* b : {&sl.far_rays, &sl.far_keys, &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.sort_tmp,
+                          &sl.ao_rays, &sl.far_seg_off, &sl.far_wofs, &sl.far_work, &sl.ao_late, &sl.shadow})
+            release(*b);
+        sl.far_cap = sl.ao_cap = 0;
+    }
 }
 
 // Size the workspace for n_rows x width pixels.
@@ -438,29 +466,119 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     const uint64_t chunk_max = 1ull << g.chunk_log2;
     const uint64_t ao_items = p->ao_enabled && g.n_ambient > 0 ? ccap * (uint64_t)p->ao_samples : 0;
     const uint32_t ac = (uint32_t)std::min(chunk_max, pow2ceil(ao_items));
-    if (g.bvh_ok && g.ao_cap < ac) {  // ray records of the split AO pass (ao_trace_kernel)
-        if (ensure(g.ao_rays, (size_t)ac * 32) || ensure(g.ao_late, (size_t)ac * 4) || ensure(g.ao_late_count, 64))
+    g.frame_ac = g.bvh_ok ? ac : 0;
+    g.frame_fc = 0;
+    if (g.bvh_ok && SL.ao_cap < ac) {  // ray records of the split AO pass (ao_trace_kernel)
+        if (ensure(SL.ao_rays, (size_t)ac * 32) || ensure(SL.ao_late, (size_t)ac * 4) || ensure(SL.ao_late_count, 64))
             return RT_FAILURE;
-        g.ao_cap = ac;
+        SL.ao_cap = ac;
     }
+    if (!g.bvh_ok || g.bvh.far_nodes.empty()) return RT_SUCCESS;
     const uint32_t fc = (uint32_t)std::min(chunk_max, pow2ceil(std::max<uint64_t>(cap, ac)));
-    if (g.bvh_ok && !g.bvh.far_nodes.empty() && g.far_cap < fc) {
-        if (ensure(g.far_rays, (size_t)fc * 32) || ensure(g.far_keys, (size_t)fc * 4) ||
-            ensure(g.far_keys_alt, (size_t)fc * 4) || ensure(g.far_vals, (size_t)fc * 4) ||
-            ensure(g.far_vals_alt, (size_t)fc * 4) || ensure(g.far_count, 64) ||
-            ensure(g.far_seg_off, (size_t)fc * 4) || ensure(g.far_seg_n, 64) || ensure(g.far_wofs, (size_t)fc * 4) ||
-            ensure(g.far_work, ((size_t)fc + fc / 64 + 64) * 16) ||
-            ensure(g.sort_tmp, far_sort_tmp_bytes(fc) + 256))
+    g.frame_fc = fc;
+    if (SL.far_cap < fc) {
+        if (ensure(SL.far_rays, (size_t)fc * 32) || ensure(SL.far_keys, (size_t)fc * 4) ||
+            ensure(SL.far_keys_alt, (size_t)fc * 4) || ensure(SL.far_vals, (size_t)fc * 4) ||
+            ensure(SL.far_vals_alt, (size_t)fc * 4) || ensure(SL.far_count, 64) ||
+            ensure(SL.far_seg_off, (size_t)fc * 4) || ensure(SL.far_seg_n, 64) || ensure(SL.far_wofs, (size_t)fc * 4) ||
+            ensure(SL.far_work, ((size_t)fc + fc / 64 + 64) * 16) ||
+            ensure(SL.sort_tmp, far_sort_tmp_bytes(fc) + 256))
             return RT_FAILURE;
-        g.far_cap = fc;
+        SL.far_cap = fc;
     }
-    if (g.bvh_ok && !g.bvh.far_nodes.empty() &&
-        (ensure(g.hit4, (size_t)cap * 16) || ensure(g.hit_prim, (size_t)cap * 4)))
-        return RT_FAILURE;
-    if (g.bvh_ok && !g.bvh.far_nodes.empty() && !g.shadow_lights.empty() && g.shadow_lights.size() <= 8 &&
-        ensure(g.shadow, g.shadow_lights.size() * (size_t)g.far_cap))
+    if (ensure(SL.hit4, (size_t)cap * 16) || ensure(SL.hit_prim, (size_t)cap * 4)) return RT_FAILURE;
+    if (!g.shadow_lights.empty() && g.shadow_lights.size() <= 8 &&
+        ensure(SL.shadow, g.shadow_lights.size() * (size_t)fc))
         return RT_FAILURE;
     return RT_SUCCESS;
+}
+
+// ---------------------------------------------------------------- count schedules
+// A BVH frame reads a few device counts on the host while it is enqueued
+// (rt_kernels.h CountSchedule). They are a function of the frame's key, so a
+// repeat of a verified frame replays the counts recorded on an earlier run of
+// it: no host sync, and the next frame's trace overlaps this frame's AO on the
+// other slot. Every replayed count is checked on the device; a mismatch fails
+// the call that next uses the slot (check_replay), and drops the schedules.
+SchedKey sched_key(const rt_render_params* p) {
+    SchedKey k;
+    std::memset(&k, 0, sizeof k);
+    k.p = *p;
+    k.gen = g.scene_gen;
+    std::memcpy(k.rows, g.traced_rows, sizeof k.rows);
+    k.far_chunk = g.frame_fc;
+    k.ao_chunk = g.frame_ac;
+    return k;
+}
+
+bool same_key(const SchedKey& a, const SchedKey& b) {
+    static int on = -1;  // RT580_REPLAY=0 (A/B): every frame reads its counts on the host
+    if (on < 0) {
+        const char* e = std::getenv("RT580_REPLAY");
+        on = e ? std::atoi(e) : 1;
+    }
+    return on && std::memcmp(&a, &b, sizeof a) == 0;
+}
+
+// (params, scene, traced rows) already rendered without node overflow
+bool frame_verified(const rt_render_params* p) {
+    return g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0 &&
+           std::memcmp(g.verified_rows, g.traced_rows, sizeof g.traced_rows) == 0;
+}
+
+int begin_schedule(CountSchedule& cs, bool replay) {
+    if (replay) {
+        if (ensure(SL.bad, 64)) return RT_FAILURE;
+        if (!SL.bad_host) {
+            HIP_TRY(hipHostMalloc((void**)&SL.bad_host, 64, hipHostMallocDefault));
+            *SL.bad_host = 0;
+            HIP_TRY(hipMemsetAsync(SL.bad.p, 0, 64, fs()));
+        }
+        cs.mode = CountSchedule::REPLAY;
+        cs.pos = 0;
+        cs.broken = false;
+        cs.bad = (uint32_t*)SL.bad.p;
+        g.replayed = true;
+    } else {
+        cs.mode = CountSchedule::RECORD;
+        cs.vals.clear();
+    }
+    set_count_schedule(&cs);
+    return RT_SUCCESS;
+}
+
+int end_schedule(CountSchedule& cs, const char* what, hipError_t e) {
+    set_count_schedule(nullptr);
+    if (cs.mode == CountSchedule::REPLAY && (cs.broken || (e == hipSuccess && cs.pos != cs.vals.size()))) {
+        g.trace_valid = g.ao_valid = false;
+        return fail("replayed %s count schedule does not fit the frame (%zu of %zu counts used)", what, cs.pos,
+                    cs.vals.size());
+    }
+    return RT_SUCCESS;
+}
+
+// After a frame that replayed a schedule: its check flag to the host, read
+// when the slot is used next (the frame is complete by then).
+int post_replay_check() {
+    if (!g.replayed) return RT_SUCCESS;
+    g.replayed = false;
+    HIP_TRY(hipMemcpyAsync(SL.bad_host, SL.bad.p, 4, hipMemcpyDeviceToHost, fs()));
+    SL.check_pending = true;
+    return RT_SUCCESS;
+}
+
+// The replay check of the slot's last frame (waits for that frame).
+int check_replay(Slot& sl) {
+    if (!sl.check_pending) return RT_SUCCESS;
+    if (g.pipeline) HIP_TRY(hipEventSynchronize(sl.done));
+    else HIP_TRY(hipStreamSynchronize(g.stream));
+    sl.check_pending = false;
+    if (*sl.bad_host == 0) return RT_SUCCESS;
+    *sl.bad_host = 0;
+    HIP_TRY(hipMemset(sl.bad.p, 0, 64));
+    g.trace_valid = g.ao_valid = false;
+    return fail("a replayed count schedule did not match its frame's counts (the frame two calls back on this "
+                "context; schedules dropped)");
 }
 
 // Phase 1: trace every level of the selected rows and count their AO calls.
@@ -473,8 +591,18 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     g.traced_rows[1] = row_step;
     g.traced_rows[2] = n_rows;
     {
+        const SchedKey key = sched_key(p);
+        const bool replay = g.trace_valid && same_key(g.key_trace, key);
+        if (begin_schedule(g.sched_trace, replay)) return RT_FAILURE;
+        if (!replay) {
+            g.key_trace = key;
+            g.trace_valid = false;
+        }
         const hipError_t e = launch_trace(sc, f, dev_work(), fs());
+        if (end_schedule(g.sched_trace, "trace", e)) return RT_FAILURE;
         if (e != hipSuccess) return fail("launch_trace (%s): %s", launch_where(), hipGetErrorString(e));
+        // a verified frame cannot overflow: its recording is valid at once (else check_capacity decides)
+        if (!replay && frame_verified(p)) g.trace_valid = true;
     }
     HIP_TRY(launch_row_counts(sc, f, dev_work(), fs()));
     HIP_TRY(hipEventRecord(g.ev[EV_TRACE], fs()));
@@ -523,7 +651,19 @@ int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     HIP_TRY(hipEventRecord(g.ev[EV_RANK], fs()));
     if (prepare_mt_stream(p, row_base_global, n_rows)) return RT_FAILURE;
     DevWork w = dev_work();
-    HIP_TRY(launch_ao(sc, f, w, fs()));
+    {
+        const SchedKey key = sched_key(p);
+        const bool replay = g.ao_valid && same_key(g.key_ao, key);
+        if (begin_schedule(g.sched_ao, replay)) return RT_FAILURE;
+        if (!replay) {
+            g.key_ao = key;
+            g.ao_valid = false;
+        }
+        const hipError_t e = launch_ao(sc, f, w, fs());
+        if (end_schedule(g.sched_ao, "AO", e)) return RT_FAILURE;
+        HIP_TRY(e);
+        if (!replay && frame_verified(p)) g.ao_valid = true;
+    }
     HIP_TRY(hipEventRecord(g.ev[EV_AO], fs()));
     HIP_TRY(launch_resolve(sc, f, w, fb_out, fs()));
     HIP_TRY(hipEventRecord(g.ev[EV_RESOLVE], fs()));
@@ -553,6 +693,8 @@ int check_capacity(const rt_render_params* p, bool& retry) {
     g.verified_gen = g.scene_gen;
     std::memcpy(g.verified_rows, g.traced_rows, sizeof g.traced_rows);
     g.verified_valid = true;
+    // this frame's trace recording (no overflow) is valid for its repeats
+    if (g.sched_trace.mode == CountSchedule::RECORD && same_key(g.key_trace, sched_key(p))) g.trace_valid = true;
     return RT_SUCCESS;
 }
 
@@ -767,7 +909,7 @@ int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     // The RNG offsets need every row before a selected one: render the prefix
     // [0, row_end) and copy the selected rows out when the selection is sparse.
     const int n_rows = prefix ? n_sel : p->row_end;
-    if (begin_slot(frame_uses_bvh(p))) return RT_FAILURE;
+    if (begin_slot(false)) return RT_FAILURE;
     for (int attempt = 0; attempt < 4; attempt++) {
         if (begin_frame()) return RT_FAILURE;
         HIP_TRY(hipEventRecord(g.ev[EV_START], fs()));
@@ -943,7 +1085,7 @@ int rt_gpu_render(const rt_render_params* p, int16_t* fb_out) {
     const size_t bytes = (size_t)n_selected_rows(p) * p->width * 6;
     if (bytes && fb_out && copy_out(dev, fb_out, bytes, fs())) return RT_FAILURE;
     HIP_TRY(hipStreamSynchronize(g.stream));
-    return RT_SUCCESS;
+    return check_replay(SL);  // the frame is complete: its replayed counts are checked now
 }
 
 int rt_gpu_host_register(void* host_ptr, uint64_t bytes) {
@@ -978,7 +1120,7 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
     if (!row_calls_device) return fail("row_calls_device is NULL");
     HIP_TRY(hipSetDevice(g.device));
     const int n_rows = n_selected_rows(p);
-    if (begin_slot(frame_uses_bvh(p))) return RT_FAILURE;
+    if (begin_slot(false)) return RT_FAILURE;
     for (int attempt = 0; attempt < 4; attempt++) {
         if (begin_frame()) return RT_FAILURE;
         HIP_TRY(hipEventRecord(g.ev[EV_START], fs()));
@@ -1158,17 +1300,19 @@ void shutdown_ctx() {
     (void)sync_all();
     for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always})
         release(*b);
-    for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute, &g.far_rays,
-                      &g.ao_rays, &g.ao_late, &g.ao_late_count, &g.far_keys, &g.far_keys_alt, &g.far_vals, &g.far_vals_alt, &g.far_count, &g.sort_tmp,
-                      &g.far_seg_off, &g.far_wofs, &g.far_work, &g.far_seg_n,
-                      &g.hit4, &g.hit_prim, &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.shadow})
+    for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute,
+                      &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims})
         release(*b);
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
                           &sl.row_calls, &sl.row_hits, &sl.row_nodes, &sl.row_base_local, &sl.totals, &sl.call_node,
                           &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.mt_stream, &sl.aofix_items, &sl.aofix_count,
-                          &sl.call_hint})
+                          &sl.call_hint, &sl.ao_rays, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
+                          &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.far_count, &sl.far_seg_off,
+                          &sl.far_seg_n, &sl.far_wofs, &sl.far_work, &sl.sort_tmp, &sl.hit4, &sl.hit_prim, &sl.shadow,
+                          &sl.bad})
             release(*b);
+        if (sl.bad_host) (void)hipHostFree(sl.bad_host);
         if (sl.stream) (void)hipStreamDestroy(sl.stream);
         if (sl.done) (void)hipEventDestroy(sl.done);
     }

@@ -246,10 +246,8 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
         if i == steps - 1:
             # the last frame's gather + de-interleave belong to the timed region
             last = finish() if dframe is not None else r
-        if synth:  # long frames: keep a progress line per step (sync costs microseconds)
-            torch.cuda.synchronize()
-            if ctx.rank == 0:
-                log("%s: step %d done" % (name, i))
+        if synth and ctx.rank == 0:  # long frames: a progress line per enqueued step (no sync: frames overlap)
+            log("%s: step %d enqueued" % (name, i))
     ctx.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -515,8 +513,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--rehearse", action="store_true",
                     help="--gpus N on a box with fewer GPUs: split the frame N ways on device 0 (device copies)")
-    ap.add_argument("--steps", type=int, default=None, help="default 20 (config2), 2 (synthetic)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 3 (config2), 1 (synthetic)")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="default 20 (config2), 10 (synthetic 1080p), 3 (synthetic 4K / 8K)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true", help="skip the north_star sub-record (config2)")
     ap.add_argument("--no-check", action="store_true", help="skip the reference-hash check of the last frame")
@@ -536,13 +535,18 @@ def main():
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     synth = WORKLOADS[args.workload][1]
-    steps = args.steps if args.steps is not None else (2 if synth else 20)
-    warmup = args.warmup if args.warmup is not None else (1 if synth else 3)
+    # 3 warmup frames: the first verifies the node capacity and records the
+    # trace phase's host reads, the second the AO phase's; from the third on a
+    # frame replays them and enqueues without a host sync (rt_shim.cpp
+    # count schedules), so consecutive frames overlap on the two slots
+    big = WORKLOADS[args.workload][2] * WORKLOADS[args.workload][3] > 1920 * 1080
+    steps = args.steps if args.steps is not None else (20 if not synth else (3 if big else 10))
+    warmup = args.warmup if args.warmup is not None else 3
 
     ctx = Ctx(args)
     out = run_workload(ctx, args.workload, steps, warmup, not args.no_cpu_baseline, not args.no_check)
     if args.workload == "config2" and not args.no_north_star:
-        ns = run_workload(ctx, "field100k_1080p", 5, 2, not args.no_cpu_baseline, False)
+        ns = run_workload(ctx, "field100k_1080p", 10, 3, not args.no_cpu_baseline, False)
         if out is not None:
             out["north_star"] = ns
     if out is not None:

@@ -23,10 +23,10 @@ def _params(scene, w, h, depth, ao, root):
 
 
 def test_pipelined_frames_alternating_accel_keep_each_framebuffer():
-    """BVH frames run on slot 0; a brute-force frame after one must not
-    overwrite slot 0's framebuffer while work the caller queued against it (a
-    delayed read on the caller's stream) is still pending (rt_shim.cpp
-    begin_slot)."""
+    """Consecutive frames alternate between two slots, BVH frames included;
+    a frame must not overwrite a slot's framebuffer while work the caller
+    queued against it (a delayed read on the caller's stream) is still
+    pending (rt_shim.cpp begin_slot)."""
     import torch
     rt580 = helpers.rt580()
     lib = rt580.load()
@@ -45,7 +45,7 @@ def test_pipelined_frames_alternating_accel_keep_each_framebuffer():
     try:
         for i in range(8):
             k = i % 2
-            assert lib.rt_gpu_set_accel(1 if k == 0 else 0) == 0  # BVH (slot 0) / brute (pipelined)
+            assert lib.rt_gpu_set_accel(1 if k == 0 else 0) == 0  # BVH / brute force
             fbp = ctypes.c_void_p()
             rt580.check(lib.rt_gpu_render_device(ctypes.byref(rts[k][1]), ctypes.byref(fbp)), "render_device")
             torch.cuda._sleep(2_000_000)  # the caller's read of this frame's fb is late
@@ -113,3 +113,94 @@ def test_count_rows_then_full_render_same_params():
         lib.rt_gpu_set_stream(lib.rt_gpu_own_stream())
     ref, _ = helpers.oracle_render(scene, w, h, depth, ao, True)
     assert np.array_equal(host.reshape(h, w, 3), ref)
+
+
+def _device_frames(lib, rt580, seq, n, dev, torch):
+    """rt_gpu_render_device for each params in seq, without a host sync in
+    between; each frame's gamma-mapped bytes copied on the caller's stream."""
+    outs = []
+    for prm in seq:
+        fbp = ctypes.c_void_p()
+        rt580.check(lib.rt_gpu_render_device(ctypes.byref(prm), ctypes.byref(fbp)), "render_device")
+        o = torch.empty(n, dtype=torch.uint8, device=dev)
+        rt580.check(lib.rt_gpu_gamma_u8(fbp, n, o.data_ptr()), "gamma_u8")
+        outs.append(o)
+    torch.cuda.synchronize()
+    return [o.cpu().numpy().tobytes() for o in outs]
+
+
+def test_replayed_bvh_frames_match_oracle():
+    """Repeats of a verified BVH frame replay its recorded host reads (count
+    schedule, rt_shim.cpp trace_rows / shade_rows) and enqueue without a host
+    sync, overlapping on the two slots. Many chunks per pass (chunk limit
+    2^8), two interleaved configurations, a chunk-limit change in between
+    (new key: recorded again): every frame equals the CPU restatement."""
+    import torch
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    root = helpers.synthetic_root("cornell10k")
+    w, h = 48, 27
+    cfg = [(4, 16), (2, 8)]
+    want = []
+    for d, a in cfg:
+        ref, _ = helpers.oracle_render("cornell10k.json", w, h, d, a, True, root=root)
+        want.append(rt580.ppm_bytes(ref).split(b"\n", 3)[3])
+    rts = [_params("cornell10k.json", w, h, d, a, root) for d, a in cfg]
+    s = rts[0][0].scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    dev = torch.device("cuda", 0)
+    rt580.check(lib.rt_gpu_set_stream(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "stream")
+    n = w * h * 3
+    order = [0, 0, 0, 0, 1, 1, 1, 0, 1, 0]
+    try:
+        for log2 in (8, 26):
+            assert lib.rt580_set_chunk_log2(log2) == 0
+            got = _device_frames(lib, rt580, [rts[k][1] for k in order], n, dev, torch)
+            assert lib.rt_gpu_accel_active() == 1
+            for i, (k, b) in enumerate(zip(order, got)):
+                assert b == want[k], "frame %d (config %d, chunk 2^%d) differs" % (i, k, log2)
+        # the synchronous path checks the replayed counts of its own frame
+        host = np.zeros(n, dtype=np.int16)
+        for _ in range(3):
+            rt580.check(lib.rt_gpu_render(ctypes.byref(rts[0][1]), host.ctypes.data), "render")
+    finally:
+        lib.rt580_set_chunk_log2(26)
+        lib.rt_gpu_set_stream(lib.rt_gpu_own_stream())
+
+
+_CORRUPT_CHILD = r"""
+import ctypes, sys
+sys.path.insert(0, sys.argv[1])
+import helpers
+rt580 = helpers.rt580()
+lib = rt580.load()
+rt = rt580.Raytracer(48, 27, helpers.synthetic_root("cornell10k"))
+assert rt.LoadSceneJSON("cornell10k.json") == 0
+rt.set_depth(2)
+rt.set_ao(8, True)
+codes = [rt.Render("") for _ in range(4)]
+print("CODES", codes, lib.rt_gpu_last_error().decode() if isinstance(lib.rt_gpu_last_error(), bytes) else lib.rt_gpu_last_error())
+"""
+
+
+def test_replay_count_mismatch_fails_the_frame(tmp_path):
+    """Diagnostic build, RT580_REPLAY_CORRUPT=1: every replayed count's device
+    check fails. The second identical Render replays the trace counts (the
+    first verified them) and must fail with the schedule error instead of
+    returning a frame; the schedules are dropped, so the third records again
+    (succeeds) and the fourth replays both phases (fails)."""
+    import os
+    import subprocess
+    import sys
+    diag = os.path.join(helpers.REPO, "580-raytracer_amd", "lib580rt_diag.so")
+    if not os.path.exists(diag):
+        pytest.skip("diagnostic build absent (make diag)")
+    env = dict(os.environ, RT580_LIB=diag, RT580_REPLAY_CORRUPT="1")
+    script = tmp_path / "child.py"
+    script.write_text(_CORRUPT_CHILD)
+    r = subprocess.run([sys.executable, str(script), os.path.dirname(os.path.abspath(__file__))], env=env,
+                       capture_output=True, text=True, timeout=240)
+    line = [l for l in r.stdout.splitlines() if l.startswith("CODES")]
+    assert line, r.stdout + r.stderr
+    assert line[0].startswith("CODES [0, 1, 0, 1]"), line[0]
+    assert "replayed count schedule" in line[0], line[0]
