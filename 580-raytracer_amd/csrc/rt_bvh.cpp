@@ -314,7 +314,9 @@ bool build_bvh(const rt_prim* prims, int n, BvhBuild& out) {
             S = std::max(S, max_abs3(p.p0) + std::sqrt(std::max(p.d, 0.0f)));
         }
     }
-    if (out.n_tri == 0 || !(S > 0.0f) || !std::isfinite(S)) return false;
+    // S <= 2^90: the quantized nodes' scales (<= 2^98 for any extent below 2S) times
+    // the slab reciprocals (<= 2^20) stay finite (node4_slab)
+    if (out.n_tri == 0 || !(S > 0.0f) || !(S <= 0x1p90f)) return false;
     out.scale = S;
     Builder B;
     B.prims = prims;
@@ -462,7 +464,7 @@ static Bvh4QNode quantize4(const Bvh4Node& nd) {
         if (!any) o = top = 0.0f;
         int e;
         (void)std::frexp(((double)top - (double)o) / 255.0, &e);  // 2^e >= extent / 255
-        e = std::max(e, -126);                                   // a normal scale
+        e = std::max(e, -100);  // scale >= 2^-100: scale / c stays a normal, exact product (node4_slab)
         for (;; e++) {
             const float scale = std::ldexp(1.0f, e);
             bool fit = true;

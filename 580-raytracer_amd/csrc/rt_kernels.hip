@@ -58,6 +58,7 @@ __device__ __forceinline__ uint32_t mersenne31_mul(uint32_t a, uint32_t b) {
 }
 
 __constant__ uint32_t c_minstd_j1[512];    // 16807^(2s+1) mod m: state offset of sample s's first draw
+__constant__ uint32_t c_xcd_order = 1u;    // xcd_block on (RT580_XCD_ORDER, A/B only; set at rt_gpu_init)
 
 
 // generate_canonical<float,24> (libstdc++ random.tcc:3348-3378) for one draw.
@@ -1194,6 +1195,18 @@ ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
     ao_body<V>(S, F, W, b, e);
 }
 
+// XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, workgroup dispatch: b and b + 8 share an XCD and its
+// 4 MiB L2), so consecutive blocks of work land on 8 different L2s. With
+// xcd_block the grid's G / 8 workgroups of one XCD take G / 8 consecutive
+// blocks per grid-stride round instead: an XCD's resident workgroups then
+// trace rays of a narrow band of neighbouring AO calls and share the BVH
+// nodes and leaf triangles they read. Speed only: a permutation of [0, G).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
+    if (!c_xcd_order || (G & 7u)) return b;
+    return (b & 7u) * (G >> 3) + (b >> 3);
+}
+
 // Split AO pass (default for BVH scenes): ao_near_kernel_w<.., V | 16384>
 // writes each item's ray (W.ao_rays), this kernel runs the near any-hit query
 // over the 4-wide tree with nothing else live, then ao_finish. Rays
@@ -1216,7 +1229,7 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     __shared__ uint32_t s_order[SN];
     __shared__ uint32_t s_bin[SORT > 0 ? NB + 1 : 1];
     const uint64_t span = SORT > 0 ? (uint64_t)SN : (uint64_t)TB;
-    for (uint64_t blk = (uint64_t)blockIdx.x * span; blk < n; blk += (uint64_t)gridDim.x * span)
+    for (uint64_t blk = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * span; blk < n; blk += (uint64_t)gridDim.x * span)
     for (int round = 0; round < (SORT > 0 ? SORT : 1); round++) {
         uint64_t i = blk + threadIdx.x;
         if (SORT > 0) {
@@ -1621,7 +1634,7 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
     const BvhView& V = S.bv;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t nwork = W.far_seg_n[1];
-    for (uint32_t w = blockIdx.x * (TB / 64) + wave; w < nwork; w += gridDim.x * (TB / 64)) {
+    for (uint32_t w = xcd_block(blockIdx.x, gridDim.x) * (TB / 64) + wave; w < nwork; w += gridDim.x * (TB / 64)) {
         // the work item: sorted rays [r0, r1) of one segment and its cell's candidate list
         const uint4 wd = W.far_work[w];
         const uint32_t r0 = __builtin_amdgcn_readfirstlane(wd.x), r1 = __builtin_amdgcn_readfirstlane(wd.y);
@@ -1958,13 +1971,88 @@ __global__ void __launch_bounds__(TB) far_brute_merge_kernel(DevScene S, DevWork
     }
 }
 
+// Brute any-hit scans of far-origin rays (AO samples, shadow rays), split like
+// far_brute_split_kernel: wave w scans slice w / nb of the shuffled records for
+// ray w % nb (slice-major, so the first slices of every ray run first). One
+// wave per ray left the pass as long as its slowest ray's full serial scan (a
+// ray no record accepts reads all of them: ~0.4 ms per launch at 100k
+// triangles, whatever the queue length -- a per-frame floor). A wave skips its
+// slice once another slice of its ray has found an acceptor (done[r], polled
+// at the start and every 8 steps); the first slice to find one claims the ray
+// (atomicOr on done[r]), so the AO call's occlusion count is raised once per
+// ray as in far_scan_kernel. The boolean does not depend on which record
+// accepted. AO rays test their call's hint record first (any slice).
+__global__ void __launch_bounds__(TB) far_brute_any_split_kernel(DevScene S, DevWork W, uint32_t first, uint32_t nb,
+                                                                 uint32_t splits, uint32_t* done, uint8_t* flag) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t total = (uint64_t)nb * splits;
+    const int n = S.n_prims;
+    for (uint64_t w = (uint64_t)blockIdx.x * (TB / 64) + (threadIdx.x >> 6); w < total;
+         w += (uint64_t)gridDim.x * (TB / 64)) {
+        const uint32_t r = (uint32_t)(w % nb), sl = (uint32_t)(w / nb);
+        if (__hip_atomic_load(done + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) continue;
+        const uint32_t q = W.far_vals_alt[first + r];
+        const float4 a = W.far_rays[2 * (size_t)q], b = W.far_rays[2 * (size_t)q + 1];
+        const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+        const uint32_t tag = __float_as_uint(a.w);
+        const float tmax = b.w;
+        uint32_t* hintp = (!flag && W.call_hint) ? W.call_hint + tag : nullptr;
+        int found_k = -1;
+        if (hintp && sl == 0) {
+            const uint32_t hk = __builtin_amdgcn_readfirstlane(*hintp);
+            if (hk < (uint32_t)n && lane == 0 && prim_hit_within(S.scan_prims[hk], o, d, tmax)) found_k = (int)hk;
+        }
+        const int k0 = (int)((uint64_t)n * sl / splits), k1 = (int)((uint64_t)n * (sl + 1) / splits);
+        uint64_t fm = __ballot(found_k >= 0);
+        for (int kb = k0, step = 0; !fm && kb < k1; kb += 64, step++) {
+            if ((step & 7) == 7 &&
+                __builtin_amdgcn_readfirstlane(__hip_atomic_load(done + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+                break;
+            const int k = kb + lane;
+            if (k < k1 && prim_hit_within(S.scan_prims[k], o, d, tmax)) found_k = k;
+            fm = __ballot(found_k >= 0);
+        }
+        if (fm && lane == __ffsll((unsigned long long)fm) - 1) {
+            if (atomicOr(done + r, 1u) == 0u) {
+                any_hit_out(W, flag, tag);
+                if (hintp) *hintp = (uint32_t)found_k;
+            }
+        }
+    }
+}
+
+// RT580_BRUTE_SPLIT bits: 1 = the closest-hit brute scans split across waves
+// (far_brute_split_kernel), 2 = the any-hit ones (far_brute_any_split_kernel).
 static int brute_split() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_BRUTE_SPLIT");
-        v = e ? atoi(e) : 1;
+        v = e ? atoi(e) : 3;
     }
     return v;
+}
+
+static int grid_for(uint64_t items, int cap);
+
+// The brute any-hit scan of the far-origin rays [first, first + nb) of the
+// sorted queue (flag: shadow flags, or null: AO occlusion counts).
+static hipError_t launch_brute_any(const DevScene& S, const DevWork& W, uint32_t first, uint32_t nb, uint8_t* flag,
+                                   hipStream_t s) {
+    if (nb == 0) return hipSuccess;
+    if (brute_split() & 2) {
+        // the sort's input keys are free now: one claim word per ray
+        uint32_t* done = W.far_keys;
+        hipError_t e = hipMemsetAsync(done, 0, (size_t)nb * 4, s);
+        if (e != hipSuccess) return e;
+        uint32_t splits = 32768u / nb;
+        splits = splits < 1u ? 1u : (splits > 256u ? 256u : splits);
+        hipLaunchKernelGGL(far_brute_any_split_kernel, dim3(grid_for((uint64_t)nb * splits * 64, 16384)), dim3(TB), 0,
+                           s, S, W, first, nb, splits, done, flag);
+    } else {
+        hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W, first,
+                           first + nb, 0, (int)S.bv.n_far, 1, flag);
+    }
+    return hipGetLastError();
 }
 
 // Far-pass flavour for a queue of nq rays: 4 = cell-major segments (any-hit
@@ -2521,7 +2609,11 @@ hipError_t upload_minstd_table(hipStream_t s) {
         x = (x * 16807ull) % 2147483647ull;
         x = (x * 16807ull) % 2147483647ull;
     }
-    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
+    static uint32_t xcd = 1u;  // (the same for every context)
+    if (const char* v = getenv("RT580_XCD_ORDER")) xcd = (uint32_t)atoi(v);
+    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xcd_order), &xcd, 4, 0, hipMemcpyHostToDevice, s);
+    return e;
 }
 
 // ---------------------------------------------------------------- kernel timer
@@ -2649,7 +2741,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
                 if (nb) {
                     RT_STEP("trace brute scan");
-                    if (brute_split() && (uint64_t)nb * 2 <= W.far_cap) {
+                    if ((brute_split() & 1) && (uint64_t)nb * 2 <= W.far_cap) {
                         // the sort's input keys are free now: 64-bit minima per brute ray
                         unsigned long long* best = reinterpret_cast<unsigned long long*>(W.far_keys);
                         if ((e = hipMemsetAsync(best, 0xff, (size_t)nb * 8, s)) != hipSuccess) return e;
@@ -2707,9 +2799,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         uint8_t* flags = W.shadow + (size_t)dl * W.far_cap;
                         if (sb) {
                             RT_STEP("trace shadow brute scan");
-                            hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)sb * 64, 16384)), dim3(TB), 0, s,
-                                               S, W, sq - sb, sq, 0, (int)S.bv.n_far, 1, flags);
-                            if ((e = hipGetLastError()) != hipSuccess) return e;
+                            if ((e = launch_brute_any(S, W, sq - sb, sb, flags, s)) != hipSuccess) return e;
                             sq -= sb;
                         }
                         if (sq) {
@@ -2894,9 +2984,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             uint32_t nq = 0, nb = 0;
             if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
             if (nb) {
-                hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W,
-                                   nq - nb, nq, 0, (int)S.bv.n_far, 1, (uint8_t*)nullptr);
-                if ((e = hipGetLastError()) != hipSuccess) return e;
+                if ((e = launch_brute_any(S, W, nq - nb, nb, (uint8_t*)nullptr, s)) != hipSuccess) return e;
                 nq -= nb;
             }
             progress("AO items [%llu, %llu) of %llu: far queue %u (brute %u)", (unsigned long long)b,

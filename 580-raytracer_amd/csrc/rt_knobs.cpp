@@ -35,6 +35,7 @@ const long kTraceWpe[] = {4, 6, 8, -1};
 const long kNearWpe[] = {0, 5, 6, 8, -1};
 const long kFarMode[] = {0, 1, 2, 3, 4, -1};
 const long kFarU[] = {1, 2, 4, -1};
+const long k0123[] = {0, 1, 2, 3, -1};
 // the AO kernel flavours launch_ao_small instantiates (rt_kernels.hip)
 const long kAoVariant[] = {
     0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,                            // ao_kernel<v>
@@ -70,7 +71,7 @@ const Knob kKnobs[] = {
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
     {"RT580_NEAR_WPE", INT_SET, 0, 0, kNearWpe, nullptr},
-    {"RT580_BRUTE_SPLIT", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_BRUTE_SPLIT", INT_SET, 0, 0, k0123, nullptr},
     {"RT580_FAR_MODE", INT_SET, 0, 0, kFarMode, nullptr},
     {"RT580_FAR_U", INT_SET, 0, 0, kFarU, nullptr},
     {"RT580_DEEP_GRID", INT_RANGE, 64, 65536, nullptr, nullptr},
@@ -78,6 +79,7 @@ const Knob kKnobs[] = {
     {"RT580_AO_VARIANT", INT_SET, 0, 0, kAoVariant, nullptr},
     {"RT580_TRACE_SCALAR", INT_SET, 0, 0, k01, nullptr},
     {"RT580_RESOLVE", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_XCD_ORDER", INT_SET, 0, 0, k01, nullptr},
     {"RT580_PROGRESS", INT_SET, 0, 0, k01, nullptr},
     // diagnostic builds (make diag) only
     {"RT580_BVH_DIAG", DIAG_ONLY, 0, 0, nullptr, nullptr},
