@@ -58,7 +58,7 @@ __device__ __forceinline__ uint32_t mersenne31_mul(uint32_t a, uint32_t b) {
 }
 
 __constant__ uint32_t c_minstd_j1[512];    // 16807^(2s+1) mod m: state offset of sample s's first draw
-__constant__ uint32_t c_xcd_order = 1u;    // xcd_block on (RT580_XCD_ORDER, A/B only; set at rt_gpu_init)
+__constant__ uint32_t c_xcd_order = 0u;    // xcd_block on (RT580_XCD_ORDER=1, A/B only: measured slower; set at rt_gpu_init)
 
 
 // generate_canonical<float,24> (libstdc++ random.tcc:3348-3378) for one draw.
@@ -1909,38 +1909,67 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
 }
 
 // Brute closest hit of far-origin tree rays, split: wave w scans slice
-// w % splits of the scene for ray w / splits (few rays, each a full scan: one
-// wave per ray left most of the GPU idle and each wave waiting on its loads);
-// the slices' lexicographic (t, primitive) minima meet in best[r] by a 64-bit
-// atomicMin (t > EPSILON > 0: float bits order like the values).
+// w % splits of the scene for the R rays of group w / splits (few rays, each a
+// full scan: one wave per ray left most of the GPU idle and each wave waiting
+// on its loads); the slices' lexicographic (t, primitive) minima meet in
+// best[r] by a 64-bit atomicMin (t > EPSILON > 0: float bits order like the
+// values). A lane loads each record of its stride once and tests it against
+// all R rays of the group (wave-uniform: scalar registers), so the scan reads
+// the scene once per R rays instead of once per ray.
+template <int R>
 __global__ void __launch_bounds__(TB) far_brute_split_kernel(DevScene S, DevWork W, uint32_t first, uint32_t nb,
                                                              uint32_t splits, unsigned long long* best) {
+    // the group's rays and each lane's best (t, primitive) per ray, in LDS (a
+    // register copy per ray would cost the kernel its occupancy)
+    __shared__ float4 sray[TB / 64][R][2];
+    __shared__ float sbt[TB / 64][R][64];
+    __shared__ int sbp[TB / 64][R][64];
     const int lane = threadIdx.x & 63;
-    const uint64_t total = (uint64_t)nb * splits;
-    for (uint64_t w = (uint64_t)blockIdx.x * (TB / 64) + (threadIdx.x >> 6); w < total;
-         w += (uint64_t)gridDim.x * (TB / 64)) {
-        const uint32_t r = (uint32_t)(w / splits), sl = (uint32_t)(w % splits);
-        const uint32_t q = W.far_vals_alt[first + r];
-        const float4 a = W.far_rays[2 * (size_t)q], b = W.far_rays[2 * (size_t)q + 1];
-        const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+    const uint32_t ng = (nb + R - 1) / R;
+    const uint64_t total = (uint64_t)ng * splits;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t w = (uint64_t)blockIdx.x * (TB / 64) + wave; w < total; w += (uint64_t)gridDim.x * (TB / 64)) {
+        const uint32_t gi = (uint32_t)(w / splits), sl = (uint32_t)(w % splits);
+        const uint32_t nr = nb - gi * R < (uint32_t)R ? nb - gi * R : (uint32_t)R;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the previous group's LDS reads are done
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if ((uint32_t)lane < 2 * nr) {
+            const uint32_t q = W.far_vals_alt[first + gi * R + (uint32_t)(lane >> 1)];
+            sray[wave][lane >> 1][lane & 1] = W.far_rays[2 * (size_t)q + (lane & 1)];
+        }
+        for (int j = 0; j < R; j++) sbp[wave][j][lane] = -1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int n = S.n_prims;
         const int k0 = (int)((uint64_t)n * sl / splits), k1 = (int)((uint64_t)n * (sl + 1) / splits);
-        Hit h;
-        h.t = 0; h.prim = -1;
-        bool found = false;
         for (int k = k0 + lane; k < k1; k += 64) {
-            float t, aa, bb, gg;
-            if (prim_test_closest(S.prims[k], o, d, t, aa, bb, gg, found ? h.t : INFINITY) && lex_better(t, k, found, h)) {
-                found = true;
-                h.t = t; h.prim = k;
+            rt_prim P;
+            load_prim(S.prims + k, P);
+#pragma unroll 1
+            for (uint32_t j = 0; j < nr; j++) {
+                const float4 a = sray[wave][j][0], b = sray[wave][j][1];
+                const int bp = sbp[wave][j][lane];
+                const float bt = sbt[wave][j][lane];
+                const bool found = bp >= 0;
+                float t, aa, bb, gg;
+                if (prim_test_closest(P, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), t, aa, bb, gg, found ? bt : INFINITY) &&
+                    (!found || t < bt || (t == bt && k < bp))) {
+                    sbt[wave][j][lane] = t;
+                    sbp[wave][j][lane] = k;
+                }
             }
         }
-        uint64_t key = found ? (((uint64_t)__float_as_uint(h.t) << 32) | (uint32_t)h.prim) : ~0ull;
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint64_t other = __shfl_xor(key, off);
-            key = other < key ? other : key;
+        for (uint32_t j = 0; j < nr; j++) {
+            const int bp = sbp[wave][j][lane];
+            uint64_t key = bp >= 0 ? (((uint64_t)__float_as_uint(sbt[wave][j][lane]) << 32) | (uint32_t)bp) : ~0ull;
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t other = __shfl_xor(key, off);
+                key = other < key ? other : key;
+            }
+            if (lane == 0 && key != ~0ull) atomicMin(best + gi * R + j, (unsigned long long)key);
         }
-        if (lane == 0 && key != ~0ull) atomicMin(best + r, (unsigned long long)key);
     }
 }
 
@@ -1972,50 +2001,96 @@ __global__ void __launch_bounds__(TB) far_brute_merge_kernel(DevScene S, DevWork
 }
 
 // Brute any-hit scans of far-origin rays (AO samples, shadow rays), split like
-// far_brute_split_kernel: wave w scans slice w / nb of the shuffled records for
-// ray w % nb (slice-major, so the first slices of every ray run first). One
-// wave per ray left the pass as long as its slowest ray's full serial scan (a
-// ray no record accepts reads all of them: ~0.4 ms per launch at 100k
-// triangles, whatever the queue length -- a per-frame floor). A wave skips its
-// slice once another slice of its ray has found an acceptor (done[r], polled
-// at the start and every 8 steps); the first slice to find one claims the ray
+// far_brute_split_kernel: wave w scans slice w / ng of the shuffled records for
+// the R rays of group w % ng (slice-major, so the first slices of every group
+// run first), each record loaded once and tested against the group's rays
+// still undecided. One wave per ray left the pass as long as its slowest ray's
+// full serial scan (a ray no record accepts reads all of them). A wave drops a
+// ray once another slice has found an acceptor for it (done[r], polled at the
+// start and every 8 steps); the first slice to find one claims the ray
 // (atomicOr on done[r]), so the AO call's occlusion count is raised once per
 // ray as in far_scan_kernel. The boolean does not depend on which record
-// accepted. AO rays test their call's hint record first (any slice).
+// accepted. AO rays test their call's hint record first (slice 0).
+template <int R>
 __global__ void __launch_bounds__(TB) far_brute_any_split_kernel(DevScene S, DevWork W, uint32_t first, uint32_t nb,
                                                                  uint32_t splits, uint32_t* done, uint8_t* flag) {
+    __shared__ float4 sray[TB / 64][R][2];  // the group's rays (register copies would cost occupancy)
+    __shared__ int sfk[TB / 64][R];         // an accepting record per ray (the AO call hint)
     const int lane = threadIdx.x & 63;
-    const uint64_t total = (uint64_t)nb * splits;
+    const uint32_t ng = (nb + R - 1) / R;
+    const uint64_t total = (uint64_t)ng * splits;
     const int n = S.n_prims;
-    for (uint64_t w = (uint64_t)blockIdx.x * (TB / 64) + (threadIdx.x >> 6); w < total;
-         w += (uint64_t)gridDim.x * (TB / 64)) {
-        const uint32_t r = (uint32_t)(w % nb), sl = (uint32_t)(w / nb);
-        if (__hip_atomic_load(done + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) continue;
-        const uint32_t q = W.far_vals_alt[first + r];
-        const float4 a = W.far_rays[2 * (size_t)q], b = W.far_rays[2 * (size_t)q + 1];
-        const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
-        const uint32_t tag = __float_as_uint(a.w);
-        const float tmax = b.w;
-        uint32_t* hintp = (!flag && W.call_hint) ? W.call_hint + tag : nullptr;
-        int found_k = -1;
-        if (hintp && sl == 0) {
-            const uint32_t hk = __builtin_amdgcn_readfirstlane(*hintp);
-            if (hk < (uint32_t)n && lane == 0 && prim_hit_within(S.scan_prims[hk], o, d, tmax)) found_k = (int)hk;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t w = (uint64_t)blockIdx.x * (TB / 64) + wave; w < total; w += (uint64_t)gridDim.x * (TB / 64)) {
+        const uint32_t gi = (uint32_t)(w % ng), sl = (uint32_t)(w / ng);
+        const uint32_t nr = nb - gi * R < (uint32_t)R ? nb - gi * R : (uint32_t)R;
+        // the group's rays still undecided (wave-uniform bit mask)
+        bool und = false;
+        if ((uint32_t)lane < nr)
+            und = __hip_atomic_load(done + gi * R + (uint32_t)lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+        uint32_t live = (uint32_t)__ballot(und);
+        if (!live) continue;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the previous group's LDS reads are done
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if ((uint32_t)lane < 2 * nr) {
+            const uint32_t q = W.far_vals_alt[first + gi * R + (uint32_t)(lane >> 1)];
+            sray[wave][lane >> 1][lane & 1] = W.far_rays[2 * (size_t)q + (lane & 1)];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        uint32_t mine = 0;  // this lane's accepted rays
+        if (!flag && W.call_hint && sl == 0 && (uint32_t)lane < nr && ((live >> lane) & 1u)) {
+            const float4 a = sray[wave][lane][0], b = sray[wave][lane][1];
+            const uint32_t hk = W.call_hint[__float_as_uint(a.w)];
+            if (hk < (uint32_t)n && prim_hit_within(S.scan_prims[hk], v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), b.w)) {
+                mine = 1u << lane;
+                sfk[wave][lane] = (int)hk;
+            }
         }
         const int k0 = (int)((uint64_t)n * sl / splits), k1 = (int)((uint64_t)n * (sl + 1) / splits);
-        uint64_t fm = __ballot(found_k >= 0);
-        for (int kb = k0, step = 0; !fm && kb < k1; kb += 64, step++) {
-            if ((step & 7) == 7 &&
-                __builtin_amdgcn_readfirstlane(__hip_atomic_load(done + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-                break;
+        uint32_t decided = 0;
+        for (int kb = k0, step = 0;; kb += 64, step++) {
+            if (__ballot(mine != 0u)) {  // new acceptors: drop their rays from the scan
+                uint32_t m = mine;
+                for (int off = 32; off > 0; off >>= 1) m |= (uint32_t)__shfl_xor((int)m, off);
+                decided = __builtin_amdgcn_readfirstlane(m);
+                live &= ~decided;
+            }
+            if (!live || kb >= k1) break;
+            if ((step & 7) == 7) {
+                bool gone = false;
+                if ((uint32_t)lane < nr && ((live >> lane) & 1u))
+                    gone = __hip_atomic_load(done + gi * R + (uint32_t)lane, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                live &= ~(uint32_t)__ballot(gone);
+                if (!live) break;
+            }
             const int k = kb + lane;
-            if (k < k1 && prim_hit_within(S.scan_prims[k], o, d, tmax)) found_k = k;
-            fm = __ballot(found_k >= 0);
+            if (k < k1) {
+                rt_prim P;
+                load_prim(S.scan_prims + k, P);
+                for (uint32_t lv = live; lv;) {
+                    const int j = __builtin_ctz(lv);
+                    lv &= lv - 1u;
+                    const float4 a = sray[wave][j][0], b = sray[wave][j][1];
+                    if (prim_hit_within(P, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), b.w)) {
+                        mine |= 1u << j;
+                        sfk[wave][j] = k;
+                    }
+                }
+            }
         }
-        if (fm && lane == __ffsll((unsigned long long)fm) - 1) {
-            if (atomicOr(done + r, 1u) == 0u) {
+        // claims: for each decided ray, its first accepting lane
+        for (uint32_t dv = decided; dv;) {
+            const int j = __builtin_ctz(dv);
+            dv &= dv - 1u;
+            const uint64_t fm = __ballot((mine >> j) & 1u);
+            if (lane == __ffsll((unsigned long long)fm) - 1 && atomicOr(done + gi * R + (uint32_t)j, 1u) == 0u) {
+                const uint32_t tag = __float_as_uint(sray[wave][j][0].w);
                 any_hit_out(W, flag, tag);
-                if (hintp) *hintp = (uint32_t)found_k;
+                if (!flag && W.call_hint) W.call_hint[tag] = (uint32_t)sfk[wave][j];
             }
         }
     }
@@ -2032,6 +2107,16 @@ static int brute_split() {
     return v;
 }
 
+// Far-origin rays per wave of the split brute scans (RT580_BRUTE_RAYS 1, 4, 8).
+static int brute_rays() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_BRUTE_RAYS");
+        v = e ? atoi(e) : 8;
+    }
+    return v;
+}
+
 static int grid_for(uint64_t items, int cap);
 
 // The brute any-hit scan of the far-origin rays [first, first + nb) of the
@@ -2044,10 +2129,17 @@ static hipError_t launch_brute_any(const DevScene& S, const DevWork& W, uint32_t
         uint32_t* done = W.far_keys;
         hipError_t e = hipMemsetAsync(done, 0, (size_t)nb * 4, s);
         if (e != hipSuccess) return e;
-        uint32_t splits = 32768u / nb;
+        const int R = brute_rays();
+        const uint32_t ng = (nb + (uint32_t)R - 1) / (uint32_t)R;
+        uint32_t splits = 32768u / ng;
         splits = splits < 1u ? 1u : (splits > 256u ? 256u : splits);
-        hipLaunchKernelGGL(far_brute_any_split_kernel, dim3(grid_for((uint64_t)nb * splits * 64, 16384)), dim3(TB), 0,
-                           s, S, W, first, nb, splits, done, flag);
+        const dim3 grid(grid_for((uint64_t)ng * splits * 64, 16384));
+        if (R == 8)
+            hipLaunchKernelGGL(far_brute_any_split_kernel<8>, grid, dim3(TB), 0, s, S, W, first, nb, splits, done, flag);
+        else if (R == 4)
+            hipLaunchKernelGGL(far_brute_any_split_kernel<4>, grid, dim3(TB), 0, s, S, W, first, nb, splits, done, flag);
+        else
+            hipLaunchKernelGGL(far_brute_any_split_kernel<1>, grid, dim3(TB), 0, s, S, W, first, nb, splits, done, flag);
     } else {
         hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W, first,
                            first + nb, 0, (int)S.bv.n_far, 1, flag);
@@ -2610,7 +2702,7 @@ hipError_t upload_minstd_table(hipStream_t s) {
         x = (x * 16807ull) % 2147483647ull;
     }
     hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
-    static uint32_t xcd = 1u;  // (the same for every context)
+    static uint32_t xcd = 0u;  // (the same for every context)
     if (const char* v = getenv("RT580_XCD_ORDER")) xcd = (uint32_t)atoi(v);
     if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xcd_order), &xcd, 4, 0, hipMemcpyHostToDevice, s);
     return e;
@@ -2676,7 +2768,22 @@ void kernel_timer_release() {
 
 
 // Sort the far queue (W.far_count entries) by direction key; returns its length.
-static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
+// Radix-sorted key bits: grid keys are cell << (24 - 2 L), so their low
+// 24 - 2 L bits are zero and the sort skips them (3 digit passes instead of
+// 4 at L = 10, 11); plane-tree keys then group by their top direction bits
+// only -- grouping, never a result (RT580_SORT_BITS=0: every bit, A/B).
+static int sort_begin_bit(const DevScene& S) {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_SORT_BITS");
+        v = e ? atoi(e) : 1;
+    }
+    if (!v || S.bv.grid_log2 <= 0) return 0;
+    const int b = 24 - 2 * S.bv.grid_log2;
+    return b > 0 ? b : 0;
+}
+
+static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
     RT_STEP("far queue count D2H");
     hipError_t e = read_counts(W.far_count, 2, W.far_count_host, s);
     if (e != hipSuccess) return e;
@@ -2686,7 +2793,7 @@ static hipError_t sort_far_queue(const DevWork& W, hipStream_t s, uint32_t& nq, 
     size_t tmp = W.sort_tmp_bytes;
     RT_STEP("far queue radix sort");
     return hipcub::DeviceRadixSort::SortPairs(W.sort_tmp, tmp, W.far_keys, W.far_keys_alt, W.far_vals,
-                                              W.far_vals_alt, (int)nq, 0, RT_DIR_KEY_BITS, s);
+                                              W.far_vals_alt, (int)nq, sort_begin_bit(S), RT_DIR_KEY_BITS, s);
 }
 
 // Per-frame counters, one launch: level counts/bases, the node-capacity probe,
@@ -2738,17 +2845,24 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 uint32_t nq = 0, nb = 0;
-                if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
+                if ((e = sort_far_queue(S, W, s, nq, nb)) != hipSuccess) return e;
                 if (nb) {
                     RT_STEP("trace brute scan");
                     if ((brute_split() & 1) && (uint64_t)nb * 2 <= W.far_cap) {
                         // the sort's input keys are free now: 64-bit minima per brute ray
                         unsigned long long* best = reinterpret_cast<unsigned long long*>(W.far_keys);
                         if ((e = hipMemsetAsync(best, 0xff, (size_t)nb * 8, s)) != hipSuccess) return e;
-                        uint32_t splits = 32768u / nb;
+                        const int R = brute_rays();
+                        const uint32_t ng = (nb + (uint32_t)R - 1) / (uint32_t)R;
+                        uint32_t splits = 32768u / ng;
                         splits = splits < 1u ? 1u : (splits > 512u ? 512u : splits);
-                        hipLaunchKernelGGL(far_brute_split_kernel, dim3(grid_for((uint64_t)nb * splits * 64, 16384)),
-                                           dim3(TB), 0, s, S, W, nq - nb, nb, splits, best);
+                        const dim3 grid(grid_for((uint64_t)ng * splits * 64, 16384));
+                        if (R == 8)
+                            hipLaunchKernelGGL(far_brute_split_kernel<8>, grid, dim3(TB), 0, s, S, W, nq - nb, nb, splits, best);
+                        else if (R == 4)
+                            hipLaunchKernelGGL(far_brute_split_kernel<4>, grid, dim3(TB), 0, s, S, W, nq - nb, nb, splits, best);
+                        else
+                            hipLaunchKernelGGL(far_brute_split_kernel<1>, grid, dim3(TB), 0, s, S, W, nq - nb, nb, splits, best);
                         if ((e = hipGetLastError()) != hipSuccess) return e;
                         hipLaunchKernelGGL(far_brute_merge_kernel, dim3(grid_for(nb, 4096)), dim3(TB), 0, s, S, W,
                                            nq - nb, nb, (const unsigned long long*)best);
@@ -2795,7 +2909,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                                            li, dl, near_wave() ? 1 : 0);
                         if ((e = hipGetLastError()) != hipSuccess) return e;
                         uint32_t sq = 0, sb = 0;
-                        if ((e = sort_far_queue(W, s, sq, sb)) != hipSuccess) return e;
+                        if ((e = sort_far_queue(S, W, s, sq, sb)) != hipSuccess) return e;
                         uint8_t* flags = W.shadow + (size_t)dl * W.far_cap;
                         if (sb) {
                             RT_STEP("trace shadow brute scan");
@@ -2982,7 +3096,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if ((e = launch_ao_fix(S, F, W, b, e1, s)) != hipSuccess) return e;
             if (!S.bv.has_far) continue;
             uint32_t nq = 0, nb = 0;
-            if ((e = sort_far_queue(W, s, nq, nb)) != hipSuccess) return e;
+            if ((e = sort_far_queue(S, W, s, nq, nb)) != hipSuccess) return e;
             if (nb) {
                 if ((e = launch_brute_any(S, W, nq - nb, nb, (uint8_t*)nullptr, s)) != hipSuccess) return e;
                 nq -= nb;

@@ -36,6 +36,7 @@ const long kNearWpe[] = {0, 5, 6, 8, -1};
 const long kFarMode[] = {0, 1, 2, 3, 4, -1};
 const long kFarU[] = {1, 2, 4, -1};
 const long k0123[] = {0, 1, 2, 3, -1};
+const long k148[] = {1, 4, 8, -1};
 // the AO kernel flavours launch_ao_small instantiates (rt_kernels.hip)
 const long kAoVariant[] = {
     0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,                            // ao_kernel<v>
@@ -72,8 +73,10 @@ const Knob kKnobs[] = {
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
     {"RT580_NEAR_WPE", INT_SET, 0, 0, kNearWpe, nullptr},
     {"RT580_BRUTE_SPLIT", INT_SET, 0, 0, k0123, nullptr},
+    {"RT580_BRUTE_RAYS", INT_SET, 0, 0, k148, nullptr},
     {"RT580_FAR_MODE", INT_SET, 0, 0, kFarMode, nullptr},
     {"RT580_FAR_U", INT_SET, 0, 0, kFarU, nullptr},
+    {"RT580_SORT_BITS", INT_SET, 0, 0, k01, nullptr},
     {"RT580_DEEP_GRID", INT_RANGE, 64, 65536, nullptr, nullptr},
     {"RT580_AO_GRID", INT_RANGE, 256, 1 << 20, nullptr, nullptr},
     {"RT580_AO_VARIANT", INT_SET, 0, 0, kAoVariant, nullptr},

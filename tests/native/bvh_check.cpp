@@ -8,6 +8,7 @@
 // and the same any-hit boolean.
 //
 // usage: bvh_check <assets root> <scene.json> <rays> [seed]
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -101,6 +102,14 @@ int main(int argc, char** argv) {
     V.grid_start = B.grid_start.empty() ? nullptr : B.grid_start.data();
     V.grid_items = B.grid_items.data();
     V.grid_always = B.grid_always.data();
+    if (!B.grid_start.empty()) {  // cell-list lengths (the far passes' per-ray candidate counts)
+        std::vector<uint32_t> len(B.grid_start.size() - 1);
+        for (size_t c = 0; c + 1 < B.grid_start.size(); c++) len[c] = B.grid_start[c + 1] - B.grid_start[c];
+        std::sort(len.begin(), len.end());
+        const size_t m = len.size();
+        std::printf("grid lists: cells=%zu median=%u p99=%u p99.99=%u max=%u\n", m, len[m / 2], len[m * 99 / 100],
+                    len[std::min(m - 1, m * 9999 / 10000)], len[m - 1]);
+    }
     V.n_always = (int)B.grid_always.size();
     V.grid_log2 = B.grid_start.empty() ? 0 : B.grid_log2;
     V.grid_r = B.grid_r;

@@ -48,3 +48,14 @@ def test_valid_switches_pass_validation():
     st, msg = _init_with({"RT580_AO_VARIANT": str(16 | 7180), "RT580_CHUNK_LOG2": "10", "RT580_EXHAUSTIVE": "1",
                           "RT580_FAR_MODE": "4", "RT580_GRID_R": "2.5"})
     assert st == 1 and "no HIP device" in msg, msg
+
+
+def test_every_switch_is_documented():
+    """INTEGRATION.md's switch table lists every RT580_* name the library
+    validates (csrc/rt_knobs.cpp), so no accepted switch is undocumented."""
+    import re
+    src = open(os.path.join(helpers.PKG, "csrc", "rt_knobs.cpp")).read()
+    names = set(re.findall(r'\{"(RT580_[A-Z0-9_]+)"', src))
+    doc = open(os.path.join(helpers.REPO, "INTEGRATION.md")).read()
+    missing = sorted(n for n in names if "`%s`" % n not in doc)
+    assert len(names) > 20 and not missing, missing

@@ -17,6 +17,12 @@ Per kernel (template instantiations kept apart):
 Peaks (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs, one wave64 VALU instruction
 per SIMD every 2 cycles at 2.4 GHz = 1.2288e12 wave-instructions/s; HBM 8 TB/s.
 
+With RT580_PROFILE_AFTER=<kernel> (e.g. row_scan_kernel): only the dispatches
+after the first dispatch of that kernel -- bench.py --row-sample's untimed
+full-frame count pass comes first, so the summary is the timed frames'. The
+kernel statistics then come from the per-dispatch trace (trace_kernel_trace.csv)
+and the counters from the PMC rows past the marker in each pass.
+
 usage: summarize_profile.py <prof_dir> <out.json>"""
 import collections
 import csv
@@ -51,18 +57,42 @@ def short(name):
     return n
 
 
+def after_marker(rows, name_key, order_key, marker):
+    """rows past the first row whose kernel name contains marker (by order_key)"""
+    rows = sorted(rows, key=lambda r: int(r[order_key]))
+    for i, r in enumerate(rows):
+        if marker in r[name_key]:
+            return rows[i + 1:]
+    return rows
+
+
 def summarize(d):
+    marker = os.environ.get("RT580_PROFILE_AFTER", "")
     stats = collections.defaultdict(lambda: {"calls": 0, "total_ns": 0.0, "pct": 0.0})
-    for r in csv.DictReader(open(os.path.join(d, "trace_kernel_stats.csv"))):
-        s = stats[short(r["Name"])]
-        s["calls"] += int(r["Calls"])
-        s["total_ns"] += float(r["TotalDurationNs"])
-        s["pct"] += float(r["Percentage"])
+    if marker:
+        tr = after_marker(list(csv.DictReader(open(os.path.join(d, "trace_kernel_trace.csv")))), "Kernel_Name",
+                          "Start_Timestamp", marker)
+        tot = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr) or 1
+        for r in tr:
+            s = stats[short(r["Kernel_Name"])]
+            dt = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            s["calls"] += 1
+            s["total_ns"] += dt
+            s["pct"] += 100.0 * dt / tot
+    else:
+        for r in csv.DictReader(open(os.path.join(d, "trace_kernel_stats.csv"))):
+            s = stats[short(r["Name"])]
+            s["calls"] += int(r["Calls"])
+            s["total_ns"] += float(r["TotalDurationNs"])
+            s["pct"] += float(r["Percentage"])
     for s in stats.values():
         s["avg_ns"] = s["total_ns"] / max(s["calls"], 1)
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "pmc*_counter_collection.csv"))):
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        if marker:
+            rows = after_marker(rows, "Kernel_Name", "Dispatch_Id", marker)
+        for r in rows:
             pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     kernels = {}
     for k, s in stats.items():
