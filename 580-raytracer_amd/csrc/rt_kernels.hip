@@ -2107,6 +2107,19 @@ static int brute_split() {
     return v;
 }
 
+// List entries in flight per lane in far_closest_kernel (RT580_FAR_CLOSEST_U 1, 2, 4).
+static int far_closest_u() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_FAR_CLOSEST_U");
+        v = e ? atoi(e) : 4;
+    }
+    return v;
+}
+
+// Largest slice of the scene one wave scans in the split any-hit brute scan.
+constexpr uint32_t kBruteSlice = 4096;
+
 // Far-origin rays per wave of the split brute scans (RT580_BRUTE_RAYS 1, 4, 8).
 static int brute_rays() {
     static int v = -1;
@@ -2133,6 +2146,11 @@ static hipError_t launch_brute_any(const DevScene& S, const DevWork& W, uint32_t
         const uint32_t ng = (nb + (uint32_t)R - 1) / (uint32_t)R;
         uint32_t splits = 32768u / ng;
         splits = splits < 1u ? 1u : (splits > 256u ? 256u : splits);
+        // slices of at most kBruteSlice records: a ray no record accepts is
+        // scanned in parallel slices even when the queue is long (the AO chunks
+        // queue ~10^5 far-origin samples; their groups decided by the call hint
+        // skip their later slices through done[])
+        splits = std::max(splits, ((uint32_t)S.n_prims + kBruteSlice - 1) / kBruteSlice);
         const dim3 grid(grid_for((uint64_t)ng * splits * 64, 16384));
         if (R == 8)
             hipLaunchKernelGGL(far_brute_any_split_kernel<8>, grid, dim3(TB), 0, s, S, W, first, nb, splits, done, flag);
@@ -2163,6 +2181,11 @@ static int far_mode(uint32_t nq) {
 // Queued tree rays of a BVH trace level (sorted by direction key): the far part
 // of bvh_closest, merged into the provisional hit with the same lexicographic
 // rule; wave-cooperative like far_any_kernel.
+// U: list entries in flight per lane in the per-lane walk of a non-uniform
+// wave (far_grid_lane): the kernel's time is its slowest lane's walk of its
+// cell's list (up to ~320 entries at 100k triangles), one dependent chain of
+// entry -> plane -> record per step.
+template <int U>
 __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, uint32_t n) {
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
     __shared__ FarTri ftile[TB / 64][64];
@@ -2190,7 +2213,7 @@ __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, 
         const FarRay fr = far_ray(S.bv, o);
         bool changed = false;
         const bool gl = live && grid_origin(S.bv, o);
-        if (far_grid_lane<true>(S, gl, o, d, fr, h, found, ftile[wave])) changed = true;
+        if (far_grid_lane<true, U>(S, gl, o, d, fr, h, found, ftile[wave])) changed = true;
         const bool walk = live && !gl;
         int sp = 0;
         stk[wave][sp++] = 0;
@@ -2889,8 +2912,15 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 if (nq) {
                     RT_STEP("trace far pass");
                     const int fm = far_mode(nq);
-                    if (fm == 1 || fm == 4)
-                        hipLaunchKernelGGL(far_closest_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                    if (fm == 1 || fm == 4) {
+                        const int u = far_closest_u();
+                        if (u == 4)
+                            hipLaunchKernelGGL(far_closest_kernel<4>, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                        else if (u == 2)
+                            hipLaunchKernelGGL(far_closest_kernel<2>, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                        else
+                            hipLaunchKernelGGL(far_closest_kernel<1>, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
+                    }
                     else if (fm == 2)
                         hipLaunchKernelGGL(far_closest_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
                     else

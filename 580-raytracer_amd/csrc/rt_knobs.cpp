@@ -30,6 +30,7 @@ struct Knob {
 };
 
 const long k01[] = {0, 1, -1};
+const long k23[] = {2, 3, -1};
 const long kSort[] = {0, 1, 2, 3, -1};
 const long kTraceWpe[] = {4, 6, 8, -1};
 const long kNearWpe[] = {0, 5, 6, 8, -1};
@@ -52,6 +53,7 @@ const char* const kTransport[] = {"rccl", "local", nullptr};
 const Knob kKnobs[] = {
     // rt_shim.cpp / raytracer.cpp
     {"RT580_PIPELINE", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_SLOTS", INT_SET, 0, 0, k23, nullptr},
     {"RT580_CHUNK_LOG2", INT_RANGE, 6, 26, nullptr, nullptr},
     {"RT580_GRID_LOG2", INT_RANGE, 0, 12, nullptr, nullptr},
     {"RT580_BVH4", INT_SET, 0, 0, k01, nullptr},
@@ -76,6 +78,7 @@ const Knob kKnobs[] = {
     {"RT580_BRUTE_RAYS", INT_SET, 0, 0, k148, nullptr},
     {"RT580_FAR_MODE", INT_SET, 0, 0, kFarMode, nullptr},
     {"RT580_FAR_U", INT_SET, 0, 0, kFarU, nullptr},
+    {"RT580_FAR_CLOSEST_U", INT_SET, 0, 0, kFarU, nullptr},
     {"RT580_SORT_BITS", INT_SET, 0, 0, k01, nullptr},
     {"RT580_DEEP_GRID", INT_RANGE, 64, 65536, nullptr, nullptr},
     {"RT580_AO_GRID", INT_RANGE, 256, 1 << 20, nullptr, nullptr},

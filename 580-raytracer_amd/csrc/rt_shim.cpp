@@ -88,11 +88,14 @@ struct State {
     uint64_t scene_gen = 0;
     // per-frame workspace: two slots, so that consecutive frames overlap on
     // two streams (frame pipelining, see begin_slot)
-    Slot slot[2];
+    static constexpr int kSlots = 3;
+    Slot slot[kSlots];
+    int nslots = 3;            // slots in use (RT580_SLOTS): frames in flight
     int cur = 0;               // slot of the frame being enqueued
     int last_slot = -1;        // slot of the previous frame call
     uint64_t frames = 0;       // frames begun
-    hipEvent_t user_mark[2] = {nullptr, nullptr};  // the caller's stream at the start of a frame call
+    int64_t slot_last[kSlots] = {-1, -1, -1};  // the frame call that last used each slot
+    hipEvent_t user_mark[kSlots] = {};  // the caller's stream at the start of the last frame calls (ring)
     // rt_gpu_render's host copy: pinned staging, filled in chunks (one event each)
     int16_t* stage = nullptr;
     size_t stage_bytes = 0;
@@ -161,9 +164,10 @@ int fail(const char* fmt, ...) {
         if (e_ != hipSuccess) return fail("%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
-// Frame pipelining. Consecutive frame calls alternate between two slots (own
-// stream and workspace), so frame k+1's latency-bound trace overlaps frame k's
-// AO kernels. BVH frames too: their host reads (trace-level counts, the AO-call
+// Frame pipelining. Consecutive frame calls rotate over three slots (own
+// stream and workspace; RT580_SLOTS=2: two), so frame k+1's latency-bound
+// trace overlaps frame k's AO kernels, and with three slots two frames' traces
+// overlap each other as well. BVH frames too: their host reads (trace-level counts, the AO-call
 // total) synchronize their own slot's stream only, and their AO chunks enqueue
 // without one (binned far queue), so the host returns while frame k's AO runs
 // and frame k+1's trace levels run beside it. Ordering:
@@ -184,10 +188,21 @@ int begin_slot(bool serialize) {
         g.cur = 0;
         return check_replay(SL);
     }
-    const int k = (int)(g.frames & 1);
+    const int ns = g.nslots;
+    const uint64_t call = g.frames;
+    const int k = (int)(call % (uint64_t)ns);
     HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));  // this call's start
-    const int slot = serialize ? 0 : (g.last_slot < 0 ? 0 : g.last_slot ^ 1);
-    const hipEvent_t wait = (g.frames == 0 || slot == g.last_slot) ? g.user_mark[k] : g.user_mark[k ^ 1];
+    const int slot = serialize ? 0 : (g.last_slot < 0 ? 0 : (g.last_slot + 1) % ns);
+    // the caller's stream at the start of the call after this slot's last one
+    // (it holds the wait for that frame and the caller's work on its
+    // framebuffer queued before that call), or now when that is this call or
+    // its mark has left the ring
+    hipEvent_t wait = g.user_mark[k];
+    if (g.slot_last[slot] >= 0) {
+        const uint64_t wc = (uint64_t)g.slot_last[slot] + 1;
+        if (wc < call && call - wc < (uint64_t)ns) wait = g.user_mark[wc % (uint64_t)ns];
+    }
+    g.slot_last[slot] = (int64_t)call;
     g.cur = slot;
     g.last_slot = slot;
     if (check_replay(SL)) return RT_FAILURE;
@@ -209,7 +224,7 @@ int end_slot() {
 // caller produced there, e.g. the all-gathered row bases of rt_gpu_shade_rows).
 int slot_wait_user() {
     if (!g.pipeline) return RT_SUCCESS;
-    const int k = (int)(g.frames & 1);  // the mark the next begin_slot overwrites, unused until then
+    const int k = (int)(g.frames % (uint64_t)g.nslots);  // the mark the next begin_slot overwrites, unused until then
     HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));
     HIP_TRY(hipStreamWaitEvent(SL.stream, g.user_mark[k], 0));
     return RT_SUCCESS;
@@ -219,7 +234,7 @@ bool frame_uses_bvh(const rt_render_params* p) {
     return g.accel == RT_ACCEL_AUTO && g.bvh_ok && bvh_usable(g.bvh, p->cam_from);
 }
 
-// Wait for every enqueued frame (both slots) and the caller's stream.
+// Wait for every enqueued frame (every slot) and the caller's stream.
 int sync_all() {
     HIP_TRY(hipStreamSynchronize(g.stream));
     if (g.pipeline)
@@ -767,6 +782,8 @@ int rt_gpu_init(int device) {
     {
         const char* e = std::getenv("RT580_PIPELINE");
         g.pipeline = !(e && std::atoi(e) == 0);
+        const char* ns = std::getenv("RT580_SLOTS");  // frames in flight (2, 3)
+        g.nslots = ns ? std::atoi(ns) : 3;
     }
     if (const char* e = std::getenv("RT580_CHUNK_LOG2")) {
         char* end = nullptr;

@@ -15,7 +15,7 @@ The scene is resident in HBM.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Parallel modes (the row split of SURVEY §8e, byte-identical frames for every N):
-  * N = 1: rt_gpu_render_device, two frames in flight, framebuffer left in HBM
+  * N = 1: rt_gpu_render_device, up to three frames in flight, framebuffer left in HBM
     (device throughput); the blocking Render() latency is reported beside it.
   * --gpus N without a launcher: rt_gpu_render_multi over devices 0..N-1 in this
     process (what the drop-in Render() calls: single-process RCCL, framebuffer
@@ -315,7 +315,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
             "scene_query": "exact BVH + plane tree (rt_bvh.h)" if lib.rt_gpu_accel_active() else
                            "brute force (every primitive per ray, as the reference)",
         },
-        "step": ("one frame; framebuffer left in HBM, two frames in flight (device throughput)" if not
+        "step": ("one frame; framebuffer left in HBM, up to three frames in flight (device throughput)" if not
                  (ctx.dist_on or ctx.multi) else
                  "one frame, whole Render(): framebuffer on device 0's host copy" if ctx.multi else
                  "one frame on every rank; rank 0 holds the gathered u8 frame"),
