@@ -1250,13 +1250,33 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
                     atomicAdd(&s_bin[key[q]], 1u);
                 }
                 __syncthreads();
-                if (threadIdx.x == 0) {
-                    uint32_t acc = 0;
-                    for (int k = 0; k < NB + 1; k++) {
-                        const uint32_t c = s_bin[k];
-                        s_bin[k] = acc;
-                        acc += c;
+                {   // exclusive scan of the NB + 1 bins: runs of PER bins per thread,
+                    // their sums scanned across the wave (shuffles) and the waves (LDS)
+                    constexpr int PER = (NB + 1 + TB - 1) / TB;
+                    __shared__ uint32_t s_wsum[TB / 64];
+                    const int k0 = threadIdx.x * PER;
+                    uint32_t run = 0;
+#pragma unroll
+                    for (int q = 0; q < PER; q++)
+                        if (k0 + q < NB + 1) run += s_bin[k0 + q];
+                    const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+                    uint32_t inc = run;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
+                        if (ln >= o) inc += v;
                     }
+                    if (ln == 63) s_wsum[wv] = inc;
+                    __syncthreads();
+                    uint32_t acc = inc - run;
+                    for (int w2 = 0; w2 < wv; w2++) acc += s_wsum[w2];
+#pragma unroll
+                    for (int q = 0; q < PER; q++)
+                        if (k0 + q < NB + 1) {
+                            const uint32_t c = s_bin[k0 + q];
+                            s_bin[k0 + q] = acc;
+                            acc += c;
+                        }
                 }
                 __syncthreads();
 #pragma unroll
@@ -1401,7 +1421,8 @@ static int ao_sort() {
         // 3: blocks of 2048 samples by 16 x 16 direction cells. AO field100k
         // 1080p 53.9 -> 49.3 ms, cornell10k 80.1 -> 77.9 ms (0: unsorted;
         // 1: 1024 / 8 x 8 50.6 / 79.4; 2: 2048 / 8 x 8 49.4; 4096 samples
-        // lose occupancy: 59.1 / 88.4)
+        // lose occupancy: 59.1 / 88.4; round 3, 2048 / 32 x 32 cells: 4
+        // waves/SIMD, north-star frame 41.8 -> 46.6 ms)
         v = e ? atoi(e) : 3;
     }
     return v;
