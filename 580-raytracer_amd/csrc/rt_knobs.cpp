@@ -31,6 +31,7 @@ struct Knob {
 
 const long k01[] = {0, 1, -1};
 const long k23[] = {2, 3, -1};
+const long k234[] = {2, 3, 4, -1};
 const long kSort[] = {0, 1, 2, 3, -1};
 const long kTraceWpe[] = {4, 6, 8, -1};
 const long kNearWpe[] = {0, 5, 6, 8, -1};
@@ -53,7 +54,9 @@ const char* const kTransport[] = {"rccl", "local", nullptr};
 const Knob kKnobs[] = {
     // rt_shim.cpp / raytracer.cpp
     {"RT580_PIPELINE", INT_SET, 0, 0, k01, nullptr},
-    {"RT580_SLOTS", INT_SET, 0, 0, k23, nullptr},
+    {"RT580_SLOTS", INT_SET, 0, 0, k234, nullptr},
+    {"RT580_AO_ORDER", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_SMALL_SLOTS", INT_SET, 0, 0, k234, nullptr},
     {"RT580_CHUNK_LOG2", INT_RANGE, 6, 26, nullptr, nullptr},
     {"RT580_GRID_LOG2", INT_RANGE, 0, 12, nullptr, nullptr},
     {"RT580_BVH4", INT_SET, 0, 0, k01, nullptr},

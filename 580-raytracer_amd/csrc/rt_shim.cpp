@@ -38,6 +38,7 @@ enum { EV_START, EV_TRACE, EV_RANK, EV_AO, EV_RESOLVE, EV_N };
 struct Slot {
     hipStream_t stream = nullptr;  // frame stream (non-blocking)
     hipEvent_t done = nullptr;     // end of the slot's last enqueued phase
+    hipEvent_t ao_done = nullptr;  // end of the AO kernels of the slot's last frame
     DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
         row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream, aofix_items, aofix_count,
         call_hint;
@@ -88,13 +89,15 @@ struct State {
     uint64_t scene_gen = 0;
     // per-frame workspace: two slots, so that consecutive frames overlap on
     // two streams (frame pipelining, see begin_slot)
-    static constexpr int kSlots = 3;
+    static constexpr int kSlots = 4;
     Slot slot[kSlots];
     int nslots = 3;            // slots in use (RT580_SLOTS): frames in flight
+    int small_slots = 3;       // the same for whole small-scene frames (RT580_SMALL_SLOTS)
     int cur = 0;               // slot of the frame being enqueued
     int last_slot = -1;        // slot of the previous frame call
     uint64_t frames = 0;       // frames begun
-    int64_t slot_last[kSlots] = {-1, -1, -1};  // the frame call that last used each slot
+    int last_ao_slot = -1;     // slot of the last frame whose AO phase was enqueued (ao_order)
+    int64_t slot_last[kSlots] = {-1, -1, -1, -1};  // the frame call that last used each slot
     hipEvent_t user_mark[kSlots] = {};  // the caller's stream at the start of the last frame calls (ring)
     // rt_gpu_render's host copy: pinned staging, filled in chunks (one event each)
     int16_t* stage = nullptr;
@@ -183,14 +186,14 @@ int fail(const char* fmt, ...) {
 int check_replay(Slot& sl);
 int post_replay_check();
 
-int begin_slot(bool serialize) {
+// ns: slots this frame rotates over (whole small-scene frames: 2, see below).
+int begin_slot(bool serialize, int ns) {
     if (!g.pipeline) {
         g.cur = 0;
         return check_replay(SL);
     }
-    const int ns = g.nslots;
     const uint64_t call = g.frames;
-    const int k = (int)(call % (uint64_t)ns);
+    const int k = (int)(call % (uint64_t)State::kSlots);
     HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));  // this call's start
     const int slot = serialize ? 0 : (g.last_slot < 0 ? 0 : (g.last_slot + 1) % ns);
     // the caller's stream at the start of the call after this slot's last one
@@ -200,7 +203,7 @@ int begin_slot(bool serialize) {
     hipEvent_t wait = g.user_mark[k];
     if (g.slot_last[slot] >= 0) {
         const uint64_t wc = (uint64_t)g.slot_last[slot] + 1;
-        if (wc < call && call - wc < (uint64_t)ns) wait = g.user_mark[wc % (uint64_t)ns];
+        if (wc < call && call - wc < (uint64_t)State::kSlots) wait = g.user_mark[wc % (uint64_t)State::kSlots];
     }
     g.slot_last[slot] = (int64_t)call;
     g.cur = slot;
@@ -224,7 +227,7 @@ int end_slot() {
 // caller produced there, e.g. the all-gathered row bases of rt_gpu_shade_rows).
 int slot_wait_user() {
     if (!g.pipeline) return RT_SUCCESS;
-    const int k = (int)(g.frames % (uint64_t)g.nslots);  // the mark the next begin_slot overwrites, unused until then
+    const int k = (int)(g.frames % (uint64_t)State::kSlots);  // the mark the next begin_slot overwrites, unused until then
     HIP_TRY(hipEventRecord(g.user_mark[k], g.stream));
     HIP_TRY(hipStreamWaitEvent(SL.stream, g.user_mark[k], 0));
     return RT_SUCCESS;
@@ -657,6 +660,27 @@ int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global
     return RT_SUCCESS;
 }
 
+// AO phases in frame order (RT580_AO_ORDER=1, rt580_set_ao_order): a frame's
+// AO kernels start after the previous frame's, so consecutive frames overlap
+// one frame's trace with the other's AO only. Off by default: AO phases that
+// run together fill each other's tails (north-star frame 44.9 -> 41.8 ms,
+// config 2 1.532 -> 1.497 ms) at the price of longer launches (config 2's AO
+// kernel 1.16 -> 2.08 ms per launch). bench.py times the AO kernel once more
+// in order, untimed, to report its isolated launch beside the live one.
+int g_ao_order = -1;  // process-wide; rt580_set_ao_order overrides
+bool ao_order() {
+    if (g_ao_order < 0) {
+        const char* e = std::getenv("RT580_AO_ORDER");
+        g_ao_order = e ? std::atoi(e) : 0;
+    }
+    return g_ao_order != 0;
+}
+
+hipError_t wait_previous_ao() {
+    if (!g.pipeline || g.last_ao_slot < 0 || g.last_ao_slot == g.cur) return hipSuccess;
+    return hipStreamWaitEvent(fs(), g.slot[g.last_ao_slot].ao_done, 0);
+}
+
 // Phase 2: number AO calls (RNG positions), AO, resolve into fb_out.
 int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_rows, const uint64_t* row_base_global,
                int16_t* fb_out) {
@@ -674,12 +698,17 @@ int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
             g.key_ao = key;
             g.ao_valid = false;
         }
+        if (ao_order()) HIP_TRY(wait_previous_ao());
         const hipError_t e = launch_ao(sc, f, w, fs());
         if (end_schedule(g.sched_ao, "AO", e)) return RT_FAILURE;
         HIP_TRY(e);
         if (!replay && frame_verified(p)) g.ao_valid = true;
     }
     HIP_TRY(hipEventRecord(g.ev[EV_AO], fs()));
+    if (g.pipeline) {
+        HIP_TRY(hipEventRecord(SL.ao_done, fs()));
+        g.last_ao_slot = g.cur;
+    }
     HIP_TRY(launch_resolve(sc, f, w, fb_out, fs()));
     HIP_TRY(hipEventRecord(g.ev[EV_RESOLVE], fs()));
     return RT_SUCCESS;
@@ -782,8 +811,10 @@ int rt_gpu_init(int device) {
     {
         const char* e = std::getenv("RT580_PIPELINE");
         g.pipeline = !(e && std::atoi(e) == 0);
-        const char* ns = std::getenv("RT580_SLOTS");  // frames in flight (2, 3)
+        const char* ns = std::getenv("RT580_SLOTS");  // frames in flight (2-4)
         g.nslots = ns ? std::atoi(ns) : 3;
+        const char* ss = std::getenv("RT580_SMALL_SLOTS");
+        g.small_slots = std::min(ss ? std::atoi(ss) : 3, g.nslots);
     }
     if (const char* e = std::getenv("RT580_CHUNK_LOG2")) {
         char* end = nullptr;
@@ -795,6 +826,7 @@ int rt_gpu_init(int device) {
     for (auto& sl : g.slot) {
         HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&sl.ao_done, hipEventDisableTiming));
     }
     for (auto& ev : g.user_mark) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HIP_TRY(hipStreamCreateWithFlags(&g.aux, hipStreamNonBlocking));
@@ -926,7 +958,9 @@ int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     // The RNG offsets need every row before a selected one: render the prefix
     // [0, row_end) and copy the selected rows out when the selection is sparse.
     const int n_rows = prefix ? n_sel : p->row_end;
-    if (begin_slot(false)) return RT_FAILURE;
+    // (RT580_SMALL_SLOTS: the slots of whole small-scene frames, A/B; config 2
+    // 1.478 ms with two, 1.460 with three)
+    if (begin_slot(false, frame_uses_bvh(p) ? g.nslots : g.small_slots)) return RT_FAILURE;
     for (int attempt = 0; attempt < 4; attempt++) {
         if (begin_frame()) return RT_FAILURE;
         HIP_TRY(hipEventRecord(g.ev[EV_START], fs()));
@@ -1034,7 +1068,7 @@ static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) 
     if (!(g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0 &&
           std::memcmp(g.verified_rows, g.traced_rows, sizeof g.traced_rows) == 0))
         return RT_SUCCESS;
-    if (begin_slot(false) || begin_frame()) return RT_FAILURE;
+    if (begin_slot(false, 2) || begin_frame()) return RT_FAILURE;
     const hipStream_t s = fs();
     HIP_TRY(hipEventRecord(g.ev[EV_START], s));
     if (trace_rows(p, 0, 1, H)) return RT_FAILURE;
@@ -1137,7 +1171,7 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
     if (!row_calls_device) return fail("row_calls_device is NULL");
     HIP_TRY(hipSetDevice(g.device));
     const int n_rows = n_selected_rows(p);
-    if (begin_slot(false)) return RT_FAILURE;
+    if (begin_slot(false, g.nslots)) return RT_FAILURE;
     for (int attempt = 0; attempt < 4; attempt++) {
         if (begin_frame()) return RT_FAILURE;
         HIP_TRY(hipEventRecord(g.ev[EV_START], fs()));
@@ -1223,6 +1257,13 @@ int rt_gpu_set_accel(int mode) {
 }
 
 int rt_gpu_accel_active(void) { return g.last_accel ? 1 : 0; }
+
+int rt580_set_ao_order(int on) {
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (on != 0 && on != 1) return fail("rt580_set_ao_order: %d is not 0 or 1", on);
+    g_ao_order = on;
+    return RT_SUCCESS;
+}
 
 int rt580_set_chunk_log2(int log2) {
     if (!g.inited) return fail("rt_gpu_init not called");
@@ -1332,6 +1373,7 @@ void shutdown_ctx() {
         if (sl.bad_host) (void)hipHostFree(sl.bad_host);
         if (sl.stream) (void)hipStreamDestroy(sl.stream);
         if (sl.done) (void)hipEventDestroy(sl.done);
+        if (sl.ao_done) (void)hipEventDestroy(sl.ao_done);
     }
     for (auto& ev : g.user_mark)
         if (ev) (void)hipEventDestroy(ev);

@@ -77,6 +77,7 @@ SIGNATURES = [
                                         ctypes.c_void_p]),
     ("rt_gpu_accel_active", ctypes.c_int, []),
     ("rt580_set_chunk_log2", ctypes.c_int, [ctypes.c_int]),
+    ("rt580_set_ao_order", ctypes.c_int, [ctypes.c_int]),
     ("rt_gpu_host_register", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     ("rt_gpu_host_unregister", ctypes.c_int, [ctypes.c_void_p]),
     ("rt580_selftest_math", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),

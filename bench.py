@@ -328,7 +328,13 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     # AO rays per timed launch: the chunked BVH launches report theirs; a
     # small-scene frame is one launch over all of its (this context's) AO rays
     k_units = k_rays.value if k_rays.value else int(local["rays_ao"]) * max(frames.value, 1)
-    out["roofline"] = roofline(name, k_ms.value, k_launches.value, k_units)
+    iso = None
+    if not ctx.dist_on and not ctx.multi and K == 1:
+        # after the timed region (and after the last frame was copied out): the
+        # same frames with AO phases in frame order, so no other frame's AO
+        # kernels run beside the timed launch -- its isolated duration
+        iso = isolated_ao_launch(lib, rt580, step, torch, int(local["rays_ao"]))
+    out["roofline"] = roofline(name, k_ms.value, k_launches.value, k_units, iso)
     if frame_np is not None:
         out["frame_check"] = frame_check(ctx, name, frame_np, single, W, H, check)
     if not ctx.dist_on and not ctx.multi and K == 1:
@@ -360,7 +366,36 @@ def frame_check(ctx, name, frame_np, single, W, H, check):
     return res
 
 
-def roofline(workload, k_ms, k_launches, k_rays):
+def isolated_ao_launch(lib, rt580, step, torch, rays_ao_frame, frames=3):
+    """Mean AO-kernel launch (ms) and AO rays per launch over `frames` frames
+    rendered with AO phases in frame order (rt580_set_ao_order(1)): the AO
+    kernel then shares the chip with the next frame's trace at most, never with
+    another frame's AO kernels. Untimed; restores the default order."""
+    rt580.check(lib.rt580_set_ao_order(1), "rt580_set_ao_order")
+    try:
+        step()
+        torch.cuda.synchronize()
+        rt580.check(lib.rt_gpu_profile(1), "rt_gpu_profile")
+        for _ in range(frames):
+            step()
+        torch.cuda.synchronize()
+        ms = [ctypes.c_double() for _ in range(4)]
+        nf = ctypes.c_int()
+        rt580.check(lib.rt_gpu_profile_read(*[ctypes.byref(m) for m in ms], ctypes.byref(nf)), "rt_gpu_profile_read")
+        rt580.check(lib.rt_gpu_profile(0), "rt_gpu_profile")
+        k_ms, k_launches, k_rays = ctypes.c_double(), ctypes.c_int(), ctypes.c_uint64()
+        rt580.check(lib.rt_gpu_profile_ao_kernel(ctypes.byref(k_ms), ctypes.byref(k_launches), ctypes.byref(k_rays)),
+                    "rt_gpu_profile_ao_kernel")
+    finally:
+        rt580.check(lib.rt580_set_ao_order(0), "rt580_set_ao_order")
+    if k_launches.value <= 0:
+        return None
+    units = k_rays.value if k_rays.value else rays_ao_frame * max(nf.value, 1)
+    return {"launch_ms": k_ms.value / k_launches.value, "rays_per_launch": units / k_launches.value,
+            "frames": frames}
+
+
+def roofline(workload, k_ms, k_launches, k_rays, iso=None):
     """Roofline of the AO ray kernel (the scene query of every AO sample; 95 %
     of the frame's rays). Neither MFMA nor HBM bounds it (no dense
     contraction; the scene is re-read from L2/MALL, see `traffic`): it is
@@ -405,9 +440,17 @@ def roofline(workload, k_ms, k_launches, k_rays):
     res["profile"] = {"file": os.path.relpath(path, REPO), "launch_ms_rocprof": prof.get("avg_ms"),
                       "valu_issue_frac_rocprof": prof.get("valu_issue_frac"),
                       "frame_share_rocprof": prof.get("frame_share"), "top_kernels": prof.get("top_kernels")}
+    if iso:
+        a_iso = prof["valu_per_ao_ray"] * iso["rays_per_launch"] / (iso["launch_ms"] * 1e-3) / 1e9
+        res["isolated"] = {"launch_ms": round(iso["launch_ms"], 4), "ao_rays_per_launch": int(iso["rays_per_launch"]),
+                           "achieved": round(a_iso, 2), "frac": round(a_iso / VALU_PEAK_GINST, 4),
+                           "note": "the same kernel timed over %d further frames with AO phases in frame order "
+                                   "(rt580_set_ao_order(1), untimed): no other frame's AO kernels beside the launch"
+                                   % iso["frames"]}
     res["note"] = ("VALU-issue roofline: counter-measured VALU wave-instructions per AO ray x AO rays per launch "
-                   "/ live launch time; traffic = FETCH_SIZE+WRITE_SIZE (x1 KiB) per AO ray x rays per launch "
-                   "(HBM is not the bound: see hbm.frac)")
+                   "/ live launch time (frames overlap: AO phases of consecutive frames may run together, which "
+                   "stretches each launch; `isolated` times it without that); traffic = FETCH_SIZE+WRITE_SIZE "
+                   "(x1 KiB) per AO ray x rays per launch (HBM is not the bound: see hbm.frac)")
     return res
 
 

@@ -234,6 +234,10 @@ int rt_gpu_accel_active(void);
  * small chunks let the tests reach the multi-chunk paths on small frames.
  * Synchronizes; applies to the following renders. Test hook. */
 int rt580_set_chunk_log2(int log2);
+/* AO phases of consecutive frames in frame order (1) or free to overlap (0,
+ * default; $RT580_AO_ORDER). Applies to the following frames. Bench hook: the
+ * isolated launch time of the AO kernel. */
+int rt580_set_ao_order(int on);
 /* Counters and HIP-event timings of the last render. */
 int rt_gpu_last_stats(rt_render_stats* stats);
 /* Bench profiling: with enable=1 every following frame records its own HIP
