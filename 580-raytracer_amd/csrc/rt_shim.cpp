@@ -139,7 +139,7 @@ struct State {
 };
 
 constexpr int kMaxCtx = 16;
-constexpr int kChunkLog2Min = 6, kChunkLog2Max = 26;  // chunk capacities of BVH frames (rays)
+constexpr int kChunkLog2Min = 6, kChunkLog2Max = 27;  // chunk capacities of BVH frames (rays)
 State g_ctx[kMaxCtx];
 int g_cur = 0;  // context the entry points act on (0 outside rt_gpu_render_multi)
 #define g (g_ctx[g_cur])

@@ -94,5 +94,5 @@ def test_chunk_limit_is_validated():
     lib = helpers.rt580().load()
     assert lib.rt_gpu_init(0) == 0
     assert lib.rt580_set_chunk_log2(5) != 0
-    assert lib.rt580_set_chunk_log2(27) != 0
+    assert lib.rt580_set_chunk_log2(28) != 0
     assert lib.rt580_set_chunk_log2(DEFAULT_LOG2) == 0

@@ -33,7 +33,7 @@ def _init_with(env):
     ({"RT580_NO_SUCH_SWITCH": "1"}, "unknown environment switch RT580_NO_SUCH_SWITCH"),
     ({"RT580_AO_VARIANT": "512"}, "RT580_AO_VARIANT=512: not one of the supported values"),
     ({"RT580_AO_VARIANT": "x"}, "not an integer"),
-    ({"RT580_CHUNK_LOG2": "27"}, "RT580_CHUNK_LOG2=27: outside [6, 26]"),
+    ({"RT580_CHUNK_LOG2": "28"}, "RT580_CHUNK_LOG2=28: outside [6, 27]"),
     ({"RT580_MULTI_TRANSPORT": "tcp"}, "not one of the supported values"),
     ({"RT580_GRID_R": "-1"}, "not a finite number > 0"),
     ({"RT580_DUMP_FAR": "/tmp/x"}, "diagnostic builds only"),
