@@ -229,7 +229,7 @@ int rt580_eval_powf(const float* x_device, float y, float* out_device, uint64_t 
 int rt_gpu_set_accel(int mode);
 int rt_gpu_accel_active(void);
 /* Largest chunk of the chunked passes of BVH frames (far-hit queue, AO ray
- * records): 2^log2 rays, log2 in [6, 27] (default 26, or $RT580_CHUNK_LOG2 read
+ * records): 2^log2 rays, log2 in [6, 27] (default 27, or $RT580_CHUNK_LOG2 read
  * by rt_gpu_init). Larger frames run in several chunks with identical results;
  * small chunks let the tests reach the multi-chunk paths on small frames.
  * Synchronizes; applies to the following renders. Test hook. */

@@ -3,7 +3,7 @@ reach by default.
 
 BVH frames run the far-hit queue of each trace level, and the AO samples
 (CalculateAmbientOcclusion, Raytracer.cpp:315-330: one RNG draw pair and one
-IntersectScene per sample), in chunks of at most 2^26 rays. A 1080p-8K frame
+IntersectScene per sample), in chunks of at most 2^27 rays. A 1080p-8K frame
 crosses those boundaries; the small frames of the other parity tests never do.
 rt580_set_chunk_log2 lowers the limit so that small frames run the same code
 over many chunks: a level's rays split across chunks (far queue, shadow flags,
@@ -21,7 +21,7 @@ import helpers
 
 pytestmark = pytest.mark.gpu
 
-DEFAULT_LOG2 = 26
+DEFAULT_LOG2 = 27
 
 
 @functools.lru_cache(None)

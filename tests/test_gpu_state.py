@@ -153,7 +153,7 @@ def test_replayed_bvh_frames_match_oracle():
     n = w * h * 3
     order = [0, 0, 0, 0, 1, 1, 1, 0, 1, 0]
     try:
-        for log2 in (8, 26):
+        for log2 in (8, 27):
             assert lib.rt580_set_chunk_log2(log2) == 0
             got = _device_frames(lib, rt580, [rts[k][1] for k in order], n, dev, torch)
             assert lib.rt_gpu_accel_active() == 1
@@ -164,7 +164,7 @@ def test_replayed_bvh_frames_match_oracle():
         for _ in range(3):
             rt580.check(lib.rt_gpu_render(ctypes.byref(rts[0][1]), host.ctypes.data), "render")
     finally:
-        lib.rt580_set_chunk_log2(26)
+        lib.rt580_set_chunk_log2(27)
         lib.rt_gpu_set_stream(lib.rt_gpu_own_stream())
 
 
