@@ -2509,14 +2509,26 @@ __global__ void count_check_kernel(const uint32_t* dev, uint32_t e0, uint32_t e1
     if (threadIdx.x == 0 && (dev[0] != e0 || (n > 1 && dev[1] != e1))) *bad = 1u;
 }
 
-// n (1 or 2) device words -> out (pinned), through the count schedule.
-static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStream_t s) {
+// n (1 or 2) device words -> out (pinned), through the count schedule. Each
+// count sizes launches over a buffer: out[0] <= cap0 and out[1] <= cap1, else
+// the frame fails before anything is launched from it (a replayed count that
+// does not fit is a broken schedule; a read one, a queue that overran).
+static hipError_t counts_fit(const uint32_t* out, int n, uint32_t cap0, uint32_t cap1) {
+    if (out[0] <= cap0 && (n < 2 || out[1] <= cap1)) return hipSuccess;
+    if (g_cs && g_cs->mode == CountSchedule::REPLAY) g_cs->broken = true;
+    RT_STEP("count check (a device count exceeds its buffer's capacity)");
+    return hipErrorInvalidValue;
+}
+
+static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStream_t s, uint32_t cap0,
+                              uint32_t cap1 = 0xffffffffu) {
     if (g_cs && g_cs->mode == CountSchedule::REPLAY) {
         if (g_cs->pos + (size_t)n > g_cs->vals.size()) {
             g_cs->broken = true;
             return hipErrorInvalidValue;
         }
         for (int i = 0; i < n; i++) out[i] = g_cs->vals[g_cs->pos++];
+        if (counts_fit(out, n, cap0, cap1) != hipSuccess) return hipErrorInvalidValue;
         uint32_t e0 = out[0];
 #ifdef RT580_DIAGNOSTICS
         {   // DIAGNOSTIC build only: RT580_REPLAY_CORRUPT=1 makes every check fail (tests the detection)
@@ -2533,6 +2545,7 @@ static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStre
     }
     hipError_t e = hipMemcpyAsync(out, dev, (size_t)n * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = counts_fit(out, n, cap0, cap1);
     if (e == hipSuccess && g_cs && g_cs->mode == CountSchedule::RECORD)
         for (int i = 0; i < n; i++) g_cs->vals.push_back(out[i]);
     return e;
@@ -2580,7 +2593,7 @@ static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t
     RT_STEP("far queue segments");
     hipError_t e = hipcub::DeviceRunLengthEncode::Encode(W.sort_tmp, tmp, W.far_keys_alt, W.far_keys, W.far_vals,
                                                          W.far_seg_n, (int)n, s);
-    if (e == hipSuccess) e = read_counts(W.far_seg_n, 1, W.far_count_host + 2, s);
+    if (e == hipSuccess) e = read_counts(W.far_seg_n, 1, W.far_count_host + 2, s, n);
     if (e != hipSuccess) return e;
     const uint32_t nseg = W.far_count_host[2];
     if (nseg == 0) return hipSuccess;
@@ -2829,9 +2842,10 @@ static int sort_begin_bit(const DevScene& S) {
 
 static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
     RT_STEP("far queue count D2H");
-    hipError_t e = read_counts(W.far_count, 2, W.far_count_host, s);
+    hipError_t e = read_counts(W.far_count, 2, W.far_count_host, s, W.far_cap, W.far_cap);
     if (e != hipSuccess) return e;
     nq = W.far_count_host[0];
+    if (W.far_count_host[1] > nq) return counts_fit(W.far_count_host, 2, W.far_cap, nq);
     nb = W.far_count_host[1];  // far-origin rays: keyed to sort last
     if (nq == 0) return hipSuccess;
     size_t tmp = W.sort_tmp_bytes;
@@ -2873,8 +2887,10 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
             uint32_t count = (uint32_t)npix;
             if (level > 0) {
                 RT_STEP("level count D2H");
-                if ((e = read_counts(W.lvl + level, 1, W.far_count_host, s)) != hipSuccess) return e;
-                count = *W.far_count_host;
+                if ((e = read_counts(W.lvl + level, 1, W.far_count_host, s, 0xffffffffu)) != hipSuccess) return e;
+                // children beyond the node capacity were never stored (the
+                // kernels clamp to it too; the frame is rendered again larger)
+                count = *W.far_count_host < W.node_cap ? *W.far_count_host : W.node_cap;
             }
             if (count == 0) {  // still publish the next level's base
                 hipLaunchKernelGGL((trace_kernel<true, 2>), dim3(1), dim3(TB), 0, s, S, F, W, level, 0u, 0u);
@@ -3054,7 +3070,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
     if (S.use_bvh) {
         // chunks of the AO items: near pass + queue, sort the misses by
         // direction, wave-cooperative far pass
-        hipError_t e = read_counts(reinterpret_cast<const uint32_t*>(W.totals), 2, W.far_count_host + 4, s);
+        hipError_t e = read_counts(reinterpret_cast<const uint32_t*>(W.totals), 2, W.far_count_host + 4, s, W.call_cap, 0u);
         if (e != hipSuccess) return e;
         const uint64_t calls = (uint64_t)W.far_count_host[4] | ((uint64_t)W.far_count_host[5] << 32);
         const uint64_t items = calls * (uint64_t)F.ao_samples;

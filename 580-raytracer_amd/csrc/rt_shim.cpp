@@ -61,6 +61,7 @@ struct SchedKey {
     uint64_t gen;
     int rows[3];
     uint32_t far_chunk, ao_chunk;  // the frame's chunk sizes (they set the passes' sequence)
+    int32_t accel;                 // the scene query (brute-force frames read no counts)
 };
 
 struct State {
@@ -147,6 +148,24 @@ int g_cur = 0;  // context the entry points act on (0 outside rt_gpu_render_mult
 char g_err[512] = "";
 uint64_t g_scene_counter = 0;  // process-wide upload counter (survives rt_gpu_shutdown)
 
+// Fault attribution. A device fault is reported by whichever HIP call next
+// looks at the device, so every error names the entry point that saw it
+// (g_call) and every device-side error also the last entry point that enqueued
+// device work (g_last_work): a fault raised by a frame but first seen by the
+// next call's upload is charged to that frame.
+const char* g_call = "";
+const char* g_last_work = "(no device work yet)";
+struct CallScope {
+    const char* prev;
+    CallScope(const char* name, bool work) : prev(g_call) {
+        g_call = name;
+        if (work) g_last_work = name;
+    }
+    ~CallScope() { g_call = prev; }
+};
+#define RT_ENTRY(name) CallScope rt_call_scope_(name, false)  // entry point that does not enqueue device work
+#define RT_WORK(name) CallScope rt_call_scope_(name, true)    // entry point that enqueues device work
+
 #define SL (g.slot[g.cur])
 
 // Stream of the frame being enqueued.
@@ -154,12 +173,25 @@ hipStream_t fs() { return g.pipeline ? g.slot[g.cur].stream : g.stream; }
 
 
 int fail(const char* fmt, ...) {
+    char msg[448];
     va_list ap;
     va_start(ap, fmt);
-    std::vsnprintf(g_err, sizeof g_err, fmt, ap);
+    std::vsnprintf(msg, sizeof msg, fmt, ap);
     va_end(ap);
+    if (g_call[0]) std::snprintf(g_err, sizeof g_err, "%s: %s", g_call, msg);
+    else std::snprintf(g_err, sizeof g_err, "%s", msg);
     std::fprintf(stderr, "rt_gpu: %s\n", g_err);
     return RT_FAILURE;
+}
+
+// A checked wait for the whole device (every stream of this process on it).
+// An error here was raised by earlier device work: named as such.
+int device_sync(const char* what) {
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess)
+        return fail("device error seen %s (raised by device work enqueued up to %s): %s", what, g_last_work,
+                    hipGetErrorString(e));
+    return RT_SUCCESS;
 }
 
 #define HIP_TRY(expr)                                                              \
@@ -238,17 +270,40 @@ bool frame_uses_bvh(const rt_render_params* p) {
     return g.accel == RT_ACCEL_AUTO && g.bvh_ok && bvh_usable(g.bvh, p->cam_from);
 }
 
-// Wait for every enqueued frame (every slot) and the caller's stream.
+// A checked wait for one stream; an error was raised by earlier device work.
+int stream_sync(hipStream_t s, const char* what) {
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess)
+        return fail("device error seen %s (raised by device work enqueued up to %s): %s", what, g_last_work,
+                    hipGetErrorString(e));
+    return RT_SUCCESS;
+}
+
+// Wait for every enqueued frame and the caller's stream -- of every context on
+// this context's device (the split rehearsal keeps several contexts on one
+// GPU; a scene upload or buffer release must not race any of them).
 int sync_all() {
-    HIP_TRY(hipStreamSynchronize(g.stream));
-    if (g.pipeline)
-        for (auto& sl : g.slot) HIP_TRY(hipStreamSynchronize(sl.stream));
+    const int dev = g.device;
+    for (int k = 0; k < kMaxCtx; k++) {
+        State& c = g_ctx[k];
+        if (!c.inited || c.device != dev) continue;
+        if (stream_sync(c.stream, "waiting for the caller's stream")) return RT_FAILURE;
+        if (c.own_stream != c.stream && stream_sync(c.own_stream, "waiting for the library's stream")) return RT_FAILURE;
+        for (auto& sl : c.slot)
+            if (sl.stream && stream_sync(sl.stream, "waiting for a frame slot")) return RT_FAILURE;
+        if (c.aux && stream_sync(c.aux, "waiting for the latency path's stream")) return RT_FAILURE;
+    }
     return RT_SUCCESS;
 }
 
 int ensure(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return RT_SUCCESS;
-    if (b.p) { (void)hipDeviceSynchronize(); (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
+    if (b.p) {  // frames in flight may still read the old buffer
+        if (device_sync("before a workspace buffer is resized")) return RT_FAILURE;
+        HIP_TRY(hipFree(b.p));
+        b.p = nullptr;
+        b.bytes = 0;
+    }
     if (bytes == 0) bytes = 64;
     size_t want = bytes + bytes / 8 + 256;
     HIP_TRY(hipMalloc(&b.p, want));
@@ -329,11 +384,24 @@ DevScene dev_scene(const rt_render_params* p) {
     return s;
 }
 
+// Scene uploads are synchronous: every copy has completed (and any device
+// error it met is reported, naming the array) before the call returns or the
+// host array is freed.
+int h2d(void* dst, const void* src, size_t bytes, const char* what) {
+    if (!bytes) return RT_SUCCESS;
+    const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g.stream);
+    if (e != hipSuccess)
+        return fail("copy of %s (%zu bytes) to the device (device work enqueued up to %s): %s", what, bytes,
+                    g_last_work, hipGetErrorString(e));
+    char w[96];
+    std::snprintf(w, sizeof w, "by the copy of %s", what);
+    return stream_sync(g.stream, w);
+}
+
 template <typename T>
-int upload_vec(DevBuf& b, const std::vector<T>& v) {
+int upload_vec(DevBuf& b, const std::vector<T>& v, const char* what) {
     if (ensure(b, sizeof(T) * v.size() + 64)) return RT_FAILURE;
-    if (!v.empty()) HIP_TRY(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, g.stream));
-    return RT_SUCCESS;
+    return h2d(b.p, v.data(), sizeof(T) * v.size(), what);
 }
 
 DevFrame dev_frame(const rt_render_params* p, int row_begin, int row_step, int n_rows) {
@@ -527,6 +595,7 @@ SchedKey sched_key(const rt_render_params* p) {
     std::memcpy(k.rows, g.traced_rows, sizeof k.rows);
     k.far_chunk = g.frame_fc;
     k.ao_chunk = g.frame_ac;
+    k.accel = frame_uses_bvh(p) ? 1 : 0;
     return k;
 }
 
@@ -596,8 +665,8 @@ int check_replay(Slot& sl) {
     *sl.bad_host = 0;
     HIP_TRY(hipMemset(sl.bad.p, 0, 64));
     g.trace_valid = g.ao_valid = false;
-    return fail("a replayed count schedule did not match its frame's counts (the frame two calls back on this "
-                "context; schedules dropped)");
+    return fail("a replayed count schedule did not match its frame's counts (the last frame enqueued on this "
+                "slot, %d frame calls back at most; schedules dropped)", g.nslots);
 }
 
 // Phase 1: trace every level of the selected rows and count their AO calls.
@@ -791,6 +860,7 @@ int clone_scene(int src) {
 extern "C" {
 
 int rt_gpu_init(int device) {
+    RT_WORK("rt_gpu_init");
     if (g.inited) return RT_SUCCESS;
     {   // every RT580_* switch known and valid (rt_knobs.cpp), before anything reads one
         char why[256];
@@ -851,6 +921,7 @@ int rt_gpu_init(int device) {
 }
 
 int rt_gpu_set_stream(void* s) {
+    RT_ENTRY("rt_gpu_set_stream");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (sync_all()) return RT_FAILURE;
     g.stream = (hipStream_t)s;  // NULL: the HIP null stream (e.g. PyTorch's default stream)
@@ -860,6 +931,7 @@ int rt_gpu_set_stream(void* s) {
 void* rt_gpu_own_stream(void) { return g.inited ? (void*)g.own_stream : nullptr; }
 
 int rt_gpu_upload_scene(const rt_scene_soa* s) {
+    RT_WORK("rt_gpu_upload_scene");
     if (!g.inited && rt_gpu_init(-1) != RT_SUCCESS) return RT_FAILURE;
     if (!s || s->abi_version != RT580_ABI_VERSION) return fail("bad rt_scene_soa / ABI version");
     if (s->n_prims < 0 || s->n_lights < 0 || s->n_materials < 0) return fail("negative scene sizes");
@@ -872,20 +944,21 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         if (s->lights[i].kind < RT_LIGHT_DIRECTIONAL || s->lights[i].kind > RT_LIGHT_AMBIENT)
             return fail("light %d: bad kind", i);
     HIP_TRY(hipSetDevice(g.device));
-    if (sync_all()) return RT_FAILURE;  // frames in flight still read the old scene
+    // frames in flight still read the old scene; a fault they raised is
+    // reported here, charged to the call that enqueued them
+    if (sync_all() || device_sync("before the scene upload")) return RT_FAILURE;
+    g.have_scene = false;  // until the new one is complete
+    g_last_work = "rt_gpu_upload_scene";
     if (ensure(g.prims, sizeof(rt_prim) * (size_t)s->n_prims + 64) ||
         ensure(g.shade, sizeof(rt_prim_shade) * (size_t)s->n_prims + 64) ||
         ensure(g.mats, sizeof(rt_material) * (size_t)s->n_materials + 64) ||
         ensure(g.lights, sizeof(rt_light) * (size_t)s->n_lights + 64))
         return RT_FAILURE;
-    if (s->n_prims) {
-        HIP_TRY(hipMemcpyAsync(g.prims.p, s->prims, sizeof(rt_prim) * s->n_prims, hipMemcpyHostToDevice, g.stream));
-        HIP_TRY(hipMemcpyAsync(g.shade.p, s->shade, sizeof(rt_prim_shade) * s->n_prims, hipMemcpyHostToDevice, g.stream));
-    }
-    if (s->n_materials)
-        HIP_TRY(hipMemcpyAsync(g.mats.p, s->materials, sizeof(rt_material) * s->n_materials, hipMemcpyHostToDevice, g.stream));
-    if (s->n_lights)
-        HIP_TRY(hipMemcpyAsync(g.lights.p, s->lights, sizeof(rt_light) * s->n_lights, hipMemcpyHostToDevice, g.stream));
+    if (h2d(g.prims.p, s->prims, sizeof(rt_prim) * (size_t)s->n_prims, "the primitive records") ||
+        h2d(g.shade.p, s->shade, sizeof(rt_prim_shade) * (size_t)s->n_prims, "the shading table") ||
+        h2d(g.mats.p, s->materials, sizeof(rt_material) * (size_t)s->n_materials, "the materials") ||
+        h2d(g.lights.p, s->lights, sizeof(rt_light) * (size_t)s->n_lights, "the lights"))
+        return RT_FAILURE;
     // exact BVH for triangle scenes that do not fit one LDS tile (rt_bvh.h)
     g.bvh = BvhBuild();
     g.bvh_ok = false;
@@ -903,11 +976,17 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         // the 4-wide form for the any-hit queries (AO, shadows); RT580_BVH4=0: binary only
         const char* b4 = std::getenv("RT580_BVH4");
         if (g.bvh_ok && !(b4 && std::atoi(b4) == 0)) collapse_bvh4(g.bvh);
-        if (g.bvh_ok && (upload_vec(g.bvh_nodes, g.bvh.nodes) || upload_vec(g.bvh_nodes4, g.bvh.nodes4q) || upload_vec(g.bvh_prims, g.bvh.prims) ||
-                         upload_vec(g.bvh_ids, g.bvh.ids) || upload_vec(g.far_nodes, g.bvh.far_nodes) ||
-                         upload_vec(g.far_tris, g.bvh.far_tris) || upload_vec(g.brute, g.bvh.brute) ||
-                         upload_vec(g.grid_start, g.bvh.grid_start) || upload_vec(g.grid_items, g.bvh.grid_items) ||
-                         upload_vec(g.grid_always, g.bvh.grid_always)))
+        if (g.bvh_ok &&
+            (upload_vec(g.bvh_nodes, g.bvh.nodes, "the BVH nodes") ||
+             upload_vec(g.bvh_nodes4, g.bvh.nodes4q, "the 4-wide BVH nodes") ||
+             upload_vec(g.bvh_prims, g.bvh.prims, "the leaf-ordered primitives") ||
+             upload_vec(g.bvh_ids, g.bvh.ids, "the leaf primitive ids") ||
+             upload_vec(g.far_nodes, g.bvh.far_nodes, "the plane-tree nodes") ||
+             upload_vec(g.far_tris, g.bvh.far_tris, "the plane records") ||
+             upload_vec(g.brute, g.bvh.brute, "the brute-force list") ||
+             upload_vec(g.grid_start, g.bvh.grid_start, "the direction-grid offsets") ||
+             upload_vec(g.grid_items, g.bvh.grid_items, "the direction-grid lists") ||
+             upload_vec(g.grid_always, g.bvh.grid_always, "the direction-grid always-list")))
             return RT_FAILURE;
         if (g.bvh_ok && !g.bvh.far_nodes.empty()) {
             // The any-hit scan order of far-origin rays (far_scan_kernel): a fixed
@@ -919,7 +998,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
             std::vector<rt_prim> perm(s->prims, s->prims + s->n_prims);
             std::mt19937 rng(580u);
             std::shuffle(perm.begin(), perm.end(), rng);
-            if (upload_vec(g.scan_prims, perm)) return RT_FAILURE;
+            if (upload_vec(g.scan_prims, perm, "the shuffled scan order")) return RT_FAILURE;
         }
         g.grid_log2 = g.bvh.grid_start.empty() ? 0 : g.bvh.grid_log2;
         g.grid_n_always = (int)g.bvh.grid_always.size();
@@ -933,7 +1012,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         g.bvh.grid_items = std::vector<uint32_t>();
         g.bvh.grid_always = std::vector<uint32_t>();
     }
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    if (device_sync("at the end of the scene upload")) return RT_FAILURE;
     g.n_prims = s->n_prims;
     g.n_lights = s->n_lights;
     g.n_ambient = 0;
@@ -952,6 +1031,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
 uint64_t rt_gpu_scene_id(void) { return g.inited && g.have_scene ? g.scene_gen : 0; }
 
 int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
+    RT_WORK("rt_gpu_render_device");
     if (check_params(p)) return RT_FAILURE;
     HIP_TRY(hipSetDevice(g.device));
     const int n_sel = n_selected_rows(p);
@@ -1122,6 +1202,7 @@ static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) 
 }
 
 int rt_gpu_render(const rt_render_params* p, int16_t* fb_out) {
+    RT_WORK("rt_gpu_render");
     if (check_params(p)) return RT_FAILURE;
     HIP_TRY(hipSetDevice(g.device));
     if (fb_out) {
@@ -1141,6 +1222,7 @@ int rt_gpu_render(const rt_render_params* p, int16_t* fb_out) {
 }
 
 int rt_gpu_host_register(void* host_ptr, uint64_t bytes) {
+    RT_ENTRY("rt_gpu_host_register");
     if (!host_ptr || bytes == 0) return fail("rt_gpu_host_register: empty range");
     if (host_registered(host_ptr, bytes)) return RT_SUCCESS;
     if (!g.inited && rt_gpu_init(-1) != RT_SUCCESS) return RT_FAILURE;
@@ -1150,6 +1232,7 @@ int rt_gpu_host_register(void* host_ptr, uint64_t bytes) {
 }
 
 int rt_gpu_host_unregister(void* host_ptr) {
+    RT_ENTRY("rt_gpu_host_unregister");
     for (size_t i = 0; i < g_host_ranges.size(); i++)
         if (g_host_ranges[i].p == (const char*)host_ptr) {
             for (int k = 0; k < kMaxCtx; k++)  // no copy into it may still be in flight
@@ -1168,6 +1251,7 @@ int rt_gpu_host_unregister(void* host_ptr) {
 }
 
 int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
+    RT_WORK("rt_gpu_count_rows");
     if (check_params(p)) return RT_FAILURE;
     if (!row_calls_device) return fail("row_calls_device is NULL");
     HIP_TRY(hipSetDevice(g.device));
@@ -1198,6 +1282,7 @@ int rt_gpu_count_rows(const rt_render_params* p, uint32_t* row_calls_device) {
 }
 
 int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device, int16_t* fb_device) {
+    RT_WORK("rt_gpu_shade_rows");
     if (check_params(p)) return RT_FAILURE;
     if (!row_base_device || !fb_device) return fail("row_base_device / fb_device is NULL");
     if (!g.split_ready || std::memcmp(&g.split_params, p, sizeof *p) != 0)
@@ -1210,6 +1295,7 @@ int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device
 }
 
 int rt_gpu_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out) {
+    RT_WORK("rt_gpu_gamma_u8");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (n && (!fb || !out)) return fail("rt_gpu_gamma_u8: NULL buffer");
     HIP_TRY(hipSetDevice(g.device));
@@ -1218,6 +1304,7 @@ int rt_gpu_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out) {
 }
 
 int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches) {
+    RT_WORK("rt580_selftest_math");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (!mismatches) return fail("rt580_selftest_math: NULL output");
     HIP_TRY(hipSetDevice(g.device));
@@ -1233,6 +1320,7 @@ int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches) {
 }
 
 int rt580_eval_powf(const float* x_device, float y, float* out_device, uint64_t n) {
+    RT_WORK("rt580_eval_powf");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (n && (!x_device || !out_device)) return fail("rt580_eval_powf: NULL buffer");
     HIP_TRY(hipSetDevice(g.device));
@@ -1241,6 +1329,7 @@ int rt580_eval_powf(const float* x_device, float y, float* out_device, uint64_t 
 }
 
 int rt_gpu_row_bases(const int32_t* gathered, int world, int n_max, int height, int rank, uint64_t* row_base) {
+    RT_WORK("rt_gpu_row_bases");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (!gathered || !row_base) return fail("rt_gpu_row_bases: NULL buffer");
     if (world <= 0 || rank < 0 || rank >= world || height < 0 || n_max < (height + world - 1) / world)
@@ -1251,15 +1340,18 @@ int rt_gpu_row_bases(const int32_t* gathered, int world, int n_max, int height, 
 }
 
 int rt_gpu_set_accel(int mode) {
+    RT_ENTRY("rt_gpu_set_accel");
     if (mode != RT_ACCEL_BRUTE && mode != RT_ACCEL_AUTO) return fail("bad accel mode %d", mode);
     g.accel = mode;
     g.verified_valid = false;  // node capacity is re-verified under the new mode
+    g.trace_valid = g.ao_valid = false;  // recorded count schedules belong to the old mode
     return RT_SUCCESS;
 }
 
 int rt_gpu_accel_active(void) { return g.last_accel ? 1 : 0; }
 
 int rt580_set_ao_order(int on) {
+    RT_ENTRY("rt580_set_ao_order");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (on != 0 && on != 1) return fail("rt580_set_ao_order: %d is not 0 or 1", on);
     g_ao_order = on;
@@ -1267,6 +1359,7 @@ int rt580_set_ao_order(int on) {
 }
 
 int rt580_set_chunk_log2(int log2) {
+    RT_ENTRY("rt580_set_chunk_log2");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (log2 < kChunkLog2Min || log2 > kChunkLog2Max)
         return fail("chunk log2 %d outside [%d, %d]", log2, kChunkLog2Min, kChunkLog2Max);
@@ -1277,6 +1370,7 @@ int rt580_set_chunk_log2(int log2) {
 }
 
 int rt_gpu_last_stats(rt_render_stats* st) {
+    RT_ENTRY("rt_gpu_last_stats");
     if (!st) return RT_INVALID_ARG;
     std::memset(st, 0, sizeof *st);
     if (!g.last_valid) return fail("no frame rendered yet");
@@ -1306,6 +1400,7 @@ int rt_gpu_last_stats(rt_render_stats* st) {
 }
 
 int rt_gpu_profile(int enable) {
+    RT_ENTRY("rt_gpu_profile");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (sync_all()) return RT_FAILURE;
     // keep g.ev on the last profiled frame's events so rt_gpu_last_stats stays valid
@@ -1318,6 +1413,7 @@ int rt_gpu_profile(int enable) {
 }
 
 int rt_gpu_profile_ao_kernel(double* ms_total, int* launches, uint64_t* ao_rays) {
+    RT_ENTRY("rt_gpu_profile_ao_kernel");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (!ms_total || !launches || !ao_rays) return fail("rt_gpu_profile_ao_kernel: NULL output");
     if (sync_all()) return RT_FAILURE;
@@ -1326,6 +1422,7 @@ int rt_gpu_profile_ao_kernel(double* ms_total, int* launches, uint64_t* ao_rays)
 }
 
 int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double* ms_resolve, int* frames) {
+    RT_ENTRY("rt_gpu_profile_read");
     if (!g.inited) return fail("rt_gpu_init not called");
     if (sync_all()) return RT_FAILURE;
     double t[4] = {0, 0, 0, 0};
@@ -1346,6 +1443,23 @@ int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double
 
 const char* rt_gpu_last_error(void) { return g_err; }
 
+int rt_gpu_synchronize(void) {
+    RT_ENTRY("rt_gpu_synchronize");
+    const int cur = g_cur;
+    int st = RT_SUCCESS;
+    for (int k = 0; k < kMaxCtx && st == RT_SUCCESS; k++) {
+        if (!g_ctx[k].inited) continue;
+        g_cur = k;
+        if (hipSetDevice(g.device) != hipSuccess) st = fail("hipSetDevice(%d) failed", g.device);
+        else if (sync_all() || device_sync("while waiting for every context")) st = RT_FAILURE;
+        for (int s = 0; s < State::kSlots && st == RT_SUCCESS; s++)
+            if (check_replay(g.slot[s])) st = RT_FAILURE;
+    }
+    g_cur = cur;
+    if (g_ctx[g_cur].inited) (void)hipSetDevice(g_ctx[g_cur].device);
+    return st;
+}
+
 }  // extern "C"
 
 namespace {
@@ -1356,7 +1470,8 @@ void release_multi_ctx(int k);
 void shutdown_ctx() {
     if (!g.inited) return;
     (void)hipSetDevice(g.device);
-    (void)sync_all();
+    if (sync_all() || device_sync("at shutdown"))
+        std::fprintf(stderr, "rt_gpu: shutting down after a device error (%s)\n", g_err);
     for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always})
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute,
@@ -1398,6 +1513,7 @@ void shutdown_ctx() {
 extern "C" {
 
 void rt_gpu_shutdown(void) {
+    RT_ENTRY("rt_gpu_shutdown");
     const int cur = g_cur;
     release_multi();
     for (int k = kMaxCtx - 1; k >= 0; k--) {
@@ -1677,7 +1793,8 @@ int multi_render(const rt_render_params* p, int16_t* fb_out, int n, const int* d
 }  // namespace
 
 extern "C" int rt_gpu_render_multi(const rt_render_params* p, int16_t* fb_out, int n_devices, const int* devices) {
-    if (g_cur != 0) return fail("rt_gpu_render_multi: re-entered");
+    RT_WORK("rt_gpu_render_multi");
+    if (g_cur != 0) return fail("re-entered");
     const int st = multi_render(p, fb_out, n_devices, devices);
     g_cur = 0;
     if (g.inited) (void)hipSetDevice(g.device);

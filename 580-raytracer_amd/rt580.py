@@ -83,6 +83,7 @@ SIGNATURES = [
     ("rt580_selftest_math", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     ("rt580_eval_powf", ctypes.c_int, [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint64]),
     ("rt_gpu_last_error", ctypes.c_char_p, []),
+    ("rt_gpu_synchronize", ctypes.c_int, []),
     ("rt_gpu_shutdown", None, []),
     ("rt580_create", ctypes.c_void_p, [ctypes.c_int, ctypes.c_int]),
     ("rt580_destroy", None, [ctypes.c_void_p]),

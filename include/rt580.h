@@ -161,7 +161,10 @@ void* rt_gpu_own_stream(void);
  * Single-rank: the RNG offsets are scanned on the device. Blocking. */
 int rt_gpu_render(const rt_render_params* params, int16_t* fb_out);
 /* Same, leaving the framebuffer in HBM (device pointer valid until the next
- * call); asynchronous on the shim's stream. */
+ * call); asynchronous on the shim's stream. A frame that replayed recorded
+ * counts (repeats of a frame, see rt_shim.cpp) is checked on the device; a
+ * mismatch is reported by the call that next uses the frame's slot (up to
+ * RT580_SLOTS calls later) or by rt_gpu_synchronize. */
 int rt_gpu_render_device(const rt_render_params* params, int16_t** fb_device);
 /* Page-lock a host buffer that will receive frames (rt_gpu_render's fb_out):
  * a frame copied into a registered range lands there with one DMA instead of
@@ -254,8 +257,15 @@ int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double
  * launches only; a small-scene frame is one launch over all of its AO rays,
  * rt_gpu_last_stats). Synchronizes. */
 int rt_gpu_profile_ao_kernel(double* ms_total, int* launches, uint64_t* ao_rays);
-/* Last error message (static storage). */
+/* Last error message (static storage). Errors name the entry point that saw
+ * them; a device fault (reported by whichever call next waits on the device)
+ * also names the last entry point that enqueued device work before it. */
 const char* rt_gpu_last_error(void);
+/* Wait for all device work of every context (every frame still in flight,
+ * rt_gpu_render_device's included) and check the replayed count schedules of
+ * those frames. RT_FAILURE names a device fault or a count mismatch and the
+ * call whose work raised it. Blocking. */
+int rt_gpu_synchronize(void);
 void rt_gpu_shutdown(void);
 
 /* ---- Reference class surface as a C ABI (what an FFI/ctypes binding calls) ----
