@@ -63,6 +63,11 @@ WORKLOADS = {
                 "BASELINE config 5: 1M-triangle field 7680x4320 depth=8 AO=256"),
 }
 CPU_BUDGET_S = 15.0  # one core, per workload (the all-cores leg renders the same pixels)
+# Frame check of the last timed frame against the oracle: pixels in 16 segments
+# spread over the frame's geometry rows (per workload: the oracle's cost per
+# pixel grows with triangles, depth and AO samples)
+CHECK_PIXELS = {"config2": 10240, "cornell10k": 10240, "field100k_1080p": 10240, "field100k": 4096, "field1m": 256}
+CHECK_SEGMENTS = 16
 
 
 def env_int(k, d):
@@ -335,14 +340,61 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
         # kernels run beside the timed launch -- its isolated duration
         iso = isolated_ao_launch(lib, rt580, step, torch, int(local["rays_ao"]))
     out["roofline"] = roofline(name, k_ms.value, k_launches.value, k_units, iso)
+    # per-row AO-call counts of the frame from one untimed GPU count pass: the
+    # RNG bases of the oracle's frame-check rows and of the CPU baseline's range
+    row_counts = None
+    if frame_np is not None and frame_np.dtype == np.int16 and not ctx.multi and not ctx.dist_on and \
+            ((check and ctx.args.check_pixels != 0) or cpu_baseline_on):
+        row_counts = helpers.rt580_dist().GpuRows(rt580, params, torch, ctx.device).count(0, 1)[:H].cpu().numpy()
     if frame_np is not None:
         out["frame_check"] = frame_check(ctx, name, frame_np, single, W, H, check)
+        if check and row_counts is not None:
+            n_px = ctx.args.check_pixels if ctx.args.check_pixels > 0 else CHECK_PIXELS[name]
+            if n_px:
+                out["frame_check"].update(oracle_rows_check(ctx, name, root, frame_np, row_counts, n_px))
     if not ctx.dist_on and not ctx.multi and K == 1:
         out["render_call_ms"] = render_latency(lib, rt580, params, torch)
     if cpu_baseline_on and ctx.n_gpus == 1 and not ctx.dist_on:
         gpu_px = frame_np.reshape(-1, 3) if frame_np is not None and frame_np.dtype == np.int16 else None
-        out["cpu_baseline"] = cpu_baseline(ctx, name, root, params, gpu_px)
+        out["cpu_baseline"] = cpu_baseline(ctx, name, root, params, gpu_px, row_counts)
     return out
+
+
+def oracle_rows_check(ctx, name, root, frame_np, row_counts, n_px):
+    """The last timed frame against the CPU restatement (oracle/, hoisted mode,
+    threaded) on CHECK_SEGMENTS pixel segments spread over the frame's rows
+    with geometry (stratified rows, staggered columns), n_px pixels in all.
+    Each segment row's RNG base is the GPU's exclusive scan of its per-row AO
+    calls; the oracle's own AO-call total of each of those rows must equal the
+    GPU's count. Covers the full-size launches (2^27-record AO chunks) that no
+    test reaches."""
+    import numpy as np
+    helpers = ctx.helpers
+    scene, _, W, H, depth, ao, _ = WORKLOADS[name]
+    counts = np.asarray(row_counts, dtype=np.int64)
+    base = np.cumsum(counts) - counts
+    nz = counts.nonzero()[0]
+    lo, hi = (int(nz[0]), int(nz[-1])) if len(nz) else (0, H - 1)
+    ns = min(CHECK_SEGMENTS, hi - lo + 1)
+    seg_n = min(W, -(-n_px // ns))
+    segs = []
+    for k in range(ns):
+        y = lo + (k * (hi - lo)) // max(ns - 1, 1)
+        x0 = (((k * 7) % ns) * (W - seg_n)) // max(ns - 1, 1)
+        segs.append((y, x0, seg_n))
+    t0 = time.perf_counter()
+    px, calls, cnt, secs = helpers.oracle_render_segments(scene, W, H, depth, ao, segs, [int(base[y]) for y, _, _ in segs],
+                                                          root=root)
+    bad_rows = [y for (y, x0, n), p in zip(segs, px) if not np.array_equal(p, frame_np[y, x0:x0 + n])]
+    bad_counts = [y for (y, _, _), c in zip(segs, calls) if c != int(counts[y])]
+    log("%s: frame check: %d pixels in %d segments against the oracle in %.1f s: %d rows differ, %d counts differ"
+        % (name, sum(n for _, _, n in segs), len(segs), time.perf_counter() - t0, len(bad_rows), len(bad_counts)))
+    return {"pixels_checked": int(sum(n for _, _, n in segs)), "segments": [list(s) for s in segs],
+            "matches_oracle_rows": not bad_rows and not bad_counts, "rows_differing": bad_rows,
+            "row_ao_calls_differing": bad_counts, "oracle_rays": cnt["rays_total"], "oracle_seconds": round(secs, 2),
+            "oracle": "oracle/rt_oracle.cpp oracle_render_segments (hoisted, %s threads); RNG base of each row "
+                      "from the GPU's exclusive scan of its per-row AO-call counts" % os.environ.get(
+                          "OMP_NUM_THREADS", os.cpu_count())}
 
 
 def frame_check(ctx, name, frame_np, single, W, H, check):
@@ -487,7 +539,7 @@ def cpu_model():
     return ""
 
 
-def cpu_baseline(ctx, name, root, params, gpu_px):
+def cpu_baseline(ctx, name, root, params, gpu_px, row_counts=None):
     """The repository's CPU restatement (oracle/) in ref-faithful mode (the
     reference's per-call work: string mesh lookup and ComputeModelMatrix per
     shape per IntersectScene call, the unused Matrix::Inverse + TransformPoint
@@ -503,8 +555,9 @@ def cpu_baseline(ctx, name, root, params, gpu_px):
     helpers, torch = ctx.helpers, ctx.torch
     scene, _, W, H, depth, ao, _ = WORKLOADS[name]
     # first row with an AO call, from the GPU's count pass (untimed)
-    rows = ctx.helpers.rt580_dist().GpuRows(ctx.rt580, params, torch, ctx.device)
-    counts = rows.count(0, 1)[:H].cpu().numpy()
+    if row_counts is None:
+        row_counts = ctx.helpers.rt580_dist().GpuRows(ctx.rt580, params, torch, ctx.device).count(0, 1)[:H].cpu().numpy()
+    counts = row_counts
     nz = counts.nonzero()[0]
     y0 = int(nz[0]) if len(nz) else 0
     p0 = y0 * W
@@ -530,8 +583,10 @@ def cpu_baseline(ctx, name, root, params, gpu_px):
         fbn, cntn, secsn = helpers.oracle_time_prefix(scene, W, H, depth, ao, p0, n, threads=threads, root=root,
                                                       faithful=True)
         res["all_cores"] = {"value": float("%.4g" % (cntn["rays_total"] / secsn / 1e6)), "cores": threads,
-                            "seconds": round(secsn, 3),
-                            "note": "same pixels; includes the count pass that splitting the serial RNG stream needs"}
+                            "host_cpus": os.cpu_count(), "seconds": round(secsn, 3),
+                            "note": "same pixels on $OMP_NUM_THREADS threads (the GPU pool's per-GPU CPU share; "
+                                    "host_cpus is the whole machine); includes the count pass that splitting the "
+                                    "serial RNG stream needs"}
         res["all_cores"]["matches_one_core"] = bool((fbn == fb1).all())
     res["matches_gpu_frame"] = parity
     cal = os.path.join(REPO, "profiles", "r03", "cpu_calibration.json")
@@ -567,6 +622,9 @@ def main():
                     help="the multi-rank path (torch.distributed + DistFrame) even with one rank: rehearses the "
                          "RCCL all-gather/gather and the per-frame host overhead of N>1 on one GPU")
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
+    ap.add_argument("--check-pixels", type=int, default=-1,
+                    help="pixels of the last timed frame checked against the oracle (16 segments over the "
+                         "geometry rows; -1: the workload's default, 0: none)")
     ap.add_argument("--row-sample", type=int, default=1,
                     help="N=1 only: time rows r = R mod K of the frame (rank R's exact share of a K-way "
                          "interleaved split; RNG bases from an untimed full-frame count), for huge frames and "
@@ -589,7 +647,7 @@ def main():
     ctx = Ctx(args)
     out = run_workload(ctx, args.workload, steps, warmup, not args.no_cpu_baseline, not args.no_check)
     if args.workload == "config2" and not args.no_north_star:
-        ns = run_workload(ctx, "field100k_1080p", 10, 3, not args.no_cpu_baseline, False)
+        ns = run_workload(ctx, "field100k_1080p", 10, 3, not args.no_cpu_baseline, not args.no_check)
         if out is not None:
             out["north_star"] = ns
     if out is not None:

@@ -19,6 +19,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <immintrin.h>
+
 // The oracle's own JSON reader (independent of the product's json_min.h).
 #include "ora_json.h"
 
@@ -31,7 +33,14 @@ static const float kOFFSET = (float)0.2;       // SHADOW_CLIPPING_OFFSET, Raytra
 // 0: hoisted (ray-invariant triangle data computed once per load; the default);
 // 1: ref-faithful cost model (oracle_set_mode; for the CPU baseline).
 static int g_faithful = 0;
-static volatile float g_sink;
+// per thread: a shared sink written per triangle test would bounce one cache line
+// between the CPU baseline's threads (ref-faithful mode)
+static thread_local volatile float g_sink;
+// 16-wide hoisted triangle scan where the CPU has AVX-512 (Tracer::scan_avx512;
+// $ORACLE_SCALAR=1: the scalar loop). Same bits either way.
+static const bool g_avx512 = __builtin_cpu_supports("avx512f") && !(std::getenv("ORACLE_SCALAR") && std::atoi(std::getenv("ORACLE_SCALAR")));
+// kEPS compared with a float (Raytracer.cpp:16-18 NearlyEquals, :376 t <= EPSILON)
+static const float kEPSf = (float)1e-6 < 1e-6 ? (float)1e-6 : std::nextafter((float)1e-6, 0.0f);
 
 // ---------------------------------------------------------------- Vector3 (Raytracer.h:39-149)
 struct V3 {
@@ -175,6 +184,12 @@ struct Mesh { int type = 0; std::vector<Tri> tris; float radius = 0; };  // valu
 // signed area, hit normal. Computed once with the same float operations, so
 // the hoisted test rounds exactly like the per-call one.
 struct WTri { V3 v0, v1, v2, N, hn; float D, area; };
+// The same values in structure-of-arrays form, padded to a multiple of 16
+// with N = 0 (nd = 0: rejected), for the 16-wide scan (scan_avx512).
+struct WTriSoA {
+    size_t n = 0;  // padded count
+    std::vector<float> v0x, v0y, v0z, v1x, v1y, v1z, v2x, v2y, v2z, nx, ny, nz, d, area;
+};
 struct Shape {
     Material mat;
     V3 S{1, 1, 1}, R, T;
@@ -182,6 +197,7 @@ struct Shape {
     std::string geo;  // geometryId (meshMap key, Raytracer.cpp:477)
     M4 model;
     std::vector<WTri> wtris;
+    WTriSoA soa;
 };
 struct Light { int type = -1; V3 color, position, direction; float intensity = 0; };
 enum { LDIR = 0, LPOINT = 1, LAMB = 2 };
@@ -243,6 +259,19 @@ static void hoist_triangles(Shape& s, const Mesh& m) {
         w.area = (float)(0.5 * V3::cross(ab, ac).dot(w.N));
         w.hn = w.N;
         w.hn.normalize();
+    }
+    WTriSoA& a = s.soa;
+    a.n = (s.wtris.size() + 15) / 16 * 16;
+    for (auto* v : {&a.v0x, &a.v0y, &a.v0z, &a.v1x, &a.v1y, &a.v1z, &a.v2x, &a.v2y, &a.v2z, &a.nx, &a.ny, &a.nz, &a.d,
+                    &a.area})
+        v->assign(a.n, 0.0f);
+    for (size_t i = 0; i < s.wtris.size(); i++) {
+        const WTri& w = s.wtris[i];
+        a.v0x[i] = w.v0.x; a.v0y[i] = w.v0.y; a.v0z[i] = w.v0.z;
+        a.v1x[i] = w.v1.x; a.v1y[i] = w.v1.y; a.v1z[i] = w.v1.z;
+        a.v2x[i] = w.v2.x; a.v2y[i] = w.v2.y; a.v2z[i] = w.v2.z;
+        a.nx[i] = w.N.x; a.ny[i] = w.N.y; a.nz[i] = w.N.z;
+        a.d[i] = w.D; a.area[i] = w.area;
     }
 }
 
@@ -481,29 +510,113 @@ struct Tracer {
         h.p = P; h.type = 0; h.n = w.hn; h.t = t; h.a = a; h.b = b; h.g = g;
         return true;
     }
-    // IntersectScene, Raytracer.cpp:473-526
-    bool intersect(const Ray& r, Hit& out) const {
+    // IntersectScene, Raytracer.cpp:473-526. any = true: only the boolean is
+    // wanted (AO samples :323, directional shadow rays :73), so the first hit
+    // decides; the closest-hit rule (first found, later ones only if strictly
+    // closer) is kept otherwise.
+    bool intersect(const Ray& r, Hit& out, bool any = false) const {
         if (g_faithful) return intersect_faithful(r, out);
         Hit best;
         bool found = false;
         for (const Shape& s : sc->shapes) {
             const Mesh& m = sc->meshes[s.mesh];
             if (m.type == 0) {
+                if (g_avx512) {
+                    if (scan_avx512(r, s, m, any, best, found) && any) return true;
+                    continue;
+                }
                 for (size_t i = 0; i < s.wtris.size(); i++) {
                     Hit h;
                     if (wtri_hit(r, s.wtris[i], h) && (!found || h.t < best.t)) {
                         found = true; best = h; best.tri = &m.tris[i]; best.mat = &s.mat;
+                        if (any) return true;
                     }
                 }
             } else {
                 Hit h;
                 if (sph_hit(r, m.radius, s.model, h) && (!found || h.t < best.t)) {
                     found = true; best = h; best.mat = &s.mat;
+                    if (any) return true;
                 }
             }
         }
         if (found) out = best;
         return found;
+    }
+    // The triangles of one shape, 16 at a time: the float operations of
+    // wtri_hit in the same order (no FMA: -ffp-contract=off holds for the
+    // intrinsics too), every lane's rejections as masks. Each accepted lane is
+    // then re-tested by wtri_hit itself in index order and combined with the
+    // scalar rule, so the Hit records are the scalar ones. kEPS is a double
+    // (Raytracer.h:12): for a float x, x < 1e-6 and x <= 1e-6 both equal
+    // x <= kEPSf, the largest float below 1e-6. Returns whether this shape
+    // had a hit (any: the first one ends the scan).
+    __attribute__((target("avx512f"))) static bool scan_avx512(const Ray& r, const Shape& s, const Mesh& m, bool any,
+                                                               Hit& best, bool& found) {
+        const WTriSoA& T = s.soa;
+        const __m512 ox = _mm512_set1_ps(r.o.x), oy = _mm512_set1_ps(r.o.y), oz = _mm512_set1_ps(r.o.z);
+        const __m512 dx = _mm512_set1_ps(r.d.x), dy = _mm512_set1_ps(r.d.y), dz = _mm512_set1_ps(r.d.z);
+        const __m512 eps = _mm512_set1_ps(kEPSf), zero = _mm512_setzero_ps(), half = _mm512_set1_ps(0.5f);
+        const __m512i absm = _mm512_set1_epi32(0x7fffffff), sgn = _mm512_set1_epi32((int)0x80000000u);
+#define ld(v, i) _mm512_loadu_ps((v).data() + (i))
+#define add _mm512_add_ps
+#define sub _mm512_sub_ps
+#define mul _mm512_mul_ps
+// CalcArea (Raytracer.cpp:937-942) of edges ab, ac against N, x 0.5
+#define area2(abx, aby, abz, acx, acy, acz, nx, ny, nz)                                                       \
+    mul(add(add(mul(sub(mul(aby, acz), mul(abz, acy)), nx), mul(sub(mul(abz, acx), mul(abx, acz)), ny)),       \
+            mul(sub(mul(abx, acy), mul(aby, acx)), nz)),                                                       \
+        half)
+        bool hit_here = false;
+        for (size_t i = 0; i < T.n; i += 16) {
+            const __m512 nx = ld(T.nx, i), ny = ld(T.ny, i), nz = ld(T.nz, i);
+            const __m512 nd = add(add(mul(nx, dx), mul(ny, dy)), mul(nz, dz));
+            __mmask16 ok = _mm512_cmp_ps_mask(_mm512_castsi512_ps(_mm512_and_si512(_mm512_castps_si512(nd), absm)), eps,
+                                              _CMP_NLE_UQ);  // !(|nd| < kEPS)
+            if (!ok) continue;
+            const __m512 no = add(add(mul(nx, ox), mul(ny, oy)), mul(nz, oz));
+            const __m512 num = _mm512_castsi512_ps(_mm512_xor_si512(_mm512_castps_si512(add(no, ld(T.d, i))), sgn));
+            const __m512 t = _mm512_div_ps(num, nd);
+            ok &= _mm512_cmp_ps_mask(t, eps, _CMP_NLE_UQ);  // !(t <= kEPS)
+            if (!ok) continue;
+            const __m512 px = add(ox, mul(dx, t)), py = add(oy, mul(dy, t)), pz = add(oz, mul(dz, t));
+            const __m512 v0x = ld(T.v0x, i), v0y = ld(T.v0y, i), v0z = ld(T.v0z, i);
+            const __m512 v1x = ld(T.v1x, i), v1y = ld(T.v1y, i), v1z = ld(T.v1z, i);
+            const __m512 v2x = ld(T.v2x, i), v2y = ld(T.v2y, i), v2z = ld(T.v2z, i);
+            const __m512 ar = ld(T.area, i);
+            const __m512 a = _mm512_div_ps(
+                area2(sub(v1x, px), sub(v1y, py), sub(v1z, pz), sub(v2x, px), sub(v2y, py), sub(v2z, pz), nx, ny, nz), ar);
+            ok &= _mm512_cmp_ps_mask(a, zero, _CMP_NLT_UQ);
+            if (!ok) continue;
+            const __m512 b = _mm512_div_ps(
+                area2(sub(px, v0x), sub(py, v0y), sub(pz, v0z), sub(v2x, v0x), sub(v2y, v0y), sub(v2z, v0z), nx, ny, nz),
+                ar);
+            ok &= _mm512_cmp_ps_mask(b, zero, _CMP_NLT_UQ);
+            if (!ok) continue;
+            const __m512 g = _mm512_div_ps(
+                area2(sub(v1x, v0x), sub(v1y, v0y), sub(v1z, v0z), sub(px, v0x), sub(py, v0y), sub(pz, v0z), nx, ny, nz),
+                ar);
+            ok &= _mm512_cmp_ps_mask(g, zero, _CMP_NLT_UQ);
+            for (unsigned mk = ok; mk; mk &= mk - 1) {
+                const size_t k = i + (size_t)__builtin_ctz(mk);
+                Hit h;
+                if (!wtri_hit(r, s.wtris[k], h)) {
+                    std::fprintf(stderr, "oracle: 16-wide triangle scan disagrees with wtri_hit\n");
+                    std::abort();
+                }
+                hit_here = true;
+                if (!found || h.t < best.t) {
+                    found = true; best = h; best.tri = &m.tris[k]; best.mat = &s.mat;
+                }
+                if (any) return true;
+            }
+        }
+        return hit_here;
+#undef ld
+#undef add
+#undef sub
+#undef mul
+#undef area2
     }
     // Ref-faithful mode (CPU-baseline timing only; same results): the work the
     // reference does per IntersectScene call as written — meshMap lookup by
@@ -553,7 +666,7 @@ struct Tracer {
             Ray ray(hp + v * kOFFSET, v);
             Hit h;
             c.ao++;
-            if (intersect(ray, h)) occ += 1.0f;
+            if (intersect(ray, h, true)) occ += 1.0f;
         }
         return 1.0f - ((float)occ / (float)ao_n);
     }
@@ -644,7 +757,8 @@ struct Tracer {
             c.shadow++;
             if (count_only) continue;
             Hit lh;
-            if (!intersect(lr, lh) || (lh.t > dist && l.type == LPOINT)) local = local + local_color(info, l, m);
+            if (!intersect(lr, lh, l.type == LDIR) || (lh.t > dist && l.type == LPOINT))
+                local = local + local_color(info, l, m);
         }
         if (bounces > 0) {
             float kr, kt;
@@ -944,6 +1058,103 @@ extern "C" int oracle_time_prefix(const char* assets_root, const char* scene, in
     *n_done = done;
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     if (counters) {
+        counters[0] = tot.primary + tot.secondary + tot.shadow + tot.ao;
+        counters[1] = tot.primary; counters[2] = tot.secondary; counters[3] = tot.shadow;
+        counters[4] = tot.ao; counters[5] = tot.ao_calls;
+    }
+    return 0;
+}
+
+// Frame check of a full-resolution GPU frame (bench.py): pixel segments
+// [x0, x0 + n) of rows y of the w x h frame, each row's first AO call at
+// row_base[k] (the GPU's exclusive scan of its per-row counts). A count pass
+// over each segment's whole row gives the in-row prefix of the segment's first
+// pixel and the row's AO-call total (-> row_calls[k], compared with the GPU's
+// count by the caller); then the segments' pixels are shaded. Work items are
+// pixels on `threads` threads. fb: sum(n) x 3 int16, segment after segment.
+extern "C" int oracle_render_segments(const char* assets_root, const char* scene, int w, int h, int depth,
+                                      int ao_samples, int threads, int n_seg, const int32_t* seg_y,
+                                      const int32_t* seg_x0, const int32_t* seg_n, const uint64_t* row_base,
+                                      int16_t* fb, uint64_t* row_calls, uint64_t* counters, double* seconds) {
+    if (w <= 0 || h <= 0 || depth < 0 || ao_samples <= 0 || threads < 1 || n_seg < 0 || !fb || !row_calls) return 2;
+    std::vector<int64_t> off((size_t)n_seg + 1, 0);
+    for (int k = 0; k < n_seg; k++) {
+        if (seg_y[k] < 0 || seg_y[k] >= h || seg_x0[k] < 0 || seg_n[k] < 0 || seg_x0[k] + seg_n[k] > w) return 2;
+        off[(size_t)k + 1] = off[(size_t)k] + seg_n[k];
+    }
+    Scene sc;
+    if (load_scene(sc, assets_root, scene) != 0) return 1;
+    for (const Shape& s : sc.shapes)
+        if (s.mesh < 0) return 1;
+    Camera2 cam = init_camera(sc, w, h);
+    Tracer tr;
+    tr.sc = &sc;
+    tr.depth = depth;
+    tr.ao_n = ao_samples;
+    tr.ao_on = 1;
+    tr.ao_bmax = (float)(2 * kPI);
+    tr.n_amb = 0;
+    for (auto& l : sc.lights) tr.n_amb += l.type == LAMB;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto run = [threads](const std::function<void()>& fn) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; t++) th.emplace_back(fn);
+        for (auto& t : th) t.join();
+    };
+    // count pass over every pixel of the segments' rows
+    std::vector<uint32_t> calls((size_t)n_seg * w);
+    {
+        std::atomic<int64_t> next{0};
+        const int64_t total = (int64_t)n_seg * w;
+        run([&] {
+            for (int64_t i; (i = next.fetch_add(1)) < total;) {
+                const int k = (int)(i / w), x = (int)(i % w);
+                Counters c;
+                tr.raycast(generate_ray(cam, x, seg_y[k]), depth, nullptr, c, true);
+                calls[(size_t)i] = (uint32_t)c.ao_calls;
+            }
+        });
+    }
+    std::vector<uint64_t> first((size_t)off[(size_t)n_seg]);  // each segment pixel's first AO call
+    for (int k = 0; k < n_seg; k++) {
+        uint64_t acc = row_base[k], tot = 0;
+        for (int x = 0; x < w; x++) {
+            if (x >= seg_x0[k] && x < seg_x0[k] + seg_n[k]) first[(size_t)(off[(size_t)k] + x - seg_x0[k])] = acc;
+            acc += calls[(size_t)k * w + x];
+            tot += calls[(size_t)k * w + x];
+        }
+        row_calls[k] = tot;
+    }
+    DrawSource src;
+    src.engine = 0;
+    const uint64_t per_call = 2ull * (uint64_t)ao_samples;
+    const int64_t npx = off[(size_t)n_seg];
+    std::vector<Counters> pc((size_t)npx);
+    {
+        std::atomic<int64_t> next{0};
+        run([&] {
+            RngCursor rng;
+            rng.src = &src;
+            for (int64_t i; (i = next.fetch_add(1)) < npx;) {
+                int k = 0;
+                while (off[(size_t)k + 1] <= i) k++;
+                const int x = seg_x0[k] + (int)(i - off[(size_t)k]);
+                rng.seek(first[(size_t)i] * per_call);
+                Counters& c = pc[(size_t)i];
+                c.primary++;
+                Pix p = tr.raycast(generate_ray(cam, x, seg_y[k]), depth, &rng, c, false);
+                int16_t* o = fb + (size_t)i * 3;
+                o[0] = p.r; o[1] = p.g; o[2] = p.b;
+            }
+        });
+    }
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (counters) {
+        Counters tot;
+        for (const Counters& c : pc) {
+            tot.primary += c.primary; tot.secondary += c.secondary; tot.shadow += c.shadow;
+            tot.ao += c.ao; tot.ao_calls += c.ao_calls;
+        }
         counters[0] = tot.primary + tot.secondary + tot.shadow + tot.ao;
         counters[1] = tot.primary; counters[2] = tot.secondary; counters[3] = tot.shadow;
         counters[4] = tot.ao; counters[5] = tot.ao_calls;

@@ -55,6 +55,15 @@ int oracle_time_prefix(const char* assets_root, const char* scene, int w, int h,
                        int threads, int64_t p0, int64_t max_pixels, double budget_s, uint64_t call_base,
                        int16_t* fb, uint64_t* counters, int64_t* n_done, double* seconds);
 
+// Frame check of a full-resolution GPU frame: segments [seg_x0[k], seg_x0[k] +
+// seg_n[k]) of rows seg_y[k], row k's first AO call at row_base[k] (absolute
+// index, minstd_rand0). row_calls[k] <- the AO calls of the whole row seg_y[k].
+// fb: sum(seg_n) x 3 int16; counters as oracle_render (segment pixels only).
+int oracle_render_segments(const char* assets_root, const char* scene, int w, int h, int depth, int ao_samples,
+                           int threads, int n_seg, const int32_t* seg_y, const int32_t* seg_x0,
+                           const int32_t* seg_n, const uint64_t* row_base, int16_t* fb, uint64_t* row_calls,
+                           uint64_t* counters, double* seconds);
+
 // 0 = hoisted (default), 1 = ref-faithful cost model (see above). Process-global.
 int oracle_set_mode(int faithful);
 

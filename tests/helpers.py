@@ -175,6 +175,38 @@ def oracle_time_prefix(scene, w, h, depth, ao_samples, p0, max_pixels, budget_s=
     return fb[:done.value], dict(zip(keys, (int(x) for x in cnt))), secs.value
 
 
+def oracle_render_segments(scene, w, h, depth, ao_samples, segments, row_base, threads=0, root=ASSETS_ROOT):
+    """Pixels of a full w x h frame at segments [(y, x0, n), ...] (hoisted mode,
+    threaded), row y's first AO call at row_base[k] -> (list of int16 (n, 3)
+    arrays, the AO calls of each segment's whole row, counters, seconds)."""
+    lib = oracle_lib()
+    f = lib.oracle_render_segments
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p] * 7 + \
+        [ctypes.POINTER(ctypes.c_double)]
+    if threads <= 0:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    ys = np.array([s[0] for s in segments], dtype=np.int32)
+    x0 = np.array([s[1] for s in segments], dtype=np.int32)
+    ns = np.array([s[2] for s in segments], dtype=np.int32)
+    base = np.ascontiguousarray(np.asarray(row_base, dtype=np.uint64))
+    fb = np.zeros((int(ns.sum()), 3), dtype=np.int16)
+    calls = np.zeros(len(segments), dtype=np.uint64)
+    cnt = np.zeros(6, dtype=np.uint64)
+    secs = ctypes.c_double(0)
+    lib.oracle_set_mode(0)
+    st = f(os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples, threads, len(segments), ys.ctypes.data,
+           x0.ctypes.data, ns.ctypes.data, base.ctypes.data, fb.ctypes.data, calls.ctypes.data, cnt.ctypes.data,
+           ctypes.byref(secs))
+    assert st == 0, "oracle_render_segments failed"
+    out, o = [], 0
+    for n in ns:
+        out.append(fb[o:o + n])
+        o += n
+    keys = ["rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls"]
+    return out, [int(c) for c in calls], dict(zip(keys, (int(x) for x in cnt))), secs.value
+
+
 @functools.lru_cache(None)
 def rt580_dist():
     spec = importlib.util.spec_from_file_location("rt580_dist", os.path.join(PKG, "rt580_dist.py"))

@@ -93,3 +93,47 @@ def test_time_prefix_is_the_frames_pixels(p0, n):
     # the serial timer stops at its budget
     fb, cnt, _ = helpers.oracle_time_prefix("simpleSphereScene.json", w, h, d, ao, 0, w * h, budget_s=0.0)
     assert len(fb) == 1 and cnt["rays_primary"] == 1
+
+
+@pytest.mark.parametrize("scene,root_name,w,h,d,ao", [
+    ("simpleSphereScene.json", None, 40, 30, 4, 8),
+    ("cornell10k.json", "cornell10k", 24, 14, 3, 4),
+])
+def test_render_segments_are_the_frames_pixels(scene, root_name, w, h, d, ao):
+    """bench.py's frame check (oracle_render_segments: pixel segments of rows of
+    the full frame, each row's RNG base given, threaded) gives exactly the
+    frame's pixels, and each row's AO-call total."""
+    root = helpers.synthetic_root(root_name) if root_name else helpers.ASSETS_ROOT
+    full, _ = helpers.oracle_render(scene, w, h, d, ao, True, root=root)
+    calls = [helpers.oracle_render(scene, w, h, d, ao, True, rows=(y, y + 1), root=root)[1]["ao_calls"]
+             for y in range(h)]
+    base = np.concatenate([[0], np.cumsum(calls)[:-1]]).astype(np.uint64)
+    segs = [(h // 2, 0, w), (h - 1, 3, w - 5), (h // 3, w // 2, w - w // 2), (h // 2 + 1, 1, 1)]
+    got, row_calls, cnt, _ = helpers.oracle_render_segments(scene, w, h, d, ao, segs, [base[y] for y, _, _ in segs],
+                                                            threads=4, root=root)
+    for (y, x0, n), px in zip(segs, got):
+        assert np.array_equal(px, full[y, x0:x0 + n]), (y, x0, n)
+    assert row_calls == [calls[y] for y, _, _ in segs]
+    assert cnt["rays_primary"] == sum(n for _, _, n in segs)
+
+
+def test_simd_triangle_scan_matches_scalar_loop():
+    """The 16-wide hoisted triangle scan (AVX-512, used when the CPU has it)
+    and the scalar loop give the same frame and rays (ORACLE_SCALAR=1 in a
+    child process selects the scalar loop)."""
+    import json
+    import sys
+    root = helpers.synthetic_root("cornell10k")
+    code = ("import sys, json; sys.path.insert(0, %r); import helpers; "
+            "fb, c = helpers.oracle_render('cornell10k.json', 32, 18, 4, 8, True, root=%r); "
+            "print(json.dumps([helpers.sha256(fb.tobytes()), c]))" % (os.path.join(helpers.REPO, "tests"), root))
+    outs = []
+    for scalar in ("0", "1"):
+        env = dict(os.environ)
+        env.pop("ORACLE_SCALAR", None)
+        if scalar == "1":
+            env["ORACLE_SCALAR"] = "1"
+        p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=600)
+        assert p.returncode == 0, p.stderr
+        outs.append(json.loads(p.stdout.strip().splitlines()[-1]))
+    assert outs[0] == outs[1]
