@@ -32,7 +32,8 @@ class Raytracer {
     int SetRngEngine(int engine);                    // Raytracer.h:592 (minstd_rand0)
     int SetRows(int row_begin, int row_end, int row_step = 1);
     int SetWriteOutput(bool on) { mWriteOutput = on; return RT_SUCCESS; }
-    // GPUs Render() shards a whole frame across (0: $RT580_GPUS, else every visible device).
+    // GPUs Render() shards a whole frame across (0: $RT580_GPUS if set, else 1 -- the
+    // device of rt_gpu_init, so one process per GPU stays one GPU per process).
     int SetGpuCount(int n) {
         if (n < 0 || n > 16) return RT_INVALID_ARG;
         mGpus = n;

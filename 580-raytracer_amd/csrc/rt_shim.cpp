@@ -721,6 +721,13 @@ int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global
         for (int i = 0; i < n_rows; i++) total = std::max(total, base[i] + calls[i]);
     }
     const uint64_t n = total * 2ull * (uint64_t)p->ao_samples;
+    // the whole stream lives on the host and the device: bounded (8 GiB each)
+    // until the engine has a block jump-ahead
+    constexpr uint64_t kMtMaxDraws = 1ull << 31;
+    if (n > kMtMaxDraws)
+        return fail("mt19937: these rows need %llu serial draws, above the %llu this build generates (use "
+                    "minstd_rand0, or fewer rows per call)",
+                    (unsigned long long)n, (unsigned long long)kMtMaxDraws);
     if (ensure(SL.mt_stream, n * 4 + 8)) return RT_FAILURE;
     std::vector<uint32_t> host(n);
     std::mt19937 gen(p->rng_seed);

@@ -204,3 +204,29 @@ def test_replay_count_mismatch_fails_the_frame(tmp_path):
     assert line, r.stdout + r.stderr
     assert line[0].startswith("CODES [0, 1, 0, 1]"), line[0]
     assert "replayed count schedule" in line[0], line[0]
+
+
+def test_accel_toggle_on_repeated_frame_keeps_rendering():
+    """The same params on a resident BVH scene, rendered (verified, recorded),
+    then again (replayed), then under RT_ACCEL_BRUTE and back under AUTO: the
+    recorded count schedules belong to the acceleration mode (rt_shim.cpp
+    SchedKey.accel), so no toggle makes a frame fail, and every frame equals
+    the oracle's."""
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    root = helpers.synthetic_root("cornell10k")
+    w, h, depth, ao = 40, 24, 3, 8
+    rt, params = _params("cornell10k.json", w, h, depth, ao, root)
+    s = rt.scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    ref, _ = helpers.oracle_render("cornell10k.json", w, h, depth, ao, True, root=root)
+    host = np.zeros(w * h * 3, dtype=np.int16)
+    try:
+        for mode in (1, 1, 0, 0, 1, 1, 0, 1):
+            assert lib.rt_gpu_set_accel(mode) == 0
+            rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "render (accel %d)" % mode)
+            assert lib.rt_gpu_accel_active() == mode
+            assert np.array_equal(host.reshape(h, w, 3), ref), "accel %d" % mode
+    finally:
+        lib.rt_gpu_set_accel(1)
+    rt.close()

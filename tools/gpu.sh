@@ -12,6 +12,8 @@
 #                                   --row-sample K --row-rank r), K in KS (default "1 2 4 8")
 #   profile TAG [bench.py args]     rocprofv3 kernel trace + one PMC pass per counter group,
 #                                   roofline + per-kernel summaries -> gpurun_out/prof_TAG/
+#   trace TAG [bench.py args]       kernel trace only (per-dispatch CSV kept): GPU busy/idle and
+#                                   per-kernel time of the last frames -> gpurun_out/trace_TAG/
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -115,8 +117,19 @@ GROUPS
   rm -f $OUT/pmc*_counter_collection.csv $OUT/trace_kernel_trace.csv
   ls $OUT
   ;;
+trace)
+  TAG=$1; shift
+  OUT=gpurun_out/trace_$TAG
+  mkdir -p $OUT
+  BENCH="python3 bench.py --no-cpu-baseline --no-north-star --no-check $*"
+  case "$*" in *--steps*) ;; *) BENCH="$BENCH --steps 6 --warmup 3";; esac
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o trace -- $BENCH > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 1; }
+  python3 tools/trace_gaps.py $OUT/trace_kernel_trace.csv 4 > $OUT/gaps.txt && head -25 $OUT/gaps.txt
+  python3 tools/frame_timeline.py $OUT/trace_kernel_trace.csv --frames 1 > $OUT/timeline.txt
+  gzip -f $OUT/trace_kernel_trace.csv
+  ;;
 *)
-  sed -n '2,16p' "$0"
+  sed -n '2,18p' "$0"
   exit 2
   ;;
 esac

@@ -4,8 +4,8 @@ directory, for bench.py's roofline block.
 
 Reads the kernel stats + PMC passes (summarize_profile.summarize) and the bench
 JSON line of the trace pass (trace.log: AO rays per launch, measured live in
-that run), and writes profiles/$RT580_PROFILE_ROUND/roofline_<workload>.json
-(default r03) and prints it:
+that run), and writes profiles/$PROFILE_ROUND/roofline_<workload>.json
+(default r04) and prints it:
   kernel, avg_ms               the AO ray kernel (ao_kernel* / ao_near_kernel* / ao_trace_kernel*)
   valu_per_ao_ray              SQ_INSTS_VALU per dispatch / AO rays per dispatch
   hbm_bytes_per_ao_ray         (FETCH_SIZE + WRITE_SIZE) x 1 KiB per dispatch / AO rays
@@ -78,7 +78,7 @@ def main():
         "top_kernels": [[n, round(v["total_ns"] / total, 4)] for n, v in top],
         "peaks": summ["peaks"],
     }
-    dst = os.path.join(REPO, "profiles", os.environ.get("RT580_PROFILE_ROUND", "r03"), "roofline_%s.json" % workload)
+    dst = os.path.join(REPO, "profiles", os.environ.get("PROFILE_ROUND", "r04"), "roofline_%s.json" % workload)
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))

@@ -17,7 +17,7 @@ Per kernel (template instantiations kept apart):
 Peaks (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs, one wave64 VALU instruction
 per SIMD every 2 cycles at 2.4 GHz = 1.2288e12 wave-instructions/s; HBM 8 TB/s.
 
-With RT580_PROFILE_AFTER=<kernel> (e.g. row_scan_kernel): only the dispatches
+With PROFILE_AFTER=<kernel> (e.g. row_scan_kernel): only the dispatches
 after the first dispatch of that kernel -- bench.py --row-sample's untimed
 full-frame count pass comes first, so the summary is the timed frames'. The
 kernel statistics then come from the per-dispatch trace (trace_kernel_trace.csv)
@@ -67,7 +67,7 @@ def after_marker(rows, name_key, order_key, marker):
 
 
 def summarize(d):
-    marker = os.environ.get("RT580_PROFILE_AFTER", "")
+    marker = os.environ.get("PROFILE_AFTER", "")
     stats = collections.defaultdict(lambda: {"calls": 0, "total_ns": 0.0, "pct": 0.0})
     if marker:
         tr = after_marker(list(csv.DictReader(open(os.path.join(d, "trace_kernel_trace.csv")))), "Kernel_Name",
