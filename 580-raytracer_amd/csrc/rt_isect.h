@@ -745,7 +745,8 @@ RTM_HD bool bvh4_any_near(const BvhView& V, rv3 o, rv3 d, float tmax = INFINITY)
 // its entry t is above the best t, and a primitive hit at the best t with a
 // lower index lies in a box entered at or before that t. Stack entries carry
 // their entry t for that pruning at pop time.
-RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
+template <class STK, class TSTK>
+RTM_HD bool bvh4_closest_near_s(const BvhView& V, rv3 o, rv3 d, Hit& h, const STK& stk, const TSTK& tstk) {
     bool found = false;
     h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
     RT_CNT(brute_tests, V.n_brute);
@@ -759,8 +760,6 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
     }
     if (!V.has_tree || dir_zero(d)) return found;
     const SlabRay sr = slab_ray(V, o, d);
-    uint32_t stk[RT_BVH_STACK + 4];
-    float tstk[RT_BVH_STACK + 4];
     int sp = 0;
     int32_t c = 0, n = 0;  // root (internal)
     for (;;) {
@@ -783,8 +782,8 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
                 }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                stk[sp] = nd.link[j];
-                tstk[sp] = t[j];
+                stk.put(sp, nd.link[j]);
+                tstk.put(sp, rt_f32_bits(t[j]));
                 sp += (ok[j] & (j != best)) ? 1 : 0;
             }
             if (best >= 0) {
@@ -796,9 +795,10 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
             have = false;
             while (sp > 0) {
                 sp--;
-                if (found && tstk[sp] > h.t) continue;
-                c = (int32_t)(stk[sp] & 0x7ffffffu);
-                n = (int32_t)(stk[sp] >> 27);
+                if (found && rt_bits_f32(tstk.get(sp)) > h.t) continue;
+                const uint32_t e = stk.get(sp);
+                c = (int32_t)(e & 0x7ffffffu);
+                n = (int32_t)(e >> 27);
                 have = true;
                 break;
             }
@@ -820,14 +820,20 @@ RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
         have = false;
         while (sp > 0) {
             sp--;
-            if (found && tstk[sp] > h.t) continue;
-            c = (int32_t)(stk[sp] & 0x7ffffffu);
-            n = (int32_t)(stk[sp] >> 27);
+            if (found && rt_bits_f32(tstk.get(sp)) > h.t) continue;
+            const uint32_t e = stk.get(sp);
+            c = (int32_t)(e & 0x7ffffffu);
+            n = (int32_t)(e >> 27);
             have = true;
             break;
         }
         if (!have) return found;
     }
+}
+
+RTM_HD bool bvh4_closest_near(const BvhView& V, rv3 o, rv3 d, Hit& h) {
+    uint32_t stk_a[RT_BVH_STACK + 4], tstk_a[RT_BVH_STACK + 4];
+    return bvh4_closest_near_s(V, o, d, h, ArrStack{stk_a}, ArrStack{tstk_a});
 }
 
 // The near closest-hit query: 4-wide tree when present, else the binary one.

@@ -45,6 +45,7 @@ namespace rt580 {
 
 #define TB 256    // threads per workgroup (4 waves)
 #define TILE 64   // primitives per LDS tile (4 KiB)
+#define NEAR_LDS 16  // traversal-stack entries per lane in LDS (trace_kernel's near phases)
 #define LVL_BASE (RT_MAX_DEPTH + 2)
 
 // ---------------------------------------------------------------- RNG
@@ -525,6 +526,12 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                                                    uint32_t i1, int light = 0, int dl = 0, int wave_near = 0) {
     __shared__ rt_prim tile[TILE];
     __shared__ WaveEntry wstk[PHASE == 3 ? TB / 64 : 1][RT_WAVE_STACK];
+    // the near queries' traversal stacks (4-wide tree): the first NEAR_LDS
+    // entries of each lane in LDS, one column per lane (PHASE 1: node links
+    // and entry distances; PHASE 3: node links), the rest in scratch
+    constexpr int NL = (BVH && (PHASE == 1 || PHASE == 3)) ? NEAR_LDS : 1;
+    __shared__ uint32_t nstk[NL][TB];
+    __shared__ uint32_t ntstk[PHASE == 1 && BVH ? NEAR_LDS : 1][TB];
     const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
     const uint32_t base_id = level == 0 ? 0u : W.lvl[LVL_BASE + level];
     // Children beyond the node capacity were not stored (the frame is re-rendered
@@ -561,7 +568,16 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
         if (PHASE == 1) {
             const FarNode root = load_far_node(S.bv.far_nodes, 0);
             const bool brute = active && far_origin(S, o);
-            const bool nh = active && !brute && bvh_closest_near(S.bv, o, d, h);
+            bool nh = false;
+            if (active && !brute) {
+                if (S.bv.nodes4) {
+                    uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS], ta[RT_BVH_STACK + 4 - NEAR_LDS];
+                    nh = bvh4_closest_near_s(S.bv, o, d, h, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa},
+                                             LdsStack<NEAR_LDS, TB>{&ntstk[0][threadIdx.x], ta});
+                } else {
+                    nh = bvh_closest_near(S.bv, o, d, h);
+                }
+            }
             bool q = false;
             if (active) {
                 W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
@@ -621,9 +637,15 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             }
             // per lane, or (wave_near, A/B) one wave-cooperative near traversal:
             // neighbouring pixels' shadow rays share a directional light's direction
-            const bool nh = (wave_near && isinf(tmax))
-                                ? bvh_any_near_wave(S.bv, lit && !brute, so, L2, wstk[threadIdx.x >> 6])
-                                : (lit && !brute && bvh_any_near(S.bv, so, L2, tmax));
+            bool nh;
+            if (wave_near && isinf(tmax)) {
+                nh = bvh_any_near_wave(S.bv, lit && !brute, so, L2, wstk[threadIdx.x >> 6]);
+            } else if (S.bv.nodes4) {
+                uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS];
+                nh = lit && !brute && bvh4_any_near_s(S.bv, so, L2, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa}, tmax);
+            } else {
+                nh = lit && !brute && bvh_any_near(S.bv, so, L2, tmax);
+            }
             if (nh) flag = 1;
             else q = lit && (brute || (!dir_zero(L2) && isinf(tmax)));
             if (active) W.shadow[(size_t)dl * W.far_cap + (item - i0)] = flag;

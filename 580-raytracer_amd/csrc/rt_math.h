@@ -32,6 +32,17 @@ RTM_HD float rt_bits_f32(uint32_t u) {
 #endif
 }
 
+// The bits of this float.
+RTM_HD uint32_t rt_f32_bits(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __float_as_uint(f);
+#else
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    return u;
+#endif
+}
+
 RTM_HD rv3 v3(float x, float y, float z) { rv3 r; r.x = x; r.y = y; r.z = z; return r; }
 RTM_HD rv3 v3_add(rv3 a, rv3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 RTM_HD rv3 v3_sub(rv3 a, rv3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
