@@ -108,7 +108,8 @@ int Raytracer::Render(const std::string outputName) {
     // The framebuffer lives as long as this instance: page-lock it once, so
     // every frame lands in it with one DMA (no staging copy)
     if (whole && !mFbRegistered && !mFrameBuffer.empty())
-        mFbRegistered = rt_gpu_host_register(mFrameBuffer.data(), mFrameBuffer.size() * sizeof(Pixel)) == RT_SUCCESS;
+        mFbRegistered = rt_gpu_host_register(mFrameBuffer.data(),
+                                             (mFrameBuffer.size() * sizeof(Pixel) + 4095) / 4096 * 4096) == RT_SUCCESS;
     // Whole frames can shard across the node's GPUs (interleaved rows, RCCL
     // exchange + gather, rt_gpu_render_multi) when SetGpuCount or $RT580_GPUS
     // asks for more than one; the default is the one device of rt_gpu_init

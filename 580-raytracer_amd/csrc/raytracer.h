@@ -5,11 +5,36 @@
 // per-pixel path on the GPU through the rt_gpu_* C ABI (include/rt580.h).
 #pragma once
 #include <cstdint>
+#include <cstdlib>
+#include <new>
 #include <string>
 #include <vector>
 
 #include "../../include/rt580.h"
 #include "rt_scene.h"
+
+// Page-aligned storage rounded up to whole pages: the framebuffer is
+// page-locked for DMA (rt_gpu_host_register), and a registration must not
+// share a page with other allocations (they would be page-locked with it, and
+// a later registration of a neighbour would overlap it).
+template <class T>
+struct PageAlloc {
+    using value_type = T;
+    PageAlloc() = default;
+    template <class U>
+    PageAlloc(const PageAlloc<U>&) {}
+    T* allocate(size_t n) {
+        const size_t bytes = (n * sizeof(T) + 4095) / 4096 * 4096;
+        void* p = nullptr;
+        if (posix_memalign(&p, 4096, bytes ? bytes : 4096) != 0) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) { std::free(p); }
+    template <class U>
+    bool operator==(const PageAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const PageAlloc<U>&) const { return false; }
+};
 
 class Raytracer {
   public:
@@ -49,7 +74,7 @@ class Raytracer {
     int mWidth, mHeight;
     float mFov = 60.0f;  // Raytracer.cpp:786
     std::string mAssetsRoot = ".";
-    std::vector<Pixel> mFrameBuffer;
+    std::vector<Pixel, PageAlloc<Pixel>> mFrameBuffer;
     rt580::Scene mScene;
     rt580::PackedScene mPacked;
     bool mSceneValid = false;

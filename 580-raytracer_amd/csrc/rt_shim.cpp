@@ -104,6 +104,11 @@ struct State {
     int16_t* stage = nullptr;
     size_t stage_bytes = 0;
     std::array<hipEvent_t, 16> stage_ev{};
+    // every other host <-> device copy of pageable memory: two halves of a
+    // pinned buffer (copy_h2d / copy_d2h), so the runtime never pins or maps
+    // caller memory on the fly
+    uint8_t* xfer = nullptr;
+    hipEvent_t xfer_ev[2] = {};
     bool pipeline = true;      // RT580_PIPELINE=0: every frame on the caller's stream
     // rt_gpu_render's latency path: a second stream for the first part's
     // resolve + copy, and the hand-off events
@@ -387,15 +392,105 @@ DevScene dev_scene(const rt_render_params* p) {
 // Scene uploads are synchronous: every copy has completed (and any device
 // error it met is reported, naming the array) before the call returns or the
 // host array is freed.
-int h2d(void* dst, const void* src, size_t bytes, const char* what) {
-    if (!bytes) return RT_SUCCESS;
-    const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g.stream);
-    if (e != hipSuccess)
-        return fail("copy of %s (%zu bytes) to the device (device work enqueued up to %s): %s", what, bytes,
-                    g_last_work, hipGetErrorString(e));
-    char w[96];
-    std::snprintf(w, sizeof w, "by the copy of %s", what);
-    return stream_sync(g.stream, w);
+int copy_h2d(void* dst, const void* src, size_t n, hipStream_t s, const char* what);
+int h2d(void* dst, const void* src, size_t bytes, const char* what) { return copy_h2d(dst, src, bytes, g.stream, what); }
+
+// Host ranges page-locked by rt_gpu_host_register (process-wide).
+struct HostRange {
+    const char* p;
+    size_t bytes;
+};
+std::vector<HostRange> g_host_ranges;
+
+bool host_registered(const void* p, size_t bytes) {
+    const char* c = (const char*)p;
+    for (const HostRange& r : g_host_ranges)
+        if (c >= r.p && c + bytes <= r.p + r.bytes) return true;
+    return false;
+}
+
+// Host <-> device copies of caller or library host memory that is not page
+// locked go through the context's pinned transfer buffer (two halves, one
+// chunk in flight while the other is filled or drained). The HIP runtime
+// otherwise pins pageable memory on the fly for large copies and keeps those
+// pins; a later allocation at a reused virtual address could then be read
+// through a stale mapping -- the device fault the round-3 GPU suite met in a
+// scene upload. Both return once the copy is complete.
+constexpr size_t kXferHalf = (size_t)8 << 20;
+
+int xfer_ready() {
+    if (g.xfer) return RT_SUCCESS;
+    HIP_TRY(hipHostMalloc((void**)&g.xfer, 2 * kXferHalf, hipHostMallocDefault));
+    for (auto& e : g.xfer_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return RT_SUCCESS;
+}
+
+int copy_h2d(void* dst, const void* src, size_t n, hipStream_t s, const char* what) {
+    if (!n) return RT_SUCCESS;
+    char w[128];
+    std::snprintf(w, sizeof w, "by the copy of %s to the device", what);
+    if (host_registered(src, n)) {
+        HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s));
+        return stream_sync(s, w);
+    }
+    if (xfer_ready()) return RT_FAILURE;
+    bool used[2] = {false, false};
+    int h = 0;
+    for (size_t off = 0; off < n; off += kXferHalf, h ^= 1) {
+        const size_t c = n - off < kXferHalf ? n - off : kXferHalf;
+        if (used[h]) {  // this half's previous chunk has left
+            const hipError_t e = hipEventSynchronize(g.xfer_ev[h]);
+            if (e != hipSuccess)
+                return fail("device error seen %s (raised by device work enqueued up to %s): %s", w, g_last_work,
+                            hipGetErrorString(e));
+        }
+        uint8_t* b = g.xfer + (size_t)h * kXferHalf;
+        std::memcpy(b, (const char*)src + off, c);
+        const hipError_t e = hipMemcpyAsync((char*)dst + off, b, c, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess)
+            return fail("copy of %s (%zu bytes) to the device (device work enqueued up to %s): %s", what, n,
+                        g_last_work, hipGetErrorString(e));
+        HIP_TRY(hipEventRecord(g.xfer_ev[h], s));
+        used[h] = true;
+    }
+    return stream_sync(s, w);
+}
+
+int copy_d2h(void* dst, const void* src, size_t n, hipStream_t s, const char* what) {
+    if (!n) return RT_SUCCESS;
+    char w[128];
+    std::snprintf(w, sizeof w, "by the copy of %s to the host", what);
+    if (host_registered(dst, n)) {
+        HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s));
+        return stream_sync(s, w);
+    }
+    if (xfer_ready()) return RT_FAILURE;
+    size_t pend_off[2] = {0, 0}, pend_n[2] = {0, 0};
+    int h = 0;
+    auto drain = [&](int k) -> int {
+        if (!pend_n[k]) return RT_SUCCESS;
+        const hipError_t e = hipEventSynchronize(g.xfer_ev[k]);
+        if (e != hipSuccess)
+            return fail("device error seen %s (raised by device work enqueued up to %s): %s", w, g_last_work,
+                        hipGetErrorString(e));
+        std::memcpy((char*)dst + pend_off[k], g.xfer + (size_t)k * kXferHalf, pend_n[k]);
+        pend_n[k] = 0;
+        return RT_SUCCESS;
+    };
+    for (size_t off = 0; off < n; off += kXferHalf, h ^= 1) {
+        const size_t c = n - off < kXferHalf ? n - off : kXferHalf;
+        if (drain(h)) return RT_FAILURE;
+        const hipError_t e = hipMemcpyAsync(g.xfer + (size_t)h * kXferHalf, (const char*)src + off, c,
+                                            hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess)
+            return fail("copy of %s (%zu bytes) to the host (device work enqueued up to %s): %s", what, n, g_last_work,
+                        hipGetErrorString(e));
+        HIP_TRY(hipEventRecord(g.xfer_ev[h], s));
+        pend_off[h] = off;
+        pend_n[h] = c;
+    }
+    if (drain(h) || drain(h ^ 1)) return RT_FAILURE;
+    return RT_SUCCESS;
 }
 
 template <typename T>
@@ -710,31 +805,39 @@ int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global
     if (p->rng_engine != RT_RNG_MT19937 || !p->ao_enabled || g.n_ambient == 0) return RT_SUCCESS;
     uint64_t total = 0;
     if (!row_base_global) {
-        HIP_TRY(hipMemcpyAsync(&total, SL.totals.p, 8, hipMemcpyDeviceToHost, fs()));
-        HIP_TRY(hipStreamSynchronize(fs()));
+        if (copy_d2h(&total, SL.totals.p, 8, fs(), "the AO-call total")) return RT_FAILURE;
     } else if (n_rows > 0) {
         std::vector<uint64_t> base((size_t)n_rows);
         std::vector<uint32_t> calls((size_t)n_rows);
-        HIP_TRY(hipMemcpyAsync(base.data(), row_base_global, (size_t)n_rows * 8, hipMemcpyDeviceToHost, fs()));
-        HIP_TRY(hipMemcpyAsync(calls.data(), SL.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToHost, fs()));
-        HIP_TRY(hipStreamSynchronize(fs()));
+        if (copy_d2h(base.data(), row_base_global, (size_t)n_rows * 8, fs(), "the row bases") ||
+            copy_d2h(calls.data(), SL.row_calls.p, (size_t)n_rows * 4, fs(), "the per-row AO calls"))
+            return RT_FAILURE;
         for (int i = 0; i < n_rows; i++) total = std::max(total, base[i] + calls[i]);
     }
     const uint64_t n = total * 2ull * (uint64_t)p->ao_samples;
-    // the whole stream lives on the host and the device: bounded (8 GiB each)
-    // until the engine has a block jump-ahead
-    constexpr uint64_t kMtMaxDraws = 1ull << 31;
+    // the stream is generated serially and lives on the device whole: bounded
+    // (16 GiB) until the engine has a block jump-ahead
+    constexpr uint64_t kMtMaxDraws = 1ull << 32;
     if (n > kMtMaxDraws)
         return fail("mt19937: these rows need %llu serial draws, above the %llu this build generates (use "
                     "minstd_rand0, or fewer rows per call)",
                     (unsigned long long)n, (unsigned long long)kMtMaxDraws);
-    if (ensure(SL.mt_stream, n * 4 + 8)) return RT_FAILURE;
-    std::vector<uint32_t> host(n);
+    if (ensure(SL.mt_stream, n * 4 + 8) || xfer_ready()) return RT_FAILURE;
+    // generated straight into the pinned transfer buffer, chunk by chunk
     std::mt19937 gen(p->rng_seed);
-    for (uint64_t i = 0; i < n; i++) host[i] = (uint32_t)gen();
-    if (n) HIP_TRY(hipMemcpyAsync(SL.mt_stream.p, host.data(), n * 4, hipMemcpyHostToDevice, fs()));
-    HIP_TRY(hipStreamSynchronize(fs()));
-    return RT_SUCCESS;
+    const size_t per = kXferHalf / 4;
+    bool used[2] = {false, false};
+    int h = 0;
+    for (uint64_t off = 0; off < n; off += per, h ^= 1) {
+        const size_t c = n - off < per ? (size_t)(n - off) : per;
+        if (used[h]) HIP_TRY(hipEventSynchronize(g.xfer_ev[h]));
+        uint32_t* b = reinterpret_cast<uint32_t*>(g.xfer + (size_t)h * kXferHalf);
+        for (size_t i = 0; i < c; i++) b[i] = (uint32_t)gen();
+        HIP_TRY(hipMemcpyAsync((uint32_t*)SL.mt_stream.p + off, b, c * 4, hipMemcpyHostToDevice, fs()));
+        HIP_TRY(hipEventRecord(g.xfer_ev[h], fs()));
+        used[h] = true;
+    }
+    return stream_sync(fs(), "by the upload of the mt19937 stream");
 }
 
 // AO phases in frame order (RT580_AO_ORDER=1, rt580_set_ao_order): a frame's
@@ -1078,19 +1181,6 @@ int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     return fail("node capacity could not be sized");
 }
 
-// Host ranges page-locked by rt_gpu_host_register (process-wide).
-struct HostRange {
-    const char* p;
-    size_t bytes;
-};
-static std::vector<HostRange> g_host_ranges;
-
-static bool host_registered(const void* p, size_t bytes) {
-    const char* c = (const char*)p;
-    for (const HostRange& r : g_host_ranges)
-        if (c >= r.p && c + bytes <= r.p + r.bytes) return true;
-    return false;
-}
 
 // The framebuffer to the caller's memory: one DMA into a registered range;
 // else device -> pinned staging in up to 16 chunks, each chunk's host copy
@@ -1174,8 +1264,7 @@ static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) 
     // once per (params, scene) -- they do not change between calls.
     if (!(g.lat_gen == g.scene_gen && std::memcmp(&g.lat_params, p, sizeof *p) == 0)) {
         std::vector<uint32_t> rc((size_t)H);
-        HIP_TRY(hipMemcpyAsync(rc.data(), SL.row_calls.p, (size_t)H * 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+        if (copy_d2h(rc.data(), SL.row_calls.p, (size_t)H * 4, s, "the per-row AO calls")) return RT_FAILURE;
         uint64_t tot = 0, tail = 0;
         for (uint32_t v : rc) tot += v;
         int r = H;
@@ -1319,11 +1408,11 @@ int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches) {
     HIP_TRY(hipMalloc(&d, 4 * sizeof(unsigned long long)));
     hipError_t e = hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), g.stream);
     if (e == hipSuccess) e = launch_math_selftest(seed, n, d, g.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(mismatches, d, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, g.stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    const int st = e == hipSuccess ? copy_d2h(mismatches, d, 4 * sizeof(uint64_t), g.stream, "the mismatch counts")
+                                   : RT_FAILURE;
     (void)hipFree(d);
     HIP_TRY(e);
-    return RT_SUCCESS;
+    return st;
 }
 
 int rt580_eval_powf(const float* x_device, float y, float* out_device, uint64_t n) {
@@ -1384,11 +1473,10 @@ int rt_gpu_last_stats(rt_render_stats* st) {
     if (sync_all()) return RT_FAILURE;
     const int n = g.last_rows;
     std::vector<uint32_t> rc(n), rh(n), rn(n);
-    if (n) {
-        HIP_TRY(hipMemcpy(rc.data(), SL.row_calls.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(rh.data(), SL.row_hits.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(rn.data(), SL.row_nodes.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-    }
+    if (n && (copy_d2h(rc.data(), SL.row_calls.p, (size_t)n * 4, g.stream, "the per-row AO calls") ||
+              copy_d2h(rh.data(), SL.row_hits.p, (size_t)n * 4, g.stream, "the per-row hits") ||
+              copy_d2h(rn.data(), SL.row_nodes.p, (size_t)n * 4, g.stream, "the per-row tree nodes")))
+        return RT_FAILURE;
     uint64_t calls = 0, hits = 0, tree = 0;
     for (int i = 0; i < n; i++) { calls += rc[i]; hits += rh[i]; tree += rn[i]; }
     st->rays_primary = (uint64_t)n * g.last_width;
@@ -1450,6 +1538,14 @@ int rt_gpu_profile_read(double* ms_trace, double* ms_rank, double* ms_ao, double
 
 const char* rt_gpu_last_error(void) { return g_err; }
 
+int rt_gpu_copy_to_host(void* host_ptr, const void* device_ptr, uint64_t bytes) {
+    RT_ENTRY("rt_gpu_copy_to_host");
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (bytes && (!host_ptr || !device_ptr)) return fail("NULL buffer");
+    HIP_TRY(hipSetDevice(g.device));
+    return copy_d2h(host_ptr, device_ptr, (size_t)bytes, g.stream, "a device buffer");
+}
+
 int rt_gpu_synchronize(void) {
     RT_ENTRY("rt_gpu_synchronize");
     const int cur = g_cur;
@@ -1510,6 +1606,9 @@ void shutdown_ctx() {
     if (g.needed_host) (void)hipHostFree(g.needed_host);
     if (g.far_count_host) (void)hipHostFree(g.far_count_host);
     if (g.stage) (void)hipHostFree(g.stage);
+    if (g.xfer) (void)hipHostFree(g.xfer);
+    for (auto& ev : g.xfer_ev)
+        if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : g.stage_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (g.own_stream) (void)hipStreamDestroy(g.own_stream);

@@ -84,6 +84,7 @@ SIGNATURES = [
     ("rt580_eval_powf", ctypes.c_int, [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint64]),
     ("rt_gpu_last_error", ctypes.c_char_p, []),
     ("rt_gpu_synchronize", ctypes.c_int, []),
+    ("rt_gpu_copy_to_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     ("rt_gpu_shutdown", None, []),
     ("rt580_create", ctypes.c_void_p, [ctypes.c_int, ctypes.c_int]),
     ("rt580_destroy", None, [ctypes.c_void_p]),
@@ -106,38 +107,14 @@ SIGNATURES = [
 _lib = None
 
 
-_HIP = None
-
-
-def _hip_runtime():
-    """The process's HIP runtime (torch's libamdhip64.so when torch is installed,
-    see _preload_torch_hip_runtime), for plain memory copies of device buffers
-    the library hands out (rt_gpu_render_device's framebuffer)."""
-    global _HIP
-    if _HIP is None:
-        import importlib.util
-        path = "libamdhip64.so"
-        spec = importlib.util.find_spec("torch")
-        if spec is not None and spec.submodule_search_locations:
-            p = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
-            if os.path.exists(p):
-                path = p
-        hip = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
-        hip.hipMemcpy.restype = ctypes.c_int
-        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-        hip.hipDeviceSynchronize.restype = ctypes.c_int
-        _HIP = hip
-    return _HIP
-
-
 def copy_to_host(device_ptr, nbytes, dtype):
-    """Synchronize the device, then copy nbytes from a device pointer into a new
-    numpy array of dtype (hipMemcpy, device to host)."""
+    """Copy nbytes from a device pointer the library handed out (e.g.
+    rt_gpu_render_device's framebuffer) into a new numpy array of dtype, after
+    the work queued on the shim's stream (rt_gpu_copy_to_host: staged through
+    the library's pinned buffer)."""
     import numpy as np
-    hip = _hip_runtime()
     out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype=dtype)
-    if hip.hipDeviceSynchronize() != 0 or hip.hipMemcpy(out.ctypes.data, device_ptr, nbytes, 2) != 0:
-        raise RuntimeError("hipMemcpy of a device framebuffer failed")
+    check(load().rt_gpu_copy_to_host(out.ctypes.data, device_ptr, nbytes), "rt_gpu_copy_to_host")
     return out
 
 

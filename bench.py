@@ -514,8 +514,14 @@ def render_latency(lib, rt580, params, torch, n=3):
     frame lands in it with one DMA. Mean of n calls after the timed region,
     after one untimed call."""
     import numpy as np
-    host = np.zeros(params.width * params.height * 3, dtype=np.int16)
-    rt580.check(lib.rt_gpu_host_register(host.ctypes.data, host.nbytes), "rt_gpu_host_register")
+    # page-aligned and page-rounded, like the class surface's own framebuffer
+    # (a registration must not share pages with other allocations)
+    n = params.width * params.height * 3
+    span = (n * 2 + 4095) // 4096 * 4096
+    raw = np.zeros(span + 4096, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    host = raw[off:off + span].view(np.int16)[:n]
+    rt580.check(lib.rt_gpu_host_register(host.ctypes.data, span), "rt_gpu_host_register")
     try:
         rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
         times = []

@@ -261,6 +261,11 @@ int rt_gpu_profile_ao_kernel(double* ms_total, int* launches, uint64_t* ao_rays)
  * them; a device fault (reported by whichever call next waits on the device)
  * also names the last entry point that enqueued device work before it. */
 const char* rt_gpu_last_error(void);
+/* Copy `bytes` from device memory (e.g. rt_gpu_render_device's framebuffer)
+ * to host memory, in order after the work queued on the shim's stream.
+ * Blocking. Pageable host memory is staged through the library's pinned
+ * buffer (the runtime never pins it on the fly). */
+int rt_gpu_copy_to_host(void* host_ptr, const void* device_ptr, uint64_t bytes);
 /* Wait for all device work of every context (every frame still in flight,
  * rt_gpu_render_device's included) and check the replayed count schedules of
  * those frames. RT_FAILURE names a device fault or a count mismatch and the
