@@ -1508,7 +1508,12 @@ static int near_wpe() {
 // far_candidate, full tests that hit
 __device__ unsigned long long g_far_stats[9];
 #define RT_FAR_STAT(k, v) atomicAdd(&g_far_stats[k], (unsigned long long)(v))
+// far_cell_any_kernel: rays of items whose cell has no candidate, (ray,
+// candidate) pairs of the other items, pairs passing far_candidate
+__device__ unsigned long long g_cell_stats[3];
+#define RT_CELL_STAT(k, v) atomicAdd(&g_cell_stats[k], (unsigned long long)(v))
 #else
+#define RT_CELL_STAT(k, v) ((void)0)
 #define RT_FAR_STAT(k, v) ((void)0)
 #endif
 
@@ -1685,7 +1690,10 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
         const bool tree = lw == 0xffffffffu;
         const uint32_t n_list = tree ? 0u : lw;
         const int n_cand = V.n_always + (int)n_list;
-        if (!tree && n_cand == 0) continue;  // no candidate: no far hit in this cell
+        if (!tree && n_cand == 0) {  // no candidate: no far hit in this cell
+            RT_CELL_STAT(0, lane == 0 ? (uint64_t)(r1 - r0) : 0ull);
+            continue;
+        }
         {
             const uint32_t rc = r0;
             const uint32_t nr = r1 - rc < 64u ? r1 - rc : 64u;
@@ -1734,7 +1742,9 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                         const rv3 oj = v3(a.x, a.y, a.z), dj = v3(b.x, b.y, b.z);
                         FarRay fj;
                         fj.R = b.w;
-                        if (far_candidate(ft, fj, oj, dj) && prim_test_any(S.prims[ft.id], oj, dj)) shit[wave][j] = 1u;
+                        const bool fc = far_candidate(ft, fj, oj, dj);
+                        RT_CELL_STAT(2, fc ? 1 : 0);
+                        if (fc && prim_test_any(S.prims[ft.id], oj, dj)) shit[wave][j] = 1u;
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1743,6 +1753,7 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                 hit = (uint32_t)lane < nr && shit[wave][lane] != 0u;
             }
             RT_FAR_STAT(0, (uint32_t)lane < nr ? 1 : 0);
+            RT_CELL_STAT(1, lane == 0 && !tree ? (uint64_t)nr * (uint64_t)n_cand : 0ull);
             RT_FAR_STAT(8, hit ? 1 : 0);
             if (hit) any_hit_out(W, flag, call);
         }
@@ -3125,7 +3136,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 else if (twpe == 6 && trace_lds() && so == 2)  // 2048 samples, 8 x 8 cells
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
-                else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
+                else if ((twpe == 6 || twpe == 5) && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
                     if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
                     const int bu = ao_budget();
                     if (bu <= 2)
@@ -3136,6 +3147,9 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     else if (bu == 5 || bu == 6)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 6>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
+                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
+                    else if (bu <= 4 && trace_wpe() == 5)  // (A/B) 5 waves per SIMD: room for the traversal state
+                        hipLaunchKernelGGL((ao_trace_kernel<5, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     else if (bu <= 4)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
@@ -3223,6 +3237,12 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     progress("far_any so far: rays %llu grid %llu uniform waves %llu lane waves %llu list entries %llu "
                              "lock-step steps %llu tree rays %llu candidates %llu hits %llu",
                              st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8]);
+                unsigned long long cs[3];
+                if (hipMemcpyFromSymbolAsync(cs, HIP_SYMBOL(g_cell_stats), sizeof cs, 0, hipMemcpyDeviceToHost, s) ==
+                        hipSuccess &&
+                    hipStreamSynchronize(s) == hipSuccess)
+                    progress("cell pass so far: rays in empty cells %llu, (ray, candidate) pairs %llu, passing "
+                             "far_candidate %llu", cs[0], cs[1], cs[2]);
             }
 #endif
             if ((e = hipGetLastError()) != hipSuccess) return e;

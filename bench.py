@@ -516,11 +516,11 @@ def render_latency(lib, rt580, params, torch, n=3):
     import numpy as np
     # page-aligned and page-rounded, like the class surface's own framebuffer
     # (a registration must not share pages with other allocations)
-    n = params.width * params.height * 3
-    span = (n * 2 + 4095) // 4096 * 4096
+    n_val = params.width * params.height * 3
+    span = (n_val * 2 + 4095) // 4096 * 4096
     raw = np.zeros(span + 4096, dtype=np.uint8)
     off = (-raw.ctypes.data) % 4096
-    host = raw[off:off + span].view(np.int16)[:n]
+    host = raw[off:off + span].view(np.int16)[:n_val]
     rt580.check(lib.rt_gpu_host_register(host.ctypes.data, span), "rt_gpu_host_register")
     try:
         rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
@@ -607,6 +607,11 @@ def cpu_baseline(ctx, name, root, params, gpu_px, row_counts=None):
 
 
 def main():
+    # a Python stack dump to stderr every $BENCH_WATCHDOG_S seconds (where a
+    # GPU run is when it stops making progress)
+    if os.environ.get("BENCH_WATCHDOG_S"):
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["BENCH_WATCHDOG_S"]), repeat=True, file=sys.stderr)
     # stdout carries exactly one JSON line: everything else written to fd 1 (the
     # drop-in's "Scene parsing completed!", RCCL's version banner at communicator
     # init) goes to stderr; the JSON line goes to the saved original stdout
