@@ -111,15 +111,6 @@ struct DevWork {
     void* sort_tmp;
     size_t sort_tmp_bytes;
     uint32_t far_cap;
-    // binned far queue (counting sort by direction cell, rt_kernels.hip
-    // bin_far_queue): per-bin counts / cursors, packed (count | work items << 32)
-    // and their exclusive scan, the scan's temporary storage; null: radix sort
-    uint32_t* bin_cnt;     // [n_bins]
-    uint64_t* bin_pk;      // [n_bins + 1]
-    uint64_t* bin_off;     // [n_bins + 1]
-    void* bin_tmp;
-    size_t bin_tmp_bytes;
-    uint32_t n_bins;
     // split AO pass (ao_trace_kernel): (o.xyz, call), (d.xyz, flag) per item of a chunk
     float4* ao_rays;       // [2 * ao_cap] or null
     uint32_t ao_cap;
@@ -180,10 +171,6 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
 const char* launch_where();
 // Temporary storage of the far-queue radix sort / run-length encoding / scan for `cap` rays.
 size_t far_sort_tmp_bytes(uint32_t cap);
-// Bins of the binned far queue for a direction grid of 2^log2 x 2^log2 cells
-// (0: none) and the scan's temporary storage for them.
-uint32_t far_bin_count(int grid_log2);
-size_t far_bin_tmp_bytes(uint32_t n_bins);
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s);
 // Latency path of small-scene frames (a frame split by rows so that the first
 // part's resolve and copy overlap the second part's AO): AO of the calls

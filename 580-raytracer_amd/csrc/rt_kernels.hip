@@ -2621,14 +2621,7 @@ __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, ui
 // far_keys / far_vals -- the sort's inputs, free now -- and the exclusive scan
 // of the run lengths), their chunks of <= 64 rays as work items, then
 // far_cell_any_kernel. One host read (the segment count).
-static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s,
-                                   bool binned) {
-    if (binned) {  // work items built from the bins (bin_far_queue)
-        RT_STEP("far cell pass");
-        hipLaunchKernelGGL(far_cell_any_kernel, dim3(grid_for((uint64_t)n + (uint64_t)(n / 64) * 64, 16384)), dim3(TB),
-                           0, s, S, W, n, flag);
-        return hipGetLastError();
-    }
+static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s) {
     size_t tmp = W.sort_tmp_bytes;
     RT_STEP("far queue segments");
     hipError_t e = hipcub::DeviceRunLengthEncode::Encode(W.sort_tmp, tmp, W.far_keys_alt, W.far_keys, W.far_vals,
@@ -2864,107 +2857,6 @@ void kernel_timer_release() {
 }
 
 
-// ---------------------------------------------------------------- binned far queue
-// The far queue grouped by direction cell with a counting sort instead of the
-// radix sort: bins [0, G) are the direction grid's cells (G = 4^grid_log2),
-// [G, G + kTreeBins) plane-tree rays by the top bits of their direction key,
-// G + kTreeBins the far-origin rays (last, as RT_KEY_BRUTE sorts). Histogram,
-// one exclusive scan of the packed (count | work items << 32) per bin, scatter
-// of the ray indices, then the cell pass's work items (<= 64 rays of one bin)
-// straight from the bins -- no run-length encoding, no host read of a segment
-// count. The order within a bin is arbitrary; no pass depends on it (any-hit
-// booleans, lexicographic closest hits).
-constexpr uint32_t kTreeBins = 1024;
-
-uint32_t far_bin_count(int grid_log2) {
-    return (grid_log2 > 0 ? (1u << (2 * grid_log2)) : 0u) + kTreeBins + 1u;
-}
-
-size_t far_bin_tmp_bytes(uint32_t n_bins) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)n_bins + 1);
-    return bytes;
-}
-
-__device__ __forceinline__ uint32_t far_bin(const BvhView& V, uint32_t key) {
-    const uint32_t G = V.grid_log2 > 0 ? (1u << (2 * V.grid_log2)) : 0u;
-    if (key >= RT_KEY_BRUTE) return G + kTreeBins;
-    if (key >= RT_KEY_TREE) return G + ((key - RT_KEY_TREE) >> 14);  // 24-bit direction key: its top 10 bits
-    return key >> (24 - 2 * V.grid_log2);
-}
-
-__global__ void __launch_bounds__(TB) far_bin_count_kernel(DevScene S, DevWork W, uint32_t n) {
-    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB)
-        atomicAdd(&W.bin_cnt[far_bin(S.bv, W.far_keys[i])], 1u);
-}
-
-__global__ void __launch_bounds__(TB) far_bin_pack_kernel(DevWork W, uint32_t nb) {
-    const uint32_t brute = nb - 1;
-    for (uint32_t b = blockIdx.x * TB + threadIdx.x; b <= nb; b += gridDim.x * TB) {
-        const uint32_t c = b < nb ? W.bin_cnt[b] : 0u;
-        const uint32_t w = b < brute ? (c + 63u) / 64u : 0u;
-        W.bin_pk[b] = (uint64_t)c | ((uint64_t)w << 32);
-    }
-}
-
-// bin_cnt counts down to 0 as the cursors of the scatter
-__global__ void __launch_bounds__(TB) far_bin_scatter_kernel(DevScene S, DevWork W, uint32_t n) {
-    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
-        const uint32_t b = far_bin(S.bv, W.far_keys[i]);
-        const uint32_t pos = (uint32_t)W.bin_off[b] + atomicSub(&W.bin_cnt[b], 1u) - 1u;
-        W.far_vals_alt[pos] = i;
-    }
-}
-
-// The cell pass's work items (sorted rays [x, y), the cell list's first entry
-// z and length w; w = ~0: a plane-tree bin) and their count in far_seg_n[1].
-__global__ void __launch_bounds__(TB) far_bin_work_kernel(DevScene S, DevWork W, uint32_t nb) {
-    const uint32_t G = S.bv.grid_log2 > 0 ? (1u << (2 * S.bv.grid_log2)) : 0u;
-    for (uint32_t b = blockIdx.x * TB + threadIdx.x; b < nb - 1; b += gridDim.x * TB) {
-        const uint64_t o0 = W.bin_off[b], o1 = W.bin_off[b + 1];
-        const uint32_t r0 = (uint32_t)o0, r1 = (uint32_t)o1, w0 = (uint32_t)(o0 >> 32);
-        if (r1 == r0) continue;
-        uint32_t lb = 0, lw = 0xffffffffu;
-        if (b < G) {
-            lb = S.bv.grid_start[b];
-            lw = S.bv.grid_start[b + 1] - lb;
-        }
-        for (uint32_t j = 0; r0 + 64u * j < r1; j++) {
-            const uint32_t a = r0 + 64u * j;
-            W.far_work[w0 + j] = make_uint4(a, r1 - a < 64u ? r1 : a + 64u, lb, lw);
-        }
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) W.far_seg_n[1] = (uint32_t)(W.bin_off[nb] >> 32);
-}
-
-static hipError_t bin_far_queue(const DevScene& S, const DevWork& W, hipStream_t s, uint32_t nq) {
-    const uint32_t nb = W.n_bins;
-    RT_STEP("far queue bins");
-    hipError_t e = hipMemsetAsync(W.bin_cnt, 0, (size_t)nb * 4, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(far_bin_count_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
-    hipLaunchKernelGGL(far_bin_pack_kernel, dim3(grid_for((uint64_t)nb + 1, 16384)), dim3(TB), 0, s, W, nb);
-    size_t tmp = W.bin_tmp_bytes;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(W.bin_tmp, tmp, W.bin_pk, W.bin_off, (int)nb + 1, s)) != hipSuccess)
-        return e;
-    hipLaunchKernelGGL(far_bin_scatter_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
-    hipLaunchKernelGGL(far_bin_work_kernel, dim3(grid_for(nb, 16384)), dim3(TB), 0, s, S, W, nb);
-    return hipGetLastError();
-}
-
-// RT580_FAR_BINS (A/B): 0 = radix sort always, 1 = binned always; default:
-// binned for queues of at least 2^18 rays (small queues sort in fewer,
-// shorter launches than the pass over every bin).
-static bool far_binned(const DevWork& W, uint32_t nq) {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_FAR_BINS");
-        v = e ? atoi(e) : 2;
-    }
-    if (!W.bin_cnt || v == 0) return false;
-    return v == 1 || nq >= (1u << 18);
-}
-
 // Sort the far queue (W.far_count entries) by direction key; returns its length.
 // Radix-sorted key bits: grid keys are cell << (24 - 2 L), so their low
 // 24 - 2 L bits are zero and the sort skips them (3 digit passes instead of
@@ -2981,20 +2873,14 @@ static int sort_begin_bit(const DevScene& S) {
     return b > 0 ? b : 0;
 }
 
-static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb,
-                                  bool& binned) {
+static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
     RT_STEP("far queue count D2H");
-    binned = false;
     hipError_t e = read_counts(W.far_count, 2, W.far_count_host, s, W.far_cap, W.far_cap);
     if (e != hipSuccess) return e;
     nq = W.far_count_host[0];
     if (W.far_count_host[1] > nq) return counts_fit(W.far_count_host, 2, W.far_cap, nq);
     nb = W.far_count_host[1];  // far-origin rays: keyed to sort last
     if (nq == 0) return hipSuccess;
-    if (far_binned(W, nq)) {
-        binned = true;
-        return bin_far_queue(S, W, s, nq);
-    }
     size_t tmp = W.sort_tmp_bytes;
     RT_STEP("far queue radix sort");
     return hipcub::DeviceRadixSort::SortPairs(W.sort_tmp, tmp, W.far_keys, W.far_keys_alt, W.far_vals,
@@ -3052,8 +2938,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 uint32_t nq = 0, nb = 0;
-                bool binned = false;
-                if ((e = sort_far_queue(S, W, s, nq, nb, binned)) != hipSuccess) return e;
+                if ((e = sort_far_queue(S, W, s, nq, nb)) != hipSuccess) return e;
                 if (nb) {
                     RT_STEP("trace brute scan");
                     if ((brute_split() & 1) && (uint64_t)nb * 2 <= W.far_cap) {
@@ -3124,8 +3009,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                                            li, dl, near_wave() ? 1 : 0);
                         if ((e = hipGetLastError()) != hipSuccess) return e;
                         uint32_t sq = 0, sb = 0;
-                        bool sbinned = false;
-                        if ((e = sort_far_queue(S, W, s, sq, sb, sbinned)) != hipSuccess) return e;
+                        if ((e = sort_far_queue(S, W, s, sq, sb)) != hipSuccess) return e;
                         uint8_t* flags = W.shadow + (size_t)dl * W.far_cap;
                         if (sb) {
                             RT_STEP("trace shadow brute scan");
@@ -3135,7 +3019,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         if (sq) {
                             RT_STEP("trace shadow far pass");
                             if (far_mode(sq) == 4) {
-                                if ((e = launch_far_cells(S, W, sq, flags, s, sbinned)) != hipSuccess) return e;
+                                if ((e = launch_far_cells(S, W, sq, flags, s)) != hipSuccess) return e;
                             } else {
                                 launch_far_any(S, W, sq, flags, s);
                             }
@@ -3252,7 +3136,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 else if (twpe == 6 && trace_lds() && so == 2)  // 2048 samples, 8 x 8 cells
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
-                else if ((twpe == 6 || twpe == 5) && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
+                else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
                     if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
                     const int bu = ao_budget();
                     if (bu <= 2)
@@ -3263,9 +3147,6 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     else if (bu == 5 || bu == 6)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 6>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
-                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    else if (bu <= 4 && trace_wpe() == 5)  // (A/B) 5 waves per SIMD: room for the traversal state
-                        hipLaunchKernelGGL((ao_trace_kernel<5, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     else if (bu <= 4)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
@@ -3315,8 +3196,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if ((e = launch_ao_fix(S, F, W, b, e1, s)) != hipSuccess) return e;
             if (!S.bv.has_far) continue;
             uint32_t nq = 0, nb = 0;
-            bool binned = false;
-            if ((e = sort_far_queue(S, W, s, nq, nb, binned)) != hipSuccess) return e;
+            if ((e = sort_far_queue(S, W, s, nq, nb)) != hipSuccess) return e;
             if (nb) {
                 if ((e = launch_brute_any(S, W, nq - nb, nb, (uint8_t*)nullptr, s)) != hipSuccess) return e;
                 nq -= nb;
@@ -3336,7 +3216,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if (nq == 0) continue;
             const int fm = far_mode(nq);
             if (fm == 4) {
-                if ((e = launch_far_cells(S, W, nq, (uint8_t*)nullptr, s, binned)) != hipSuccess) return e;
+                if ((e = launch_far_cells(S, W, nq, (uint8_t*)nullptr, s)) != hipSuccess) return e;
             } else if (fm == 1)
                 launch_far_any(S, W, nq, (uint8_t*)nullptr, s);
             else if (fm == 2)

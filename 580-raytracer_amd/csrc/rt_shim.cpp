@@ -46,7 +46,7 @@ struct Slot {
     // provisional hits -- per slot, so that consecutive BVH frames overlap
     // like the others (count schedule replay, see trace_rows)
     DevBuf ao_rays, ao_late, ao_late_count, far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count,
-        far_seg_off, far_seg_n, far_wofs, far_work, sort_tmp, hit4, hit_prim, shadow, bin_cnt, bin_pk, bin_off, bin_tmp;
+        far_seg_off, far_seg_n, far_wofs, far_work, sort_tmp, hit4, hit_prim, shadow;
     uint32_t far_cap = 0, ao_cap = 0;
     // replayed count schedules: the device checks' flag, its host copy (read
     // when the slot is next used), and whether a replayed frame is unchecked
@@ -562,12 +562,6 @@ DevWork dev_work() {
     w.sort_tmp = SL.sort_tmp.p;
     w.sort_tmp_bytes = SL.sort_tmp.bytes;
     w.far_cap = std::min(SL.far_cap, g.frame_fc);
-    w.n_bins = (g.bvh_ok && !g.bvh.far_nodes.empty() && SL.bin_cnt.p) ? far_bin_count(g.grid_log2) : 0u;
-    w.bin_cnt = w.n_bins ? (uint32_t*)SL.bin_cnt.p : nullptr;
-    w.bin_pk = w.n_bins ? (uint64_t*)SL.bin_pk.p : nullptr;
-    w.bin_off = w.n_bins ? (uint64_t*)SL.bin_off.p : nullptr;
-    w.bin_tmp = SL.bin_tmp.p;
-    w.bin_tmp_bytes = SL.bin_tmp.bytes;
     w.ao_cap = std::min(SL.ao_cap, g.frame_ac);
     w.ao_rays = w.ao_cap ? (float4*)SL.ao_rays.p : nullptr;
     w.ao_late = w.ao_cap ? (uint32_t*)SL.ao_late.p : nullptr;
@@ -675,12 +669,6 @@ int ensure_work(const rt_render_params* p, int n_rows) {
         SL.far_cap = fc;
     }
     if (ensure(SL.hit4, (size_t)cap * 16) || ensure(SL.hit_prim, (size_t)cap * 4)) return RT_FAILURE;
-    {   // the binned far queue's per-bin arrays (the scene's direction grid)
-        const uint32_t nb = far_bin_count(g.grid_log2);
-        if (ensure(SL.bin_cnt, (size_t)nb * 4) || ensure(SL.bin_pk, ((size_t)nb + 1) * 8) ||
-            ensure(SL.bin_off, ((size_t)nb + 1) * 8) || ensure(SL.bin_tmp, far_bin_tmp_bytes(nb) + 256))
-            return RT_FAILURE;
-    }
     if (!g.shadow_lights.empty() && g.shadow_lights.size() <= 8 &&
         ensure(SL.shadow, g.shadow_lights.size() * (size_t)fc))
         return RT_FAILURE;
@@ -1599,7 +1587,7 @@ void shutdown_ctx() {
                           &sl.call_hint, &sl.ao_rays, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
                           &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.far_count, &sl.far_seg_off,
                           &sl.far_seg_n, &sl.far_wofs, &sl.far_work, &sl.sort_tmp, &sl.hit4, &sl.hit_prim, &sl.shadow,
-                          &sl.bin_cnt, &sl.bin_pk, &sl.bin_off, &sl.bin_tmp, &sl.bad})
+                          &sl.bad})
             release(*b);
         if (sl.bad_host) (void)hipHostFree(sl.bad_host);
         if (sl.stream) (void)hipStreamDestroy(sl.stream);
