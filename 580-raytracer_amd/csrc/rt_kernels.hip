@@ -1674,7 +1674,12 @@ __device__ __forceinline__ bool far_tree_any_wave(const DevScene& S, bool live, 
 // staged rays instead. Hit rays: any_hit_out. A wave's work item is one chunk
 // of <= 64 rays of one segment (a directional light's shadow rays all share a
 // cell); grid-stride over the work items (their count is read on the device).
-__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
+// U: staged rays per lane per step (their LDS reads issued together, then the
+// U candidate tests: fewer dependent LDS round trips per (ray, candidate)
+// pair). A ray already hit is not re-checked per step (hits are ~1e-3 of the
+// rays; a second accepting candidate only repeats the flag).
+template <int U>
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(U >= 4 ? 6 : FAR_ANY_WPE)))
 far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
     __shared__ float4 sray[TB / 64][64][2];
     __shared__ uint32_t shit[TB / 64][64];
@@ -1735,16 +1740,41 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                         ft = V.far_tris[k < 0 ? V.grid_always[k + V.n_always] : V.grid_items[lb + (uint32_t)k]];
                     }
                     const uint32_t step = 64u >> lg;
-                    for (uint32_t j0 = 0; j0 < nr; j0 += step) {
-                        const uint32_t j = j0 + (uint32_t)g;
-                        if (!has || j >= nr || shit[wave][j] != 0u) continue;
-                        const float4 a = sray[wave][j][0], b = sray[wave][j][1];
-                        const rv3 oj = v3(a.x, a.y, a.z), dj = v3(b.x, b.y, b.z);
-                        FarRay fj;
-                        fj.R = b.w;
-                        const bool fc = far_candidate(ft, fj, oj, dj);
-                        RT_CELL_STAT(2, fc ? 1 : 0);
-                        if (fc && prim_test_any(S.prims[ft.id], oj, dj)) shit[wave][j] = 1u;
+                    if (U == 1) {
+                        for (uint32_t j0 = 0; j0 < nr; j0 += step) {
+                            const uint32_t j = j0 + (uint32_t)g;
+                            if (!has || j >= nr || shit[wave][j] != 0u) continue;
+                            const float4 a = sray[wave][j][0], b = sray[wave][j][1];
+                            const rv3 oj = v3(a.x, a.y, a.z), dj = v3(b.x, b.y, b.z);
+                            FarRay fj;
+                            fj.R = b.w;
+                            const bool fc = far_candidate(ft, fj, oj, dj);
+                            RT_CELL_STAT(2, fc ? 1 : 0);
+                            if (fc && prim_test_any(S.prims[ft.id], oj, dj)) shit[wave][j] = 1u;
+                        }
+                    } else {
+                        for (uint32_t j0 = 0; j0 < nr; j0 += step * U) {
+                            float4 a[U], b[U];
+                            bool live[U];
+#pragma unroll
+                            for (int u = 0; u < U; u++) {
+                                const uint32_t j = j0 + (uint32_t)u * step + (uint32_t)g;
+                                live[u] = has && j < nr;
+                                const uint32_t jj = live[u] ? j : 0u;
+                                a[u] = sray[wave][jj][0];
+                                b[u] = sray[wave][jj][1];
+                            }
+#pragma unroll
+                            for (int u = 0; u < U; u++) {
+                                const rv3 oj = v3(a[u].x, a[u].y, a[u].z), dj = v3(b[u].x, b[u].y, b[u].z);
+                                FarRay fj;
+                                fj.R = b[u].w;
+                                const bool fc = live[u] && far_candidate(ft, fj, oj, dj);
+                                RT_CELL_STAT(2, fc ? 1 : 0);
+                                if (fc && prim_test_any(S.prims[ft.id], oj, dj))
+                                    shit[wave][j0 + (uint32_t)u * step + (uint32_t)g] = 1u;
+                            }
+                        }
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2616,6 +2646,16 @@ __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, ui
     }
 }
 
+// Rays per lane per step of the cell pass (RT580_CELL_U 1, 2, 4).
+static int cell_u() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_CELL_U");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
+}
+
 // The any-hit far pass over the sorted queue [0, n) (far-origin rays
 // excluded): segments of one key (run-length encoding of the sorted keys into
 // far_keys / far_vals -- the sort's inputs, free now -- and the exclusive scan
@@ -2640,8 +2680,11 @@ static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t
     hipLaunchKernelGGL(far_chunk_expand_kernel, dim3(grid_for((uint64_t)nseg * 64, 16384)), dim3(TB), 0, s, S, W, nseg,
                        n);
     RT_STEP("far cell pass");
-    hipLaunchKernelGGL(far_cell_any_kernel, dim3(grid_for((uint64_t)(n / 64 + nseg) * 64, 16384)), dim3(TB), 0, s, S,
-                       W, n, flag);
+    const dim3 cgrid(grid_for((uint64_t)(n / 64 + nseg) * 64, 16384));
+    const int cu = cell_u();
+    if (cu == 4) hipLaunchKernelGGL(far_cell_any_kernel<4>, cgrid, dim3(TB), 0, s, S, W, n, flag);
+    else if (cu == 2) hipLaunchKernelGGL(far_cell_any_kernel<2>, cgrid, dim3(TB), 0, s, S, W, n, flag);
+    else hipLaunchKernelGGL(far_cell_any_kernel<1>, cgrid, dim3(TB), 0, s, S, W, n, flag);
 #ifdef RT580_DIAGNOSTICS
     {
         uint32_t nw[2] = {0, 0};
