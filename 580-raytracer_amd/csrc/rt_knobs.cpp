@@ -77,7 +77,6 @@ const Knob kKnobs[] = {
     {"RT580_AO_BUDGET", INT_RANGE, 0, 64, nullptr, nullptr},
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
     {"RT580_CELL_U", INT_SET, 0, 0, kCellU, nullptr},
-    {"RT580_CU_SPLIT", INT_RANGE, 0, 255, nullptr, nullptr},
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
     {"RT580_NEAR_WPE", INT_SET, 0, 0, kNearWpe, nullptr},
     {"RT580_BRUTE_SPLIT", INT_SET, 0, 0, k0123, nullptr},

@@ -37,10 +37,6 @@ enum { EV_START, EV_TRACE, EV_RANK, EV_AO, EV_RESOLVE, EV_N };
 
 struct Slot {
     hipStream_t stream = nullptr;  // frame stream (non-blocking)
-    // RT580_CU_SPLIT > 0: the AO phase on its own stream over most of the CUs,
-    // while `stream` (the trace chain, the resolve) keeps the others (see rt_gpu_init)
-    hipStream_t ao_stream = nullptr;
-    hipEvent_t ao_go = nullptr, ao_end = nullptr;
     hipEvent_t done = nullptr;     // end of the slot's last enqueued phase
     hipEvent_t ao_done = nullptr;  // end of the AO kernels of the slot's last frame
     DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
@@ -297,8 +293,6 @@ int sync_all() {
         State& c = g_ctx[k];
         if (!c.inited || c.device != dev) continue;
         if (stream_sync(c.stream, "waiting for the caller's stream")) return RT_FAILURE;
-        for (auto& sl : c.slot)
-            if (sl.ao_stream && stream_sync(sl.ao_stream, "waiting for a frame slot's AO stream")) return RT_FAILURE;
         if (c.own_stream != c.stream && stream_sync(c.own_stream, "waiting for the library's stream")) return RT_FAILURE;
         for (auto& sl : c.slot)
             if (sl.stream && stream_sync(sl.stream, "waiting for a frame slot")) return RT_FAILURE;
@@ -885,19 +879,9 @@ int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
             g.ao_valid = false;
         }
         if (ao_order()) HIP_TRY(wait_previous_ao());
-        // the AO phase on the slot's AO stream (its own CUs) when there is one
-        const hipStream_t as = (g.pipeline && SL.ao_stream) ? SL.ao_stream : fs();
-        if (as != fs()) {
-            HIP_TRY(hipEventRecord(SL.ao_go, fs()));
-            HIP_TRY(hipStreamWaitEvent(as, SL.ao_go, 0));
-        }
-        const hipError_t e = launch_ao(sc, f, w, as);
+        const hipError_t e = launch_ao(sc, f, w, fs());
         if (end_schedule(g.sched_ao, "AO", e)) return RT_FAILURE;
         HIP_TRY(e);
-        if (as != fs()) {
-            HIP_TRY(hipEventRecord(SL.ao_end, as));
-            HIP_TRY(hipStreamWaitEvent(fs(), SL.ao_end, 0));
-        }
         if (!replay && frame_verified(p)) g.ao_valid = true;
     }
     HIP_TRY(hipEventRecord(g.ev[EV_AO], fs()));
@@ -1020,36 +1004,8 @@ int rt_gpu_init(int device) {
             return fail("RT580_CHUNK_LOG2=%s: not an integer in [%d, %d]", e, kChunkLog2Min, kChunkLog2Max);
         g.chunk_log2 = (int)v;
     }
-    // RT580_CU_SPLIT = n > 0 (A/B): n CUs of the device, spread evenly
-    // over its XCDs, serve the frames' trace chains (a chain of small,
-    // latency-bound launches per recursion level) and the other CUs the AO
-    // phases, through per-slot streams with CU masks. Without it (default)
-    // both phases share every CU and a chain's kernels wait for CU slots behind
-    // other frames' long-running AO workgroups.
-    int cu_split = 0;
-    if (const char* e = std::getenv("RT580_CU_SPLIT")) cu_split = std::atoi(e);
-    std::vector<uint32_t> mask_t, mask_a;
-    if (cu_split > 0) {
-        hipDeviceProp_t prop;
-        HIP_TRY(hipGetDeviceProperties(&prop, device));
-        const int ncu = prop.multiProcessorCount;
-        if (cu_split >= ncu) return fail("RT580_CU_SPLIT=%d: not below the device's %d CUs", cu_split, ncu);
-        mask_t.assign((size_t)(ncu + 31) / 32, 0u);
-        mask_a.assign(mask_t.size(), 0u);
-        for (int c = 0; c < ncu; c++) {
-            const bool t = (int)((int64_t)c * cu_split / ncu) != (int)((int64_t)(c + 1) * cu_split / ncu);
-            (t ? mask_t : mask_a)[(size_t)c / 32] |= 1u << (c % 32);
-        }
-    }
     for (auto& sl : g.slot) {
-        if (cu_split > 0) {
-            HIP_TRY(hipExtStreamCreateWithCUMask(&sl.stream, (uint32_t)mask_t.size(), mask_t.data()));
-            HIP_TRY(hipExtStreamCreateWithCUMask(&sl.ao_stream, (uint32_t)mask_a.size(), mask_a.data()));
-            HIP_TRY(hipEventCreateWithFlags(&sl.ao_go, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&sl.ao_end, hipEventDisableTiming));
-        } else {
-            HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-        }
+        HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&sl.ao_done, hipEventDisableTiming));
     }
@@ -1635,9 +1591,6 @@ void shutdown_ctx() {
             release(*b);
         if (sl.bad_host) (void)hipHostFree(sl.bad_host);
         if (sl.stream) (void)hipStreamDestroy(sl.stream);
-        if (sl.ao_stream) (void)hipStreamDestroy(sl.ao_stream);
-        if (sl.ao_go) (void)hipEventDestroy(sl.ao_go);
-        if (sl.ao_end) (void)hipEventDestroy(sl.ao_end);
         if (sl.done) (void)hipEventDestroy(sl.done);
         if (sl.ao_done) (void)hipEventDestroy(sl.ao_done);
     }
