@@ -1076,11 +1076,11 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     g.grid_log2 = g.grid_n_always = 0;
     if (s->n_prims > 64) {
         g.bvh_ok = build_bvh(s->prims, s->n_prims, g.bvh);
-        // far-search direction grid: 2048^2 cells up to 300k triangles (field100k:
-        // 19.4 candidates per far-pass ray against 33.7 at 1024^2; 139M list
-        // entries, 5.6 s host build), 1024^2 above (RT580_GRID_LOG2: other
-        // sizes, 0 = plane tree only)
-        int glog2 = s->n_prims <= 300000 ? 11 : 10;
+        // far-search direction grid: 2048^2 cells (field100k: 19.4 candidates
+        // per far-pass ray against 33.7 at 1024^2; 139M list entries, 5.6 s host
+        // build; config 5's 1M triangles: its row sample 1,370 -> 1,227 ms, 12 s
+        // build; RT580_GRID_LOG2: other sizes, 0 = plane tree only)
+        int glog2 = 11;
         if (const char* e = std::getenv("RT580_GRID_LOG2")) glog2 = std::atoi(e);
         if (g.bvh_ok && glog2 > 0 && glog2 <= 12) build_dir_grid(s->prims, g.bvh, glog2);
         // the 4-wide form for the any-hit queries (AO, shadows); RT580_BVH4=0: binary only

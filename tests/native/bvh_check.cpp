@@ -96,8 +96,8 @@ int main(int argc, char** argv) {
     V.scale = B.scale;
     // far search: the direction grid (default) or, with RT_FAR_TREE=1, the plane tree only
     const bool use_grid = !(std::getenv("RT_FAR_TREE") && std::atoi(std::getenv("RT_FAR_TREE")) == 1);
-    // the product's rule (rt_shim.cpp rt_gpu_upload_scene): 2048^2 cells up to 300k triangles, 1024^2 above
-    const int glog2 = std::getenv("RT_GRID_LOG2") ? std::atoi(std::getenv("RT_GRID_LOG2")) : (P.size() <= 300000 ? 11 : 10);
+    // the product's rule (rt_shim.cpp rt_gpu_upload_scene): 2048^2 cells
+    const int glog2 = std::getenv("RT_GRID_LOG2") ? std::atoi(std::getenv("RT_GRID_LOG2")) : 11;
     if (use_grid) build_dir_grid(P.data(), B, glog2);
     V.grid_start = B.grid_start.empty() ? nullptr : B.grid_start.data();
     V.grid_items = B.grid_items.data();
