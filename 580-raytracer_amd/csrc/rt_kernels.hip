@@ -1507,12 +1507,25 @@ static int near_wpe() {
 // the longest lane list / U), plane-tree rays, candidates passing
 // far_candidate, full tests that hit
 __device__ unsigned long long g_far_stats[9];
+#ifdef RT580_DIAG_NO_STATS  // timing ablations: no per-pair atomics
+#define RT_FAR_STAT(k, v) ((void)0)
+#else
 #define RT_FAR_STAT(k, v) atomicAdd(&g_far_stats[k], (unsigned long long)(v))
+#endif
 // far_cell_any_kernel: rays of items whose cell has no candidate, (ray,
 // candidate) pairs of the other items, pairs passing far_candidate
 __device__ unsigned long long g_cell_stats[3];
-#define RT_CELL_STAT(k, v) atomicAdd(&g_cell_stats[k], (unsigned long long)(v))
+#ifdef RT580_DIAG_NO_STATS
+#define RT_CELL_STAT(k, v) ((void)0)
 #else
+#define RT_CELL_STAT(k, v) atomicAdd(&g_cell_stats[k], (unsigned long long)(v))
+#endif
+// RT580_CELL_SKIP (timing attribution only; results wrong): 1 no candidate
+// loop, 2 no full tests, 3 no far_candidate either (the loop's LDS reads kept)
+__device__ int g_cell_skip;
+#define CELL_SKIP(k) (g_cell_skip == (k))
+#else
+#define CELL_SKIP(k) false
 #define RT_CELL_STAT(k, v) ((void)0)
 #define RT_FAR_STAT(k, v) ((void)0)
 #endif
@@ -1674,119 +1687,177 @@ __device__ __forceinline__ bool far_tree_any_wave(const DevScene& S, bool live, 
 // staged rays instead. Hit rays: any_hit_out. A wave's work item is one chunk
 // of <= 64 rays of one segment (a directional light's shadow rays all share a
 // cell); grid-stride over the work items (their count is read on the device).
-// U: staged rays per lane per step (their LDS reads issued together, then the
-// U candidate tests: fewer dependent LDS round trips per (ray, candidate)
-// pair). A ray already hit is not re-checked per step (hits are ~1e-3 of the
-// rays; a second accepting candidate only repeats the flag).
-template <int U>
-__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(U >= 4 ? 6 : FAR_ANY_WPE)))
+// A ray already hit is not re-checked per step (hits are ~1e-3 of the rays; a
+// second accepting candidate only repeats the flag). Pairs passing
+// far_candidate (~1 % of the north-star frame's 2.4e9 pairs) are queued in LDS
+// and get their full tests 64 at a time (cell_full_tests): tested in place,
+// each cost a whole divergent wave step (3.0 of the frame's 5.0 candidate-loop
+// ms, measured with RT580_CELL_SKIP). (Software-pipelining the items' load
+// chains -- next item's indices and descriptor in flight during the current
+// item -- measured slower: 41.7 vs 38.8 ms, 9.8 vs 8.4 ms at a 1/8 share.)
+struct CellItem {
+    uint32_t r0, nr, lb, n_list;
+    bool tree, skip;
+};
+__device__ __forceinline__ CellItem cell_item(const BvhView& V, uint4 wd) {
+    CellItem it;
+    it.r0 = __builtin_amdgcn_readfirstlane(wd.x);
+    const uint32_t r1 = __builtin_amdgcn_readfirstlane(wd.y);
+    it.lb = __builtin_amdgcn_readfirstlane(wd.z);
+    const uint32_t lw = __builtin_amdgcn_readfirstlane(wd.w);
+    it.nr = r1 - it.r0 < 64u ? r1 - it.r0 : 64u;
+    it.tree = lw == 0xffffffffu;
+    it.n_list = it.tree ? 0u : lw;
+    it.skip = !it.tree && V.n_always + (int)it.n_list == 0;  // no candidate: no far hit in this cell
+    return it;
+}
+__device__ __forceinline__ int cell_lg(int lt) {
+    return lt > 32 ? 6 : lt > 16 ? 5 : lt > 8 ? 4 : lt > 4 ? 3 : lt > 2 ? 2 : lt > 1 ? 1 : 0;
+}
+// The item's index loads for this lane: its ray's queue entry (q) and its
+// first-chunk candidate's far_tris index (gi).
+__device__ __forceinline__ void cell_indices(const BvhView& V, const DevWork& W, const CellItem& it, int lane,
+                                             uint32_t& q, uint32_t& gi) {
+    q = 0u;
+    gi = 0u;
+    if (it.skip) return;
+    if ((uint32_t)lane < it.nr) q = W.far_vals_alt[it.r0 + lane];
+    if (it.tree) return;
+    const int n_cand = V.n_always + (int)it.n_list;
+    const int lt = n_cand < 64 ? n_cand : 64, lg = cell_lg(lt);
+    const int kk = lane & ((1 << lg) - 1);
+    if (kk < lt) {
+        const int k = kk - V.n_always;
+        gi = k < 0 ? V.grid_always[k + V.n_always] : V.grid_items[it.lb + (uint32_t)k];
+    }
+}
+
+// The queued pairs [0, qn) of far_cell_any_kernel (qn < 128): the full
+// reference test of each, one pair per lane; a hit flags the ray. Whole wave.
+__device__ __forceinline__ void cell_full_tests(const DevScene& S, const float4 (*sray)[2], uint32_t* shit,
+                                                const uint32_t* pq_id, const uint8_t* pq_j, uint32_t qn) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i = lane; i < qn; i += 64) {
+        const uint32_t j = pq_j[i];
+        if (CELL_SKIP(2) || shit[j] != 0u) continue;
+        const float4 a = sray[j][0], b = sray[j][1];
+        if (prim_test_any(S.prims[pq_id[i]], v3(a.x, a.y, a.z), v3(b.x, b.y, b.z))) shit[j] = 1u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
 far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
     __shared__ float4 sray[TB / 64][64][2];
     __shared__ uint32_t shit[TB / 64][64];
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
+    __shared__ uint32_t pq_id[TB / 64][128];
+    __shared__ uint8_t pq_j[TB / 64][128];
     const BvhView& V = S.bv;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t nwork = W.far_seg_n[1];
-    for (uint32_t w = xcd_block(blockIdx.x, gridDim.x) * (TB / 64) + wave; w < nwork; w += gridDim.x * (TB / 64)) {
-        // the work item: sorted rays [r0, r1) of one segment and its cell's candidate list
-        const uint4 wd = W.far_work[w];
-        const uint32_t r0 = __builtin_amdgcn_readfirstlane(wd.x), r1 = __builtin_amdgcn_readfirstlane(wd.y);
-        const uint32_t lb = __builtin_amdgcn_readfirstlane(wd.z), lw = __builtin_amdgcn_readfirstlane(wd.w);
-        const bool tree = lw == 0xffffffffu;
-        const uint32_t n_list = tree ? 0u : lw;
-        const int n_cand = V.n_always + (int)n_list;
-        if (!tree && n_cand == 0) {  // no candidate: no far hit in this cell
-            RT_CELL_STAT(0, lane == 0 ? (uint64_t)(r1 - r0) : 0ull);
-            continue;
+    const uint32_t stride = gridDim.x * (TB / 64);
+    uint32_t w = xcd_block(blockIdx.x, gridDim.x) * (TB / 64) + wave;
+    if (w >= nwork) return;
+    for (;;) {
+        const CellItem cur = cell_item(V, W.far_work[w]);
+        uint32_t q, gi;
+        cell_indices(V, W, cur, lane, q, gi);
+        const bool live = !cur.skip && (uint32_t)lane < cur.nr;
+        float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(1.0f, 0.0f, 0.0f, 0.0f);
+        if (live) {
+            a = W.far_rays[2 * (size_t)q];
+            b = W.far_rays[2 * (size_t)q + 1];
         }
-        {
-            const uint32_t rc = r0;
-            const uint32_t nr = r1 - rc < 64u ? r1 - rc : 64u;
-            rv3 o = v3(0, 0, 0), d = v3(1, 0, 0);
-            FarRay fr;
-            fr.R = 0.0f;
-            uint32_t call = 0;
-            // the previous chunk's LDS reads are done before it is overwritten
+        const int n_cand = V.n_always + (int)cur.n_list;
+        FarTri ft0;
+        if (!cur.skip && !cur.tree) ft0 = V.far_tris[gi];
+        const uint32_t wn = w + stride;
+        if (cur.skip) {
+            RT_CELL_STAT(0, lane == 0 ? (uint64_t)cur.nr : 0ull);
+        } else {
+            const uint32_t nr = cur.nr;
+            // the previous item's LDS reads are done before it is overwritten
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if ((uint32_t)lane < nr) {
-                const uint32_t q = W.far_vals_alt[rc + lane];
-                float4 a = W.far_rays[2 * (size_t)q], b = W.far_rays[2 * (size_t)q + 1];
-                o = v3(a.x, a.y, a.z);
-                d = v3(b.x, b.y, b.z);
-                call = __float_as_uint(a.w);
-                fr = far_ray(V, o);
-                b.w = fr.R;
+            if (live) {
                 sray[wave][lane][0] = a;
-                sray[wave][lane][1] = b;
+                sray[wave][lane][1] = make_float4(b.x, b.y, b.z, far_ray(V, v3(a.x, a.y, a.z)).R);
                 shit[wave][lane] = 0u;
             }
             bool hit = false;
-            if (tree) {
-                hit = far_tree_any_wave(S, (uint32_t)lane < nr, o, d, fr, stk[wave]);
+            if (cur.tree) {
+                // the rays back from LDS (registers are short across the candidate loop)
+                const float4 at = sray[wave][lane][0], bt = sray[wave][lane][1];
+                FarRay fr;
+                fr.R = bt.w;
+                hit = far_tree_any_wave(S, live, v3(at.x, at.y, at.z), v3(bt.x, bt.y, bt.z), fr, stk[wave]);
             } else {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                for (int kc = 0; kc < n_cand; kc += 64) {
+                uint32_t qn = 0;  // queued (candidate, ray) pairs, wave-uniform
+                for (int kc = 0; kc < (CELL_SKIP(1) ? 0 : n_cand); kc += 64) {
                     const int lt = n_cand - kc < 64 ? n_cand - kc : 64;
-                    const int lg = lt > 32 ? 6 : lt > 16 ? 5 : lt > 8 ? 4 : lt > 4 ? 3 : lt > 2 ? 2 : lt > 1 ? 1 : 0;
+                    const int lg = cell_lg(lt);
                     const int kk = lane & ((1 << lg) - 1), g = lane >> lg;
                     const bool has = kk < lt;
-                    FarTri ft;
-                    if (has) {
+                    FarTri ft = ft0;
+                    if (kc > 0 && has) {
                         const int k = kc + kk - V.n_always;
-                        ft = V.far_tris[k < 0 ? V.grid_always[k + V.n_always] : V.grid_items[lb + (uint32_t)k]];
+                        ft = V.far_tris[k < 0 ? V.grid_always[k + V.n_always] : V.grid_items[cur.lb + (uint32_t)k]];
                     }
                     const uint32_t step = 64u >> lg;
-                    if (U == 1) {
-                        for (uint32_t j0 = 0; j0 < nr; j0 += step) {
-                            const uint32_t j = j0 + (uint32_t)g;
-                            if (!has || j >= nr || shit[wave][j] != 0u) continue;
-                            const float4 a = sray[wave][j][0], b = sray[wave][j][1];
-                            const rv3 oj = v3(a.x, a.y, a.z), dj = v3(b.x, b.y, b.z);
+                    for (uint32_t j0 = 0; j0 < nr; j0 += step) {
+                        const uint32_t j = j0 + (uint32_t)g;
+                        bool fc = false;
+                        if (has && j < nr && shit[wave][j] == 0u) {
+                            const float4 aj = sray[wave][j][0], bj = sray[wave][j][1];
                             FarRay fj;
-                            fj.R = b.w;
-                            const bool fc = far_candidate(ft, fj, oj, dj);
-                            RT_CELL_STAT(2, fc ? 1 : 0);
-                            if (fc && prim_test_any(S.prims[ft.id], oj, dj)) shit[wave][j] = 1u;
+                            fj.R = bj.w;
+                            if (CELL_SKIP(3)) {
+                                if (aj.x == ft.n[0] && bj.w == ft.d) shit[wave][j] = 1u;
+                                continue;
+                            }
+                            fc = far_candidate(ft, fj, v3(aj.x, aj.y, aj.z), v3(bj.x, bj.y, bj.z));
                         }
-                    } else {
-                        for (uint32_t j0 = 0; j0 < nr; j0 += step * U) {
-                            float4 a[U], b[U];
-                            bool live[U];
-#pragma unroll
-                            for (int u = 0; u < U; u++) {
-                                const uint32_t j = j0 + (uint32_t)u * step + (uint32_t)g;
-                                live[u] = has && j < nr;
-                                const uint32_t jj = live[u] ? j : 0u;
-                                a[u] = sray[wave][jj][0];
-                                b[u] = sray[wave][jj][1];
-                            }
-#pragma unroll
-                            for (int u = 0; u < U; u++) {
-                                const rv3 oj = v3(a[u].x, a[u].y, a[u].z), dj = v3(b[u].x, b[u].y, b[u].z);
-                                FarRay fj;
-                                fj.R = b[u].w;
-                                const bool fc = live[u] && far_candidate(ft, fj, oj, dj);
-                                RT_CELL_STAT(2, fc ? 1 : 0);
-                                if (fc && prim_test_any(S.prims[ft.id], oj, dj))
-                                    shit[wave][j0 + (uint32_t)u * step + (uint32_t)g] = 1u;
-                            }
+                        RT_CELL_STAT(2, fc ? 1 : 0);
+                        // passing pairs are queued; their full tests run 64 at a time
+                        // (~1 % of pairs pass: tested in place they would each cost a
+                        // whole wave step)
+                        const uint64_t m = __ballot(fc);
+                        if (m == 0) continue;
+                        if (fc) {
+                            const uint32_t slot = qn + (uint32_t)__popcll(m & lanemask_lt());
+                            pq_id[wave][slot] = ft.id;
+                            pq_j[wave][slot] = j;
+                        }
+                        qn += (uint32_t)__popcll(m);
+                        if (qn >= 64u) {
+                            cell_full_tests(S, sray[wave], shit[wave], pq_id[wave], pq_j[wave], qn);
+                            qn = 0;
                         }
                     }
                 }
+                if (qn) cell_full_tests(S, sray[wave], shit[wave], pq_id[wave], pq_j[wave], qn);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                hit = (uint32_t)lane < nr && shit[wave][lane] != 0u;
+                hit = live && shit[wave][lane] != 0u;
             }
-            RT_FAR_STAT(0, (uint32_t)lane < nr ? 1 : 0);
-            RT_CELL_STAT(1, lane == 0 && !tree ? (uint64_t)nr * (uint64_t)n_cand : 0ull);
+            RT_FAR_STAT(0, live ? 1 : 0);
+            RT_CELL_STAT(1, lane == 0 && !cur.tree ? (uint64_t)nr * (uint64_t)n_cand : 0ull);
             RT_FAR_STAT(8, hit ? 1 : 0);
-            if (hit) any_hit_out(W, flag, call);
+            if (hit) any_hit_out(W, flag, __float_as_uint(sray[wave][lane][0].w));
         }
+        if (wn >= nwork) break;
+        w = wn;
     }
 }
 
@@ -2646,16 +2717,6 @@ __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, ui
     }
 }
 
-// Rays per lane per step of the cell pass (RT580_CELL_U 1, 2, 4).
-static int cell_u() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_CELL_U");
-        v = e ? atoi(e) : 1;
-    }
-    return v;
-}
-
 // The any-hit far pass over the sorted queue [0, n) (far-origin rays
 // excluded): segments of one key (run-length encoding of the sorted keys into
 // far_keys / far_vals -- the sort's inputs, free now -- and the exclusive scan
@@ -2680,11 +2741,17 @@ static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t
     hipLaunchKernelGGL(far_chunk_expand_kernel, dim3(grid_for((uint64_t)nseg * 64, 16384)), dim3(TB), 0, s, S, W, nseg,
                        n);
     RT_STEP("far cell pass");
+#ifdef RT580_DIAGNOSTICS
+    {
+        const char* ev = getenv("RT580_CELL_SKIP");
+        const int sk = ev ? atoi(ev) : 0;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess ||
+            (e = hipMemcpyToSymbol(HIP_SYMBOL(g_cell_skip), &sk, sizeof sk, 0, hipMemcpyHostToDevice)) != hipSuccess)
+            return e;
+    }
+#endif
     const dim3 cgrid(grid_for((uint64_t)(n / 64 + nseg) * 64, 16384));
-    const int cu = cell_u();
-    if (cu == 4) hipLaunchKernelGGL(far_cell_any_kernel<4>, cgrid, dim3(TB), 0, s, S, W, n, flag);
-    else if (cu == 2) hipLaunchKernelGGL(far_cell_any_kernel<2>, cgrid, dim3(TB), 0, s, S, W, n, flag);
-    else hipLaunchKernelGGL(far_cell_any_kernel<1>, cgrid, dim3(TB), 0, s, S, W, n, flag);
+    hipLaunchKernelGGL(far_cell_any_kernel, cgrid, dim3(TB), 0, s, S, W, n, flag);
 #ifdef RT580_DIAGNOSTICS
     {
         uint32_t nw[2] = {0, 0};
