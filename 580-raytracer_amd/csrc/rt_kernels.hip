@@ -1673,6 +1673,43 @@ __device__ __forceinline__ bool far_tree_any_wave(const DevScene& S, bool live, 
     return hit;
 }
 
+// The plane-tree far search of bvh_closest for the lanes with `walk` set
+// (far_closest's tree part): the wave walks the tree once for all of them,
+// merging into (h, found) with the lexicographic rule. Returns whether h
+// changed. stk: the wave's LDS stack. Whole wave.
+__device__ __forceinline__ bool far_tree_closest_wave(const DevScene& S, bool walk, rv3 o, rv3 d, const FarRay& fr,
+                                                      Hit& h, bool& found, int32_t* stk) {
+    bool changed = false;
+    int sp = 0;
+    stk[sp++] = 0;
+    while (sp > 0) {
+        const int fnode = __builtin_amdgcn_readfirstlane(stk[--sp]);
+        const FarNode fn = load_far_node(S.bv.far_nodes, fnode);
+        float T;
+        const bool may = walk && far_node_may(fn, fr, o, d, T) && !(found && h.t < T);
+        if (__ballot(may) == 0) continue;
+        if (fn.count == 0) {
+            stk[sp++] = fn.first + 1;
+            stk[sp++] = fn.first;
+            continue;
+        }
+        for (int k = fn.first; k < fn.first + fn.count; k++) {
+            const FarTri ft = load_far_tri(S.bv.far_tris, k);
+            const bool cand = may && far_candidate(ft, fr, o, d);
+            if (__ballot(cand) == 0) continue;
+            const rt_prim P = load_prim_scalar(S.prims, (int)ft.id);
+            float t, a, b, g;
+            if (cand && prim_test_closest(P, o, d, t, a, b, g, found ? h.t : INFINITY) &&
+                lex_better(t, (int)ft.id, found, h)) {
+                found = true;
+                changed = true;
+                h.t = t; h.a = a; h.b = b; h.g = g; h.prim = (int)ft.id;
+            }
+        }
+    }
+    return changed;
+}
+
 // Cell-major any-hit far pass over the sorted queue [0, n) (far-origin rays
 // excluded), cut into segments of one sort key (far_seg_off / far_keys, see
 // launch_far_cells). A wave takes a segment: a grid cell's rays share one
@@ -1858,6 +1895,161 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
         }
         if (wn >= nwork) break;
         w = wn;
+    }
+}
+
+// (t, primitive) as one ordered key: t > 0 for every accepted hit (tri_test
+// rejects t <= EPSILON), so its bits order like the floats; the lexicographic
+// rule lex_better is then the minimum of the keys.
+__device__ __forceinline__ unsigned long long hit_key(float t, int prim) {
+    return ((unsigned long long)rt_f32_bits(t) << 32) | (uint32_t)prim;
+}
+
+// The queued pairs [0, qn) of far_cell_closest_kernel (qn < 128): the full
+// closest test of each, one pair per lane, bounded by the ray's best so far
+// (any bound >= the final best gives the same minimum); an accepted hit
+// lowers the ray's key. Whole wave.
+__device__ __forceinline__ void cell_closest_tests(const DevScene& S, const float4 (*sray)[2],
+                                                   unsigned long long* sbest, const uint32_t* pq_id,
+                                                   const uint8_t* pq_j, uint32_t qn) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i = lane; i < qn; i += 64) {
+        const uint32_t j = pq_j[i], id = pq_id[i];
+        const unsigned long long kb = sbest[j];
+        const float tcut = kb == ~0ull ? INFINITY : rt_bits_f32((uint32_t)(kb >> 32));
+        const float4 a = sray[j][0], b = sray[j][1];
+        float t, ba, bb, bg;
+        if (prim_test_closest(S.prims[id], v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), t, ba, bb, bg, tcut))
+            atomicMin(&sbest[j], hit_key(t, (int)id));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Cell-major closest-hit far pass over the sorted queue [0, n) of a trace
+// level (far-origin rays excluded), on the work items of launch_far_cells:
+// far_cell_any_kernel's shape with bvh_closest's far part per ray. A wave
+// stages an item's rays and their provisional hits (hit4 / hit_prim) in LDS;
+// lanes hold the cell's candidates and step through the rays (far_candidate);
+// passing pairs are queued and tested 64 at a time, each hit folded into the
+// ray's (t, primitive) key with an LDS atomicMin (= lex_better's order). The
+// winner's barycentrics are then recomputed (tri_test's outputs do not depend
+// on its bound) and stored if it changed. Plane-tree items walk the tree
+// (far_tree_closest_wave). Against far_closest_kernel, whose per-lane list
+// walk makes a wave as slow as its longest cell list, one dependent
+// entry -> plane -> record chain per step.
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
+far_cell_closest_kernel(DevScene S, DevWork W) {
+    __shared__ float4 sray[TB / 64][64][2];
+    __shared__ unsigned long long sbest[TB / 64][64];
+    __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
+    __shared__ uint32_t pq_id[TB / 64][128];
+    __shared__ uint8_t pq_j[TB / 64][128];
+    const BvhView& V = S.bv;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t nwork = W.far_seg_n[1];
+    const uint32_t stride = gridDim.x * (TB / 64);
+    for (uint32_t w = xcd_block(blockIdx.x, gridDim.x) * (TB / 64) + wave; w < nwork; w += stride) {
+        const CellItem cur = cell_item(V, W.far_work[w]);
+        if (cur.skip) continue;  // no candidate: no far hit in this cell
+        uint32_t q, gi;
+        cell_indices(V, W, cur, lane, q, gi);
+        const bool live = (uint32_t)lane < cur.nr;
+        float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(1.0f, 0.0f, 0.0f, 0.0f);
+        uint32_t node = 0;
+        if (live) {
+            a = W.far_rays[2 * (size_t)q];
+            b = W.far_rays[2 * (size_t)q + 1];
+            node = __float_as_uint(a.w);
+        }
+        if (cur.tree) {
+            Hit h;
+            h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
+            if (live) {
+                const float4 hv = W.hit4[node];
+                h.prim = W.hit_prim[node];
+                h.t = hv.x; h.a = hv.y; h.b = hv.z; h.g = hv.w;
+            }
+            bool found = h.prim >= 0;
+            const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+            if (far_tree_closest_wave(S, live, o, d, far_ray(V, o), h, found, stk[wave])) {
+                W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
+                W.hit_prim[node] = h.prim;
+            }
+            continue;
+        }
+        const int n_cand = V.n_always + (int)cur.n_list;
+        const FarTri ft0 = V.far_tris[gi];
+        // the ray's best so far as a key (hit4.x = t, hit_prim)
+        unsigned long long k0 = ~0ull;
+        if (live) {
+            const int hp = W.hit_prim[node];
+            if (hp >= 0) k0 = hit_key(W.hit4[node].x, hp);
+        }
+        // the previous item's LDS reads are done before it is overwritten
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (live) {
+            sray[wave][lane][0] = a;
+            sray[wave][lane][1] = make_float4(b.x, b.y, b.z, far_ray(V, v3(a.x, a.y, a.z)).R);
+            sbest[wave][lane] = k0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t nr = cur.nr;
+        uint32_t qn = 0;  // queued (candidate, ray) pairs, wave-uniform
+        for (int kc = 0; kc < n_cand; kc += 64) {
+            const int lt = n_cand - kc < 64 ? n_cand - kc : 64;
+            const int lg = cell_lg(lt);
+            const int kk = lane & ((1 << lg) - 1), g = lane >> lg;
+            const bool has = kk < lt;
+            FarTri ft = ft0;
+            if (kc > 0 && has) {
+                const int k = kc + kk - V.n_always;
+                ft = V.far_tris[k < 0 ? V.grid_always[k + V.n_always] : V.grid_items[cur.lb + (uint32_t)k]];
+            }
+            const uint32_t step = 64u >> lg;
+            for (uint32_t j0 = 0; j0 < nr; j0 += step) {
+                const uint32_t j = j0 + (uint32_t)g;
+                bool fc = false;
+                if (has && j < nr) {
+                    const float4 aj = sray[wave][j][0], bj = sray[wave][j][1];
+                    FarRay fj;
+                    fj.R = bj.w;
+                    fc = far_candidate(ft, fj, v3(aj.x, aj.y, aj.z), v3(bj.x, bj.y, bj.z));
+                }
+                const uint64_t m = __ballot(fc);
+                if (m == 0) continue;
+                if (fc) {
+                    const uint32_t slot = qn + (uint32_t)__popcll(m & lanemask_lt());
+                    pq_id[wave][slot] = ft.id;
+                    pq_j[wave][slot] = j;
+                }
+                qn += (uint32_t)__popcll(m);
+                if (qn >= 64u) {
+                    cell_closest_tests(S, sray[wave], sbest[wave], pq_id[wave], pq_j[wave], qn);
+                    qn = 0;
+                }
+            }
+        }
+        if (qn) cell_closest_tests(S, sray[wave], sbest[wave], pq_id[wave], pq_j[wave], qn);
+        if (live) {
+            const unsigned long long kb = sbest[wave][lane];
+            if (kb != k0) {  // a far hit won: its full record
+                const int id = (int)(uint32_t)kb;
+                const float4 ar = sray[wave][lane][0], br = sray[wave][lane][1];
+                float t, ba, bb, bg;
+                (void)prim_test_closest(S.prims[id], v3(ar.x, ar.y, ar.z), v3(br.x, br.y, br.z), t, ba, bb, bg);
+                W.hit4[node] = make_float4(t, ba, bb, bg);
+                W.hit_prim[node] = id;
+            }
+        }
     }
 }
 
@@ -2262,12 +2454,14 @@ static int brute_split() {
     return v;
 }
 
-// List entries in flight per lane in far_closest_kernel (RT580_FAR_CLOSEST_U 1, 2, 4).
+// The trace levels' closest-hit far pass (RT580_FAR_CLOSEST_U): 0 cell-major
+// (far_cell_closest_kernel), else far_closest_kernel with that many list entries
+// in flight per lane (1, 2, 4).
 static int far_closest_u() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_FAR_CLOSEST_U");
-        v = e ? atoi(e) : 4;
+        v = e ? atoi(e) : 0;
     }
     return v;
 }
@@ -2369,33 +2563,7 @@ __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, 
         bool changed = false;
         const bool gl = live && grid_origin(S.bv, o);
         if (far_grid_lane<true, U>(S, gl, o, d, fr, h, found, ftile[wave])) changed = true;
-        const bool walk = live && !gl;
-        int sp = 0;
-        stk[wave][sp++] = 0;
-        while (sp > 0) {
-            const int fnode = __builtin_amdgcn_readfirstlane(stk[wave][--sp]);
-            const FarNode fn = load_far_node(S.bv.far_nodes, fnode);
-            float T;
-            const bool may = walk && far_node_may(fn, fr, o, d, T) && !(found && h.t < T);
-            if (__ballot(may) == 0) continue;
-            if (fn.count == 0) {
-                stk[wave][sp++] = fn.first + 1;
-                stk[wave][sp++] = fn.first;
-                continue;
-            }
-            for (int k = fn.first; k < fn.first + fn.count; k++) {
-                const FarTri ft = load_far_tri(S.bv.far_tris, k);
-                const bool cand = may && far_candidate(ft, fr, o, d);
-                if (__ballot(cand) == 0) continue;
-                const rt_prim P = load_prim_scalar(S.prims, (int)ft.id);
-                float t, a, b, g;
-                if (cand && prim_test_closest(P, o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, (int)ft.id, found, h)) {
-                    found = true;
-                    changed = true;
-                    h.t = t; h.a = a; h.b = b; h.g = g; h.prim = (int)ft.id;
-                }
-            }
-        }
+        if (far_tree_closest_wave(S, live && !gl, o, d, fr, h, found, stk[wave])) changed = true;
         if (changed) {
             W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
             W.hit_prim[node] = h.prim;
@@ -2695,25 +2863,44 @@ __global__ void far_chunk_count_kernel(DevWork W, uint32_t nseg) {
 }
 // One descriptor per work item (sorted rays [x, y), the cell list's first
 // entry z and length w; w = ~0: a plane-tree segment), so the cell pass reads
-// one record per item instead of a chain of lookups.
+// one record per item instead of a chain of lookups. A lane per segment writes
+// its first item; the rare segments of more than 64 rays (a directional
+// light's shadow rays all share a cell) get their other items from the whole
+// wave. (A wave per segment: 265-350 us for the AO queue's ~3M segments.)
 __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, uint32_t n) {
     const int lane = threadIdx.x & 63;
     const int shift = 24 - 2 * S.bv.grid_log2;
-    for (uint32_t k = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < nseg;
-         k += gridDim.x * (blockDim.x / 64)) {
-        const uint32_t b = W.far_wofs[k], c = W.far_keys_alt[k], key = W.far_keys[k];
-        const uint32_t s0 = W.far_seg_off[k], s1 = k + 1 < nseg ? W.far_seg_off[k + 1] : n;
-        uint32_t lb = 0, lw = 0xffffffffu;
-        if (key < RT_KEY_TREE) {
-            const uint32_t cell = key >> shift;
-            lb = S.bv.grid_start[cell];
-            lw = S.bv.grid_start[cell + 1] - lb;
+    for (uint32_t base = (blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64u; base < nseg;
+         base += gridDim.x * blockDim.x) {
+        const uint32_t k = base + (uint32_t)lane;
+        const bool valid = k < nseg;
+        uint32_t b = 0, c = 0, s0 = 0, s1 = 0, lb = 0, lw = 0xffffffffu;
+        if (valid) {
+            b = W.far_wofs[k];
+            c = W.far_keys_alt[k];
+            const uint32_t key = W.far_keys[k];
+            s0 = W.far_seg_off[k];
+            s1 = k + 1 < nseg ? W.far_seg_off[k + 1] : n;
+            if (key < RT_KEY_TREE) {
+                const uint32_t cell = key >> shift;
+                lb = S.bv.grid_start[cell];
+                lw = S.bv.grid_start[cell + 1] - lb;
+            }
+            W.far_work[b] = make_uint4(s0, s1 - s0 < 64u ? s1 : s0 + 64u, lb, lw);
+            if (k == nseg - 1) W.far_seg_n[1] = b + c;
         }
-        for (uint32_t j = lane; j < c; j += 64) {
-            const uint32_t r0 = s0 + 64u * j;
-            W.far_work[b + j] = make_uint4(r0, s1 - r0 < 64u ? s1 : r0 + 64u, lb, lw);
+        uint64_t big = __ballot(valid && c > 1u);
+        while (big) {
+            const int src = __ffsll((unsigned long long)big) - 1;
+            big &= big - 1;
+            const uint32_t bb = (uint32_t)__shfl((int)b, src), cc = (uint32_t)__shfl((int)c, src);
+            const uint32_t ss0 = (uint32_t)__shfl((int)s0, src), ss1 = (uint32_t)__shfl((int)s1, src);
+            const uint32_t llb = (uint32_t)__shfl((int)lb, src), llw = (uint32_t)__shfl((int)lw, src);
+            for (uint32_t j = 1u + (uint32_t)lane; j < cc; j += 64u) {
+                const uint32_t r0 = ss0 + 64u * j;
+                W.far_work[bb + j] = make_uint4(r0, ss1 - r0 < 64u ? ss1 : r0 + 64u, llb, llw);
+            }
         }
-        if (k == nseg - 1 && lane == 0) W.far_seg_n[1] = b + c;
     }
 }
 
@@ -2722,7 +2909,8 @@ __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, ui
 // far_keys / far_vals -- the sort's inputs, free now -- and the exclusive scan
 // of the run lengths), their chunks of <= 64 rays as work items, then
 // far_cell_any_kernel. One host read (the segment count).
-static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s) {
+static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s,
+                                   bool closest = false) {
     size_t tmp = W.sort_tmp_bytes;
     RT_STEP("far queue segments");
     hipError_t e = hipcub::DeviceRunLengthEncode::Encode(W.sort_tmp, tmp, W.far_keys_alt, W.far_keys, W.far_vals,
@@ -2738,8 +2926,7 @@ static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t
     tmp = W.sort_tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(W.sort_tmp, tmp, W.far_keys_alt, W.far_wofs, (int)nseg, s)) != hipSuccess)
         return e;
-    hipLaunchKernelGGL(far_chunk_expand_kernel, dim3(grid_for((uint64_t)nseg * 64, 16384)), dim3(TB), 0, s, S, W, nseg,
-                       n);
+    hipLaunchKernelGGL(far_chunk_expand_kernel, dim3(grid_for(nseg, 16384)), dim3(TB), 0, s, S, W, nseg, n);
     RT_STEP("far cell pass");
 #ifdef RT580_DIAGNOSTICS
     {
@@ -2751,7 +2938,10 @@ static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t
     }
 #endif
     const dim3 cgrid(grid_for((uint64_t)(n / 64 + nseg) * 64, 16384));
-    hipLaunchKernelGGL(far_cell_any_kernel, cgrid, dim3(TB), 0, s, S, W, n, flag);
+    if (closest)
+        hipLaunchKernelGGL(far_cell_closest_kernel, cgrid, dim3(TB), 0, s, S, W);
+    else
+        hipLaunchKernelGGL(far_cell_any_kernel, cgrid, dim3(TB), 0, s, S, W, n, flag);
 #ifdef RT580_DIAGNOSTICS
     {
         uint32_t nw[2] = {0, 0};
@@ -3092,7 +3282,9 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 if (nq) {
                     RT_STEP("trace far pass");
                     const int fm = far_mode(nq);
-                    if (fm == 1 || fm == 4) {
+                    if (fm == 4 && far_closest_u() == 0) {
+                        if ((e = launch_far_cells(S, W, nq, nullptr, s, /*closest=*/true)) != hipSuccess) return e;
+                    } else if (fm == 1 || fm == 4) {
                         const int u = far_closest_u();
                         if (u == 4)
                             hipLaunchKernelGGL(far_closest_kernel<4>, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);

@@ -37,6 +37,7 @@ const long kTraceWpe[] = {4, 6, 8, -1};
 const long kNearWpe[] = {0, 5, 6, 8, -1};
 const long kFarMode[] = {0, 1, 2, 3, 4, -1};
 const long kFarU[] = {1, 2, 4, -1};
+const long kFarCU[] = {0, 1, 2, 4, -1};
 const long k0123[] = {0, 1, 2, 3, -1};
 const long k148[] = {1, 4, 8, -1};
 // the AO kernel flavours launch_ao_small instantiates (rt_kernels.hip)
@@ -64,6 +65,7 @@ const Knob kKnobs[] = {
     {"RT580_MULTI_TRANSPORT", STRING_SET, 0, 0, nullptr, kTransport},
     {"RT580_GPUS", INT_RANGE, 1, 16, nullptr, nullptr},
     {"RT580_REPLAY", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_GRAPH", INT_SET, 0, 0, k01, nullptr},
     // rt_bvh.cpp
     {"RT580_LEAF_MAX", INT_RANGE, 1, 8, nullptr, nullptr},
     {"RT580_BVH_INFLATE", FLOAT_NONNEG, 0, 0, nullptr, nullptr},
@@ -81,7 +83,7 @@ const Knob kKnobs[] = {
     {"RT580_BRUTE_RAYS", INT_SET, 0, 0, k148, nullptr},
     {"RT580_FAR_MODE", INT_SET, 0, 0, kFarMode, nullptr},
     {"RT580_FAR_U", INT_SET, 0, 0, kFarU, nullptr},
-    {"RT580_FAR_CLOSEST_U", INT_SET, 0, 0, kFarU, nullptr},
+    {"RT580_FAR_CLOSEST_U", INT_SET, 0, 0, kFarCU, nullptr},
     {"RT580_SORT_BITS", INT_SET, 0, 0, k01, nullptr},
     {"RT580_DEEP_GRID", INT_RANGE, 64, 65536, nullptr, nullptr},
     {"RT580_AO_GRID", INT_RANGE, 256, 1 << 20, nullptr, nullptr},

@@ -118,6 +118,18 @@ struct State {
     rt_render_params lat_params{};
     uint64_t lat_gen = ~0ull;
     int lat_row = -1;
+    // render_split's frame as a HIP graph per slot: one launch instead of the
+    // ~40 enqueue calls. Captured on the second identical call of a slot (the
+    // first allocates), replayed while the key holds.
+    struct FrameGraph {
+        rt_render_params p{};
+        uint64_t gen = ~0ull, buf_gen = ~0ull;
+        const void* fb = nullptr;
+        int seen = 0;
+        hipGraphExec_t exec = nullptr;
+    };
+    std::array<FrameGraph, 4> fgraph{};
+    bool graphs_off = false;
     uint32_t* far_count_host = nullptr;  // pinned: counts read on the host (rt_kernels.hip read_counts)
     // count schedules of the trace phase and of the AO phase (rt_kernels.h
     // CountSchedule), each valid for the frame of its key
@@ -301,8 +313,13 @@ int sync_all() {
     return RT_SUCCESS;
 }
 
+// Bumped by every workspace (re)allocation and release: a captured frame
+// graph (render_split) holds the buffer addresses of its capture.
+uint64_t g_buf_gen = 0;
+
 int ensure(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return RT_SUCCESS;
+    g_buf_gen++;
     if (b.p) {  // frames in flight may still read the old buffer
         if (device_sync("before a workspace buffer is resized")) return RT_FAILURE;
         HIP_TRY(hipFree(b.p));
@@ -317,6 +334,7 @@ int ensure(DevBuf& b, size_t bytes) {
 }
 
 void release(DevBuf& b) {
+    if (b.p) g_buf_gen++;
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
@@ -1222,32 +1240,12 @@ static int copy_out(const int16_t* dev, int16_t* fb_out, size_t bytes, hipStream
     return RT_SUCCESS;
 }
 
-// rt_gpu_render's latency path for small-scene whole frames into a registered
-// host framebuffer: after the trace and the AO-call numbering, the frame's
-// rows split in two at row r (the calls of rows [0, r) are the first ones of
-// the serial RNG stream, so the split needs no other change): AO of the first
-// part, then -- on a second stream -- its resolve and copy to the host while
-// the second part's AO runs. Same kernels, same bytes. done = false when the
-// frame does not qualify (the caller takes the plain path).
-static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) {
-    done = false;
+// render_split's enqueue on stream s (both halves; the caller ends the slot).
+static int enqueue_split(const rt_render_params* p, int16_t* fb_out, hipStream_t s) {
     const int H = p->height, W = p->width;
     const size_t bytes = (size_t)H * W * 6;
-    if (!g.pipeline || H < 2 || p->row_begin != 0 || p->row_step != 1 || p->row_end != H ||
-        !host_registered(fb_out, bytes) || frame_uses_bvh(p))
-        return RT_SUCCESS;
     DevFrame f = dev_frame(p, 0, 1, H);
     const DevScene sc = dev_scene(p);
-    if (!ao_calls_supported(sc, f)) return RT_SUCCESS;
-    // only a (params, scene) whose node capacity is verified (no retry here)
-    g.traced_rows[0] = 0;
-    g.traced_rows[1] = 1;
-    g.traced_rows[2] = H;
-    if (!(g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0 &&
-          std::memcmp(g.verified_rows, g.traced_rows, sizeof g.traced_rows) == 0))
-        return RT_SUCCESS;
-    if (begin_slot(false, 2) || begin_frame()) return RT_FAILURE;
-    const hipStream_t s = fs();
     HIP_TRY(hipEventRecord(g.ev[EV_START], s));
     if (trace_rows(p, 0, 1, H)) return RT_FAILURE;
     if (ensure(SL.fb, bytes)) return RT_FAILURE;
@@ -1291,6 +1289,78 @@ static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) 
     HIP_TRY(hipMemcpyAsync(fb_out + (size_t)p0 * 3, out + (size_t)p0 * 3, (size_t)(np - p0) * 6,
                            hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamWaitEvent(s, g.aux_done, 0));  // the slot is free once both halves are done
+    return RT_SUCCESS;
+}
+
+// rt_gpu_render's latency path for small-scene whole frames into a registered
+// host framebuffer: after the trace and the AO-call numbering, the frame's
+// rows split in two at row r (the calls of rows [0, r) are the first ones of
+// the serial RNG stream, so the split needs no other change): AO of the first
+// part, then -- on a second stream -- its resolve and copy to the host while
+// the second part's AO runs. Same kernels, same bytes. done = false when the
+// frame does not qualify (the caller takes the plain path).
+static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) {
+    done = false;
+    const int H = p->height, W = p->width;
+    const size_t bytes = (size_t)H * W * 6;
+    if (!g.pipeline || H < 2 || p->row_begin != 0 || p->row_step != 1 || p->row_end != H ||
+        !host_registered(fb_out, bytes) || frame_uses_bvh(p))
+        return RT_SUCCESS;
+    DevFrame f = dev_frame(p, 0, 1, H);
+    const DevScene sc = dev_scene(p);
+    if (!ao_calls_supported(sc, f)) return RT_SUCCESS;
+    // only a (params, scene) whose node capacity is verified (no retry here)
+    g.traced_rows[0] = 0;
+    g.traced_rows[1] = 1;
+    g.traced_rows[2] = H;
+    if (!(g.verified_valid && g.verified_gen == g.scene_gen && std::memcmp(&g.verified, p, sizeof *p) == 0 &&
+          std::memcmp(g.verified_rows, g.traced_rows, sizeof g.traced_rows) == 0))
+        return RT_SUCCESS;
+    if (begin_slot(false, 2) || begin_frame()) return RT_FAILURE;
+    const hipStream_t s = fs();
+    // As a graph once the split row is known and the slot has run this exact
+    // frame (its buffers exist); not while profiling (per-frame event sets)
+    // or for mt19937 (its stream is prepared on the host per call).
+    State::FrameGraph& G = g.fgraph[g.cur];
+    const bool key = G.gen == g.scene_gen && G.buf_gen == g_buf_gen && G.fb == fb_out &&
+                     std::memcmp(&G.p, p, sizeof *p) == 0;
+    static int graphs = -1;  // RT580_GRAPH=0: plain enqueue (A/B)
+    if (graphs < 0) {
+        const char* e = std::getenv("RT580_GRAPH");
+        graphs = e ? std::atoi(e) : 1;
+    }
+    const bool graph_ok = graphs && !g.graphs_off && !g.profiling && p->rng_engine != RT_RNG_MT19937 &&
+                          g.lat_gen == g.scene_gen && std::memcmp(&g.lat_params, p, sizeof *p) == 0;
+    if (graph_ok && key && G.exec) {
+        HIP_TRY(hipGraphLaunch(G.exec, s));
+    } else if (graph_ok && key && G.seen) {
+        if (G.exec) (void)hipGraphExecDestroy(G.exec);
+        G.exec = nullptr;
+        HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+        const int rc = enqueue_split(p, fb_out, s);
+        hipGraph_t gr = nullptr;
+        const hipError_t ec = hipStreamEndCapture(s, &gr);
+        hipError_t ei = hipErrorUnknown;
+        if (rc == RT_SUCCESS && ec == hipSuccess && gr) ei = hipGraphInstantiate(&G.exec, gr, nullptr, nullptr, 0);
+        if (gr) (void)hipGraphDestroy(gr);
+        if (ei != hipSuccess) {  // no graphs on this device/runtime: the plain enqueue from now on
+            (void)hipGetLastError();
+            G.exec = nullptr;
+            g.graphs_off = true;
+            if (enqueue_split(p, fb_out, s)) return RT_FAILURE;
+        } else {
+            HIP_TRY(hipGraphLaunch(G.exec, s));
+        }
+    } else {
+        if (enqueue_split(p, fb_out, s)) return RT_FAILURE;
+        G.p = *p;
+        G.gen = g.scene_gen;
+        G.buf_gen = g_buf_gen;
+        G.fb = fb_out;
+        G.seen = 1;
+        if (G.exec) (void)hipGraphExecDestroy(G.exec);
+        G.exec = nullptr;
+    }
     if (end_slot()) return RT_FAILURE;
     HIP_TRY(hipStreamSynchronize(s));
     done = true;

@@ -506,13 +506,15 @@ def roofline(workload, k_ms, k_launches, k_rays, iso=None):
     return res
 
 
-def render_latency(lib, rt580, params, torch, n=3):
+def render_latency(lib, rt580, params, torch, n=5, warm=4):
     """Blocking rt_gpu_render (what Render() calls): first launch -> int16
     framebuffer on the host (SURVEY §8d ms/frame), excluding scene load/upload
     and the PPM write. The host framebuffer is page-locked once
     (rt_gpu_host_register), as the class surface does with its own, so the
     frame lands in it with one DMA. Mean of n calls after the timed region,
-    after one untimed call."""
+    after `warm` untimed calls (a small-scene frame is captured as a HIP graph
+    on each slot's second call, rt_shim.cpp render_split: the steady state of
+    repeated renders)."""
     import numpy as np
     # page-aligned and page-rounded, like the class surface's own framebuffer
     # (a registration must not share pages with other allocations)
@@ -523,7 +525,8 @@ def render_latency(lib, rt580, params, torch, n=3):
     host = raw[off:off + span].view(np.int16)[:n_val]
     rt580.check(lib.rt_gpu_host_register(host.ctypes.data, span), "rt_gpu_host_register")
     try:
-        rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
+        for _ in range(warm):
+            rt580.check(lib.rt_gpu_render(ctypes.byref(params), host.ctypes.data), "rt_gpu_render")
         times = []
         for _ in range(n):
             torch.cuda.synchronize()

@@ -230,3 +230,41 @@ def test_accel_toggle_on_repeated_frame_keeps_rendering():
     finally:
         lib.rt_gpu_set_accel(1)
     rt.close()
+
+
+def _registered(n_val):
+    """A page-aligned, page-rounded int16 host buffer of n_val values (a
+    registration must not share pages with other allocations)."""
+    span = (n_val * 2 + 4095) // 4096 * 4096
+    raw = np.zeros(span + 4096, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    return raw, raw[off:off + span].view(np.int16)[:n_val], span
+
+
+def test_graph_replayed_small_frames_match_oracle():
+    """The blocking small-scene rt_gpu_render into a registered framebuffer
+    (render_split) runs each slot's frame as a HIP graph from the slot's second
+    identical call on (rt_shim.cpp FrameGraph). Every call -- plain, captured,
+    replayed, after a parameter change (new key) and into another registered
+    buffer (new key) -- equals the CPU restatement."""
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    scene, w, h = "simpleSphereSceneAO.json", 64, 48
+    cfg = [(4, 8), (3, 4)]
+    want = [helpers.oracle_render(scene, w, h, d, a, True)[0] for d, a in cfg]
+    rts = [_params(scene, w, h, d, a, helpers.ASSETS_ROOT) for d, a in cfg]
+    s = rts[0][0].scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    bufs = [_registered(w * h * 3) for _ in range(2)]
+    for _, buf, span in bufs:
+        rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "host_register")
+    try:
+        # (config, buffer) per call: 6 calls cover plain, capture and replay on both slots
+        for k, b in [(0, 0)] * 6 + [(1, 0)] * 5 + [(0, 1)] * 5 + [(0, 0)] * 2:
+            buf = bufs[b][1]
+            buf[:] = -1
+            rt580.check(lib.rt_gpu_render(ctypes.byref(rts[k][1]), buf.ctypes.data), "render")
+            assert np.array_equal(buf.reshape(h, w, 3), want[k]), "config %d buffer %d differs" % (k, b)
+    finally:
+        for _, buf, _ in bufs:
+            lib.rt_gpu_host_unregister(buf.ctypes.data)
