@@ -694,4 +694,54 @@ void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells) {
     out.grid_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+void coarsen_dir_grid(BvhBuild& out) {
+    out.grid2_start.clear();
+    out.grid2_items.clear();
+    if (out.grid_log2 < 2 || out.grid_start.empty()) return;
+    const int L = out.grid_log2, M = 1 << L, Mc = M / 2;
+    const size_t nc = (size_t)Mc * Mc;
+    unsigned nt = std::thread::hardware_concurrency();
+    if (nt < 1) nt = 1;
+    if (nt > 16) nt = 16;
+    // per thread: a band of coarse rows, its merged lists back to back
+    std::vector<std::vector<uint32_t>> items(nt), lens(nt);
+    {
+        std::vector<std::thread> th;
+        for (unsigned w = 0; w < nt; w++)
+            th.emplace_back([&, w] {
+                const int i0 = (int)((int64_t)Mc * w / nt), i1 = (int)((int64_t)Mc * (w + 1) / nt);
+                std::vector<uint32_t> u;
+                for (int ic = i0; ic < i1; ic++)
+                    for (int jc = 0; jc < Mc; jc++) {
+                        u.clear();
+                        for (int a = 0; a < 2; a++)
+                            for (int b = 0; b < 2; b++) {
+                                const size_t c = ((size_t)(2 * ic + a) << L) | (size_t)(2 * jc + b);
+                                u.insert(u.end(), out.grid_items.begin() + out.grid_start[c],
+                                         out.grid_items.begin() + out.grid_start[c + 1]);
+                            }
+                        std::sort(u.begin(), u.end());
+                        u.erase(std::unique(u.begin(), u.end()), u.end());
+                        items[w].insert(items[w].end(), u.begin(), u.end());
+                        lens[w].push_back((uint32_t)u.size());
+                    }
+            });
+        for (auto& t : th) t.join();
+    }
+    out.grid2_start.assign(nc + 1, 0);
+    uint64_t total = 0;
+    size_t c = 0;
+    for (unsigned w = 0; w < nt; w++)
+        for (uint32_t n : lens[w]) {
+            out.grid2_start[c++] = (uint32_t)total;
+            total += n;
+        }
+    out.grid2_start[nc] = (uint32_t)total;
+    out.grid2_items.reserve(total);
+    for (unsigned w = 0; w < nt; w++) {
+        out.grid2_items.insert(out.grid2_items.end(), items[w].begin(), items[w].end());
+        std::vector<uint32_t>().swap(items[w]);
+    }
+}
+
 }  // namespace rt580

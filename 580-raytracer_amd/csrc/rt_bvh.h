@@ -135,6 +135,11 @@ struct BvhBuild {
     std::vector<uint32_t> grid_items;
     std::vector<uint32_t> grid_always;
     double grid_ms = 0.0;
+    // The same grid at half the resolution per axis (coarsen_dir_grid): a cell's
+    // list is the union of its four children's, for frames of few rays (rows of
+    // a K-way split), whose cells would hold few rays each.
+    std::vector<uint32_t> grid2_start;  // [(M/2)^2 + 1]
+    std::vector<uint32_t> grid2_items;
 };
 
 // Build over prims[0..n). Returns false if there are no triangles or a tree
@@ -147,6 +152,13 @@ void collapse_bvh4(BvhBuild& out);
 // Build the far-search direction grid over out.far_tris (after build_bvh; the
 // query side is rt_isect.h grid_cell / far_any / far_closest).
 void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells);
+
+// out.grid2_* from out.grid_* (after build_dir_grid): coarse cell (i, j) lists
+// the sorted union of fine cells (2i + a, 2j + b). grid_cell(d, L - 1) is
+// grid_cell(d, L)'s (i >> 1, j >> 1) (power-of-two scalings of one float), and
+// a direction of the coarse cell lies in one of its children, whose list is
+// conservative: so is the union.
+void coarsen_dir_grid(BvhBuild& out);
 
 // Render-time guard for the camera (float ranges only; the bounds hold for any origin).
 bool bvh_usable(const BvhBuild& b, const float cam_from[3]);

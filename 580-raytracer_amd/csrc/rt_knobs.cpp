@@ -60,6 +60,7 @@ const Knob kKnobs[] = {
     {"RT580_SMALL_SLOTS", INT_SET, 0, 0, k234, nullptr},
     {"RT580_CHUNK_LOG2", INT_RANGE, 6, 27, nullptr, nullptr},
     {"RT580_GRID_LOG2", INT_RANGE, 0, 12, nullptr, nullptr},
+    {"RT580_GRID_COARSE_PX", INT_RANGE, 0, 1L << 31, nullptr, nullptr},
     {"RT580_BVH4", INT_SET, 0, 0, k01, nullptr},
     {"RT580_CALL_HINT", INT_SET, 0, 0, k01, nullptr},
     {"RT580_MULTI_TRANSPORT", STRING_SET, 0, 0, nullptr, kTransport},

@@ -82,9 +82,11 @@ struct State {
     bool have_scene = false;
     // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
     DevBuf bvh_nodes, bvh_nodes4, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always, scan_prims;
+    DevBuf grid2_start, grid2_items;  // the half-resolution grid (coarsen_dir_grid)
     BvhBuild bvh;
     bool bvh_ok = false;
     int grid_log2 = 0, grid_n_always = 0;  // far-search direction grid (uploaded; host copy dropped)
+    bool grid2 = false;                    // grid2_* uploaded (log2 = grid_log2 - 1)
     int accel = RT_ACCEL_AUTO;
     bool last_accel = false;
     uint64_t scene_gen = 0;
@@ -358,7 +360,22 @@ int check_params(const rt_render_params* p) {
     return RT_SUCCESS;
 }
 
-DevScene dev_scene(const rt_render_params* p) {
+// Frames of fewer pixels than this use the half-resolution direction grid:
+// fewer rays per cell there, and a cell's list is read once per chunk of its
+// rays. North-star frame's K-way row shares (rank 1), fine -> coarse: K = 2
+// 22.45 -> 21.62 ms, 4: 13.40 -> 12.32, 8: 8.66 -> 7.55; the whole frame (2.07M
+// pixels) keeps the fine grid (38.8 vs 39.1 ms). RT580_GRID_COARSE_PX (0: never).
+long grid_coarse_px() {
+    static long v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("RT580_GRID_COARSE_PX");
+        v = e ? std::atol(e) : 1572864L;
+    }
+    return v;
+}
+
+// n_rows: the frame's rows (selects the direction grid; -1: the fine one).
+DevScene dev_scene(const rt_render_params* p, int n_rows) {
     DevScene s;
     std::memset(&s, 0, sizeof s);
     s.prims = (const rt_prim*)g.prims.p;
@@ -398,11 +415,12 @@ DevScene dev_scene(const rt_render_params* p) {
     }
 #endif
     v.scale = g.bvh.scale;
-    v.grid_start = (const uint32_t*)g.grid_start.p;
-    v.grid_items = (const uint32_t*)g.grid_items.p;
+    const bool coarse = g.grid2 && n_rows >= 0 && (long)n_rows * p->width < grid_coarse_px();
+    v.grid_start = (const uint32_t*)(coarse ? g.grid2_start.p : g.grid_start.p);
+    v.grid_items = (const uint32_t*)(coarse ? g.grid2_items.p : g.grid_items.p);
     v.grid_always = (const uint32_t*)g.grid_always.p;
     v.n_always = g.grid_n_always;
-    v.grid_log2 = g.grid_log2;
+    v.grid_log2 = coarse ? g.grid_log2 - 1 : g.grid_log2;
     v.grid_r = g.bvh.grid_r;
     return s;
 }
@@ -786,7 +804,7 @@ int check_replay(Slot& sl) {
 int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_rows) {
     if (ensure_work(p, n_rows)) return RT_FAILURE;  // (launch_trace zeroes the per-frame counters)
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
-    const DevScene sc = dev_scene(p);
+    const DevScene sc = dev_scene(p, n_rows);
     g.last_accel = sc.use_bvh != 0;
     g.traced_rows[0] = row_begin;
     g.traced_rows[1] = row_step;
@@ -883,7 +901,7 @@ hipError_t wait_previous_ao() {
 int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_rows, const uint64_t* row_base_global,
                int16_t* fb_out) {
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
-    const DevScene sc = dev_scene(p);
+    const DevScene sc = dev_scene(p, n_rows);
     HIP_TRY(launch_rank(sc, f, dev_work(), row_base_global, fs()));
     HIP_TRY(hipEventRecord(g.ev[EV_RANK], fs()));
     if (prepare_mt_stream(p, row_base_global, n_rows)) return RT_FAILURE;
@@ -945,7 +963,8 @@ int check_capacity(const rt_render_params* p, bool& retry) {
 std::vector<DevBuf State::*> scene_bufs() {
     return {&State::prims, &State::shade, &State::mats, &State::lights, &State::bvh_nodes, &State::bvh_nodes4,
             &State::bvh_prims, &State::bvh_ids, &State::far_nodes, &State::far_tris, &State::brute,
-            &State::grid_start, &State::grid_items, &State::grid_always, &State::scan_prims};
+            &State::grid_start, &State::grid_items, &State::grid_always, &State::scan_prims, &State::grid2_start,
+            &State::grid2_items};
 }
 
 // The scene of context `src` into the current context without building
@@ -971,6 +990,7 @@ int clone_scene(int src) {
     g.bvh = c.bvh;  // the host copy keeps only the small arrays (nodes, far nodes, brute list)
     g.bvh_ok = c.bvh_ok;
     g.grid_log2 = c.grid_log2;
+    g.grid2 = c.grid2;
     g.grid_n_always = c.grid_n_always;
     g.n_prims = c.n_prims;
     g.n_lights = c.n_lights;
@@ -1092,6 +1112,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     g.bvh_ok = false;
     release(g.scan_prims);
     g.grid_log2 = g.grid_n_always = 0;
+    g.grid2 = false;
     if (s->n_prims > 64) {
         g.bvh_ok = build_bvh(s->prims, s->n_prims, g.bvh);
         // far-search direction grid: 2048^2 cells (field100k: 19.4 candidates
@@ -1101,6 +1122,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         int glog2 = 11;
         if (const char* e = std::getenv("RT580_GRID_LOG2")) glog2 = std::atoi(e);
         if (g.bvh_ok && glog2 > 0 && glog2 <= 12) build_dir_grid(s->prims, g.bvh, glog2);
+        if (g.bvh_ok && grid_coarse_px() > 0) coarsen_dir_grid(g.bvh);
         // the 4-wide form for the any-hit queries (AO, shadows); RT580_BVH4=0: binary only
         const char* b4 = std::getenv("RT580_BVH4");
         if (g.bvh_ok && !(b4 && std::atoi(b4) == 0)) collapse_bvh4(g.bvh);
@@ -1114,7 +1136,9 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
              upload_vec(g.brute, g.bvh.brute, "the brute-force list") ||
              upload_vec(g.grid_start, g.bvh.grid_start, "the direction-grid offsets") ||
              upload_vec(g.grid_items, g.bvh.grid_items, "the direction-grid lists") ||
-             upload_vec(g.grid_always, g.bvh.grid_always, "the direction-grid always-list")))
+             upload_vec(g.grid_always, g.bvh.grid_always, "the direction-grid always-list") ||
+             upload_vec(g.grid2_start, g.bvh.grid2_start, "the half-resolution grid offsets") ||
+             upload_vec(g.grid2_items, g.bvh.grid2_items, "the half-resolution grid lists")))
             return RT_FAILURE;
         if (g.bvh_ok && !g.bvh.far_nodes.empty()) {
             // The any-hit scan order of far-origin rays (far_scan_kernel): a fixed
@@ -1129,6 +1153,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
             if (upload_vec(g.scan_prims, perm, "the shuffled scan order")) return RT_FAILURE;
         }
         g.grid_log2 = g.bvh.grid_start.empty() ? 0 : g.bvh.grid_log2;
+        g.grid2 = g.grid_log2 > 1 && !g.bvh.grid2_start.empty();
         g.grid_n_always = (int)g.bvh.grid_always.size();
         // the device needs only the arrays; keep the host copy small
         g.bvh.prims = std::vector<rt_prim>();
@@ -1139,6 +1164,8 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         g.bvh.grid_start = std::vector<uint32_t>();
         g.bvh.grid_items = std::vector<uint32_t>();
         g.bvh.grid_always = std::vector<uint32_t>();
+        g.bvh.grid2_start = std::vector<uint32_t>();
+        g.bvh.grid2_items = std::vector<uint32_t>();
     }
     if (device_sync("at the end of the scene upload")) return RT_FAILURE;
     g.n_prims = s->n_prims;
@@ -1245,7 +1272,7 @@ static int enqueue_split(const rt_render_params* p, int16_t* fb_out, hipStream_t
     const int H = p->height, W = p->width;
     const size_t bytes = (size_t)H * W * 6;
     DevFrame f = dev_frame(p, 0, 1, H);
-    const DevScene sc = dev_scene(p);
+    const DevScene sc = dev_scene(p, H);
     HIP_TRY(hipEventRecord(g.ev[EV_START], s));
     if (trace_rows(p, 0, 1, H)) return RT_FAILURE;
     if (ensure(SL.fb, bytes)) return RT_FAILURE;
@@ -1307,7 +1334,7 @@ static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) 
         !host_registered(fb_out, bytes) || frame_uses_bvh(p))
         return RT_SUCCESS;
     DevFrame f = dev_frame(p, 0, 1, H);
-    const DevScene sc = dev_scene(p);
+    const DevScene sc = dev_scene(p, H);
     if (!ao_calls_supported(sc, f)) return RT_SUCCESS;
     // only a (params, scene) whose node capacity is verified (no retry here)
     g.traced_rows[0] = 0;
@@ -1645,7 +1672,7 @@ void shutdown_ctx() {
     (void)hipSetDevice(g.device);
     if (sync_all() || device_sync("at shutdown"))
         std::fprintf(stderr, "rt_gpu: shutting down after a device error (%s)\n", g_err);
-    for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always})
+    for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always, &g.grid2_start, &g.grid2_items})
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute,
                       &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims})

@@ -268,3 +268,43 @@ def test_graph_replayed_small_frames_match_oracle():
     finally:
         for _, buf, _ in bufs:
             lib.rt_gpu_host_unregister(buf.ctypes.data)
+
+
+_GRID_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import helpers
+rt580 = helpers.rt580()
+root = helpers.synthetic_root(sys.argv[2])
+ok = []
+for d, a in [(4, 16), (2, 8)]:
+    rt = rt580.Raytracer(64, 36, root)
+    assert rt.LoadSceneJSON(sys.argv[2] + ".json") == 0
+    rt.set_depth(d)
+    rt.set_ao(a, True)
+    assert rt.Render("") == 0
+    ref, _ = helpers.oracle_render(sys.argv[2] + ".json", 64, 36, d, a, True, root=root)
+    ok.append(bool(np.array_equal(rt.framebuffer(), ref)))
+    rt.close()
+print("MATCH", ok)
+"""
+
+
+@pytest.mark.parametrize("scene", ["cornell10k", "field100k"])
+def test_fine_direction_grid_small_frames_match_oracle(tmp_path, scene):
+    """Frames below RT580_GRID_COARSE_PX pixels (every other GPU test's frame)
+    take the half-resolution direction grid; the fine grid is the whole
+    1080p-and-up frames'. RT580_GRID_COARSE_PX=0 forces the fine grid onto
+    small frames: both grids answer as the oracle."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, RT580_GRID_COARSE_PX="0")
+    script = tmp_path / "child.py"
+    script.write_text(_GRID_CHILD)
+    r = subprocess.run([sys.executable, str(script), os.path.dirname(os.path.abspath(__file__)), scene], env=env,
+                       capture_output=True, text=True, timeout=280)
+    line = [l for l in r.stdout.splitlines() if l.startswith("MATCH")]
+    assert line, r.stdout + r.stderr
+    assert line[0] == "MATCH [True, True]", line[0]
