@@ -1394,7 +1394,10 @@ ao_late_kernel(DevScene S, DevWork W) {
     }
 }
 
-// (Persistent forms of ao_trace_kernel -- lanes refilled from the chunk as
+// (A wave per late ray, its lanes sharing the ray's traversal stack -- 64
+// entries popped at a time, children pushed with wave prefix sums: correct,
+// but north-star 38.8 -> 56-58 ms; the late rays' frontiers are narrow. Not
+// kept. Persistent forms of ao_trace_kernel -- lanes refilled from the chunk as
 // they finish, per-iteration atomic fetch, static per-wave ranges, or batched
 // fetch with prefetched records -- measured 94 / 137 / 133 ms against 89 ms
 // for this kernel on cornell10k's AO; the SIMD-efficiency model
