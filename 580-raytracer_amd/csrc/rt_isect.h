@@ -723,6 +723,39 @@ RTM_HD int bvh4_any_near_budget(const BvhView& V, rv3 o, rv3 d, const STK& stk, 
     }
 }
 
+// bvh4_any_near_budget that also returns, when undecided (-1), the walk's
+// state: the stack [0, sp) and the entry (c, n) it was about to descend --
+// bvh4_any_near_resume continues from there (the brute list is done).
+template <class STK>
+RTM_HD int bvh4_any_near_budget_state(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, int& sp,
+                                      int32_t& c, int32_t& n) {
+    sp = 0;
+    c = 0;
+    n = 0;  // root (internal)
+    for (int k = 0; k < V.n_brute; k++)
+        if (prim_hit_within(V.all[V.brute[k]], o, d, INFINITY)) return 1;
+    if (!V.has_tree || dir_zero(d)) return 0;
+    const SlabRay sr = slab_ray(V, o, d);
+    for (int visits = 0;; visits++) {
+        if (visits == budget) return -1;
+        if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, n)) return 0;
+        if (bvh4_leaf_hit(V, o, d, INFINITY, c, n)) return 1;
+        if (!bvh4_pop(stk, sp, c, n)) return 0;
+    }
+}
+
+// The rest of an undecided bvh4_any_near_budget_state walk: the same boolean
+// as the whole query (the visits are split, not changed).
+template <class STK>
+RTM_HD bool bvh4_any_near_resume(const BvhView& V, rv3 o, rv3 d, const STK& stk, int sp, int32_t c, int32_t n) {
+    const SlabRay sr = slab_ray(V, o, d);
+    for (;;) {
+        if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, n)) return false;
+        if (bvh4_leaf_hit(V, o, d, INFINITY, c, n)) return true;
+        if (!bvh4_pop(stk, sp, c, n)) return false;
+    }
+}
+
 RTM_HD bool bvh4_any_near(const BvhView& V, rv3 o, rv3 d, float tmax = INFINITY) {
     RT_CNT(brute_tests, V.n_brute);
     for (int k = 0; k < V.n_brute; k++)

@@ -72,6 +72,9 @@ struct RayItem {
 };
 
 // Per-frame device workspace (owned by the shim, sized by capacity).
+constexpr int kLateSaved = 22;               // stack entries a saved late-ray walk may hold
+constexpr int kLateWords = 2 + kLateSaved;  // words per saved walk
+
 struct DevWork {
     NodeRec* nodes;        // [node_cap]
     RayItem* rays;         // [node_cap] (indexed by node id; level 0 is implicit)
@@ -118,6 +121,12 @@ struct DevWork {
     // ao_trace_kernel (item index in the chunk), finished by ao_late_kernel
     uint32_t* ao_late;       // [ao_cap] or null
     uint32_t* ao_late_count; // [1]
+    // the walk state of late rays [0, ao_state_cap) (ao_late_kernel resumes it
+    // instead of starting over): per slot kLateWords words -- the entry about to
+    // be descended (c), n | sp << 8 (~0: not saved, the stack was deeper than
+    // kLateSaved), then the stack [0, sp). Null: late rays start over.
+    uint32_t* ao_state;
+    uint32_t ao_state_cap;
     // provisional closest hits of the tree rays (node id) between the near and
     // far phases of a BVH trace level: (t, alpha, beta, gamma), prim (-1: none)
     float4* hit4;          // [node_cap]

@@ -1322,7 +1322,9 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
         if (BUDGET > 0 && LDS_D > 0) {
             uint32_t stk_a[RT_BVH_STACK + 4 - (LDS_D > 0 ? LDS_D : 0)];
             const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
-            const int r = flag == 1u ? bvh4_any_near_budget(S.bv, o, d, stk, BUDGET) : 0;
+            int sp = 0;
+            int32_t wc = 0, wn = 0;
+            const int r = flag == 1u ? bvh4_any_near_budget_state(S.bv, o, d, stk, BUDGET, sp, wc, wn) : 0;
             hit = r > 0;
             late = r < 0;
             const uint64_t lm = __ballot(late);
@@ -1331,7 +1333,17 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
                 uint32_t base = 0;
                 if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count, (uint32_t)__popcll(lm));
                 base = __shfl(base, leader);
-                if (late) W.ao_late[base + (uint32_t)__popcll(lm & lanemask_lt())] = (uint32_t)i;
+                if (late) {
+                    const uint32_t slot = base + (uint32_t)__popcll(lm & lanemask_lt());
+                    W.ao_late[slot] = (uint32_t)i;
+                    if (slot < W.ao_state_cap) {  // the walk so far, for ao_late_kernel to resume
+                        uint32_t* rec = W.ao_state + (size_t)slot * kLateWords;
+                        rec[0] = (uint32_t)wc;
+                        rec[1] = sp <= kLateSaved ? ((uint32_t)wn | ((uint32_t)sp << 8)) : 0xffffffffu;
+                        if (sp <= kLateSaved)
+                            for (int t = 0; t < sp; t++) rec[2 + t] = stk.get(t);
+                    }
+                }
             }
         } else if (LDS_D > 0) {
             uint32_t stk_a[RT_BVH_STACK + 4 - (LDS_D > 0 ? LDS_D : 0)];
@@ -1387,6 +1399,13 @@ ao_late_kernel(DevScene S, DevWork W) {
                 base = __shfl(base, leader);
                 if (late) W.ao_late[half + base + (uint32_t)__popcll(lm & lanemask_lt())] = i;
             }
+        } else if (SRC == 0 && live && k < W.ao_state_cap && W.ao_state[(size_t)k * kLateWords + 1] != 0xffffffffu) {
+            // ao_trace_kernel's walk of this ray, continued (same boolean)
+            const uint32_t* rec = W.ao_state + (size_t)k * kLateWords;
+            const uint32_t h1 = rec[1];
+            const int sp = (int)(h1 >> 8);
+            for (int t = 0; t < sp; t++) stk.put(t, rec[2 + t]);
+            hit = bvh4_any_near_resume(S.bv, o, d, stk, sp, (int32_t)rec[0], (int32_t)(h1 & 255u));
         } else {
             hit = live && bvh4_any_near_s(S.bv, o, d, stk);
         }
@@ -2472,6 +2491,17 @@ static int far_closest_u() {
 // Largest slice of the scene one wave scans in the split any-hit brute scan.
 constexpr uint32_t kBruteSlice = 4096;
 
+// Waves a split brute scan aims at (ray groups x slices): RT580_BRUTE_WAVES
+// (A/B; the scan of a few far-origin rays is a full-GPU launch either way).
+static uint32_t brute_waves() {
+    static long v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_BRUTE_WAVES");
+        v = e ? atol(e) : 32768;
+    }
+    return (uint32_t)v;
+}
+
 // Far-origin rays per wave of the split brute scans (RT580_BRUTE_RAYS 1, 4, 8).
 static int brute_rays() {
     static int v = -1;
@@ -2496,7 +2526,7 @@ static hipError_t launch_brute_any(const DevScene& S, const DevWork& W, uint32_t
         if (e != hipSuccess) return e;
         const int R = brute_rays();
         const uint32_t ng = (nb + (uint32_t)R - 1) / (uint32_t)R;
-        uint32_t splits = 32768u / ng;
+        uint32_t splits = brute_waves() / ng;
         splits = splits < 1u ? 1u : (splits > 256u ? 256u : splits);
         // slices of at most kBruteSlice records: a ray no record accepts is
         // scanned in parallel slices even when the queue is long (the AO chunks
@@ -3250,7 +3280,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         if ((e = hipMemsetAsync(best, 0xff, (size_t)nb * 8, s)) != hipSuccess) return e;
                         const int R = brute_rays();
                         const uint32_t ng = (nb + (uint32_t)R - 1) / (uint32_t)R;
-                        uint32_t splits = 32768u / ng;
+                        uint32_t splits = brute_waves() / ng;
                         splits = splits < 1u ? 1u : (splits > 512u ? 512u : splits);
                         const dim3 grid(grid_for((uint64_t)ng * splits * 64, 16384));
                         if (R == 8)

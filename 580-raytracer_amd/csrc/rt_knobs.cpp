@@ -78,10 +78,12 @@ const Knob kKnobs[] = {
     {"RT580_AO_SORT", INT_SET, 0, 0, kSort, nullptr},
     {"RT580_AO_BUDGET", INT_RANGE, 0, 64, nullptr, nullptr},
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_AO_RESUME", INT_SET, 0, 0, k01, nullptr},
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
     {"RT580_NEAR_WPE", INT_SET, 0, 0, kNearWpe, nullptr},
     {"RT580_BRUTE_SPLIT", INT_SET, 0, 0, k0123, nullptr},
     {"RT580_BRUTE_RAYS", INT_SET, 0, 0, k148, nullptr},
+    {"RT580_BRUTE_WAVES", INT_RANGE, 256, 1 << 20, nullptr, nullptr},
     {"RT580_FAR_MODE", INT_SET, 0, 0, kFarMode, nullptr},
     {"RT580_FAR_U", INT_SET, 0, 0, kFarU, nullptr},
     {"RT580_FAR_CLOSEST_U", INT_SET, 0, 0, kFarCU, nullptr},

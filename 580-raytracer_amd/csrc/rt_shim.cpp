@@ -45,6 +45,7 @@ struct Slot {
     // BVH frames: the far queue, the AO ray records and the split trace's
     // provisional hits -- per slot, so that consecutive BVH frames overlap
     // like the others (count schedule replay, see trace_rows)
+    DevBuf ao_state;  // saved walks of late AO rays (DevWork::ao_state)
     DevBuf ao_rays, ao_late, ao_late_count, far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count,
         far_seg_off, far_seg_n, far_wofs, far_work, sort_tmp, hit4, hit_prim, shadow;
     uint32_t far_cap = 0, ao_cap = 0;
@@ -564,6 +565,16 @@ DevFrame dev_frame(const rt_render_params* p, int row_begin, int row_step, int n
     return f;
 }
 
+// RT580_AO_RESUME=0 (A/B): late AO rays start their walk over in ao_late_kernel.
+bool ao_resume() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("RT580_AO_RESUME");
+        v = e ? std::atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 DevWork dev_work() {
     DevWork w;
     w.nodes = (NodeRec*)SL.nodes.p;
@@ -602,6 +613,8 @@ DevWork dev_work() {
     w.ao_rays = w.ao_cap ? (float4*)SL.ao_rays.p : nullptr;
     w.ao_late = w.ao_cap ? (uint32_t*)SL.ao_late.p : nullptr;
     w.ao_late_count = w.ao_cap ? (uint32_t*)SL.ao_late_count.p : nullptr;
+    w.ao_state_cap = w.ao_cap && ao_resume() ? w.ao_cap / 16 : 0u;
+    w.ao_state = w.ao_state_cap ? (uint32_t*)SL.ao_state.p : nullptr;
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
     w.hit4 = split ? (float4*)SL.hit4.p : nullptr;
     w.hit_prim = split ? (int32_t*)SL.hit_prim.p : nullptr;
@@ -648,7 +661,7 @@ void set_chunk_log2(int log2) {
     g.chunk_log2 = log2;
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.far_rays, &sl.far_keys, &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.sort_tmp,
-                          &sl.ao_rays, &sl.far_seg_off, &sl.far_wofs, &sl.far_work, &sl.ao_late, &sl.shadow})
+                          &sl.ao_rays, &sl.far_seg_off, &sl.far_wofs, &sl.far_work, &sl.ao_late, &sl.shadow, &sl.ao_state})
             release(*b);
         sl.far_cap = sl.ao_cap = 0;
     }
@@ -687,7 +700,8 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     g.frame_ac = g.bvh_ok ? ac : 0;
     g.frame_fc = 0;
     if (g.bvh_ok && SL.ao_cap < ac) {  // ray records of the split AO pass (ao_trace_kernel)
-        if (ensure(SL.ao_rays, (size_t)ac * 32) || ensure(SL.ao_late, (size_t)ac * 4) || ensure(SL.ao_late_count, 64))
+        if (ensure(SL.ao_rays, (size_t)ac * 32) || ensure(SL.ao_late, (size_t)ac * 4) || ensure(SL.ao_late_count, 64) ||
+            (ao_resume() && ensure(SL.ao_state, (size_t)(ac / 16) * kLateWords * 4)))
             return RT_FAILURE;
         SL.ao_cap = ac;
     }
@@ -1681,7 +1695,7 @@ void shutdown_ctx() {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
                           &sl.row_calls, &sl.row_hits, &sl.row_nodes, &sl.row_base_local, &sl.totals, &sl.call_node,
                           &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.mt_stream, &sl.aofix_items, &sl.aofix_count,
-                          &sl.call_hint, &sl.ao_rays, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
+                          &sl.call_hint, &sl.ao_rays, &sl.ao_state, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
                           &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.far_count, &sl.far_seg_off,
                           &sl.far_seg_n, &sl.far_wofs, &sl.far_work, &sl.sort_tmp, &sl.hit4, &sl.hit_prim, &sl.shadow,
                           &sl.bad})

@@ -225,6 +225,16 @@ int main(int argc, char** argv) {
                         if (q >= 0 && (q == 1) != a4 && bad4.fetch_add(1) < 10)
                             std::printf("MISMATCH4 budget %d ray %ld kind %d: %d vs %d\n", budget, r, kind, q, a4);
                     }
+                    // ... and an undecided walk resumed from its saved state (ao_late_kernel)
+                    for (int budget : {1, 2, 4, 8}) {
+                        uint32_t sa[RT_BVH_STACK + 4];
+                        int sp;
+                        int32_t c, n;
+                        const int q = bvh4_any_near_budget_state(V, o, d, ArrStack{sa}, budget, sp, c, n);
+                        const bool res = q < 0 ? bvh4_any_near_resume(V, o, d, ArrStack{sa}, sp, c, n) : q == 1;
+                        if (res != a4 && bad4.fetch_add(1) < 10)
+                            std::printf("MISMATCH4 resume budget %d ray %ld kind %d: %d vs %d\n", budget, r, kind, res, a4);
+                    }
                     Hit h2, h4;
                     const bool c2 = bvh_closest(V, o, d, h2, false), c4 = bvh4_closest_near(V, o, d, h4);
                     if (c2 != c4 || (c2 && (h2.prim != h4.prim || fbits(h2.t) != fbits(h4.t) || fbits(h2.a) != fbits(h4.a) ||
