@@ -723,6 +723,20 @@ RTM_HD int bvh4_any_near_budget(const BvhView& V, rv3 o, rv3 d, const STK& stk, 
     }
 }
 
+// An undecided walk (stack [0, sp), entry (c, n) next) continued for at most
+// `budget` more leaf visits: 1 hit, 0 no hit, -1 still undecided (state updated).
+template <class STK>
+RTM_HD int bvh4_any_near_resume_budget(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, int& sp,
+                                       int32_t& c, int32_t& n) {
+    const SlabRay sr = slab_ray(V, o, d);
+    for (int visits = 0;; visits++) {
+        if (visits == budget) return -1;
+        if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, n)) return 0;
+        if (bvh4_leaf_hit(V, o, d, INFINITY, c, n)) return 1;
+        if (!bvh4_pop(stk, sp, c, n)) return 0;
+    }
+}
+
 // bvh4_any_near_budget that also returns, when undecided (-1), the walk's
 // state: the stack [0, sp) and the entry (c, n) it was about to descend --
 // bvh4_any_near_resume continues from there (the brute list is done).
@@ -735,13 +749,7 @@ RTM_HD int bvh4_any_near_budget_state(const BvhView& V, rv3 o, rv3 d, const STK&
     for (int k = 0; k < V.n_brute; k++)
         if (prim_hit_within(V.all[V.brute[k]], o, d, INFINITY)) return 1;
     if (!V.has_tree || dir_zero(d)) return 0;
-    const SlabRay sr = slab_ray(V, o, d);
-    for (int visits = 0;; visits++) {
-        if (visits == budget) return -1;
-        if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, n)) return 0;
-        if (bvh4_leaf_hit(V, o, d, INFINITY, c, n)) return 1;
-        if (!bvh4_pop(stk, sp, c, n)) return 0;
-    }
+    return bvh4_any_near_resume_budget(V, o, d, stk, budget, sp, c, n);
 }
 
 // The rest of an undecided bvh4_any_near_budget_state walk: the same boolean

@@ -121,10 +121,11 @@ struct DevWork {
     // ao_trace_kernel (item index in the chunk), finished by ao_late_kernel
     uint32_t* ao_late;       // [ao_cap] or null
     uint32_t* ao_late_count; // [1]
-    // the walk state of late rays [0, ao_state_cap) (ao_late_kernel resumes it
-    // instead of starting over): per slot kLateWords words -- the entry about to
-    // be descended (c), n | sp << 8 (~0: not saved, the stack was deeper than
-    // kLateSaved), then the stack [0, sp). Null: late rays start over.
+    // the walk state of late rays [0, ao_state_cap) of each late queue (region
+    // 0: ao_trace_kernel's, region 1: a budgeted ao_late_kernel's), resumed by
+    // the next level instead of starting over: per slot kLateWords words -- the
+    // entry about to be descended (c), n | sp << 8 (~0: not saved, the stack was
+    // deeper than kLateSaved), then the stack [0, sp). Null: late rays start over.
     uint32_t* ao_state;
     uint32_t ao_state_cap;
     // provisional closest hits of the tree rays (node id) between the near and

@@ -1386,9 +1386,27 @@ ao_late_kernel(DevScene S, DevWork W) {
         const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
         uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
         const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
+        // the walk saved for this ray by the previous level (region SRC of ao_state)
+        int sp = 0;
+        int32_t wc = 0, wn = 0;
+        bool saved = false;
+        if (live && k < W.ao_state_cap) {
+            const uint32_t* rec = W.ao_state + ((size_t)SRC * W.ao_state_cap + k) * kLateWords;
+            const uint32_t h1 = rec[1];
+            if (h1 != 0xffffffffu) {
+                saved = true;
+                sp = (int)(h1 >> 8);
+                wn = (int32_t)(h1 & 255u);
+                wc = (int32_t)rec[0];
+                for (int t = 0; t < sp; t++) stk.put(t, rec[2 + t]);
+            }
+        }
         bool hit, late = false;
         if (BUDGET2 > 0 && two) {
-            const int r = live ? bvh4_any_near_budget(S.bv, o, d, stk, BUDGET2) : 0;
+            int r = 0;
+            if (live)
+                r = saved ? bvh4_any_near_resume_budget(S.bv, o, d, stk, BUDGET2, sp, wc, wn)
+                          : bvh4_any_near_budget_state(S.bv, o, d, stk, BUDGET2, sp, wc, wn);
             hit = r > 0;
             late = r < 0;
             const uint64_t lm = __ballot(late);
@@ -1397,15 +1415,20 @@ ao_late_kernel(DevScene S, DevWork W) {
                 uint32_t base = 0;
                 if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count + 1, (uint32_t)__popcll(lm));
                 base = __shfl(base, leader);
-                if (late) W.ao_late[half + base + (uint32_t)__popcll(lm & lanemask_lt())] = i;
+                if (late) {
+                    const uint32_t slot = base + (uint32_t)__popcll(lm & lanemask_lt());
+                    W.ao_late[half + slot] = i;
+                    if (slot < W.ao_state_cap) {  // region 1: for the last level
+                        uint32_t* rec = W.ao_state + ((size_t)W.ao_state_cap + slot) * kLateWords;
+                        rec[0] = (uint32_t)wc;
+                        rec[1] = sp <= kLateSaved ? ((uint32_t)wn | ((uint32_t)sp << 8)) : 0xffffffffu;
+                        if (sp <= kLateSaved)
+                            for (int t = 0; t < sp; t++) rec[2 + t] = stk.get(t);
+                    }
+                }
             }
-        } else if (SRC == 0 && live && k < W.ao_state_cap && W.ao_state[(size_t)k * kLateWords + 1] != 0xffffffffu) {
-            // ao_trace_kernel's walk of this ray, continued (same boolean)
-            const uint32_t* rec = W.ao_state + (size_t)k * kLateWords;
-            const uint32_t h1 = rec[1];
-            const int sp = (int)(h1 >> 8);
-            for (int t = 0; t < sp; t++) stk.put(t, rec[2 + t]);
-            hit = bvh4_any_near_resume(S.bv, o, d, stk, sp, (int32_t)rec[0], (int32_t)(h1 & 255u));
+        } else if (saved) {  // the saved walk, continued (same boolean)
+            hit = bvh4_any_near_resume(S.bv, o, d, stk, sp, wc, wn);
         } else {
             hit = live && bvh4_any_near_s(S.bv, o, d, stk);
         }

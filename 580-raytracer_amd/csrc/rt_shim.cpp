@@ -701,7 +701,7 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     g.frame_fc = 0;
     if (g.bvh_ok && SL.ao_cap < ac) {  // ray records of the split AO pass (ao_trace_kernel)
         if (ensure(SL.ao_rays, (size_t)ac * 32) || ensure(SL.ao_late, (size_t)ac * 4) || ensure(SL.ao_late_count, 64) ||
-            (ao_resume() && ensure(SL.ao_state, (size_t)(ac / 16) * kLateWords * 4)))
+            (ao_resume() && ensure(SL.ao_state, 2 * (size_t)(ac / 16) * kLateWords * 4)))
             return RT_FAILURE;
         SL.ao_cap = ac;
     }

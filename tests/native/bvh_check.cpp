@@ -231,7 +231,9 @@ int main(int argc, char** argv) {
                         int sp;
                         int32_t c, n;
                         const int q = bvh4_any_near_budget_state(V, o, d, ArrStack{sa}, budget, sp, c, n);
-                        const bool res = q < 0 ? bvh4_any_near_resume(V, o, d, ArrStack{sa}, sp, c, n) : q == 1;
+                        int q2 = q;
+                        if (q < 0) q2 = bvh4_any_near_resume_budget(V, o, d, ArrStack{sa}, 2 * budget, sp, c, n);
+                        const bool res = q2 < 0 ? bvh4_any_near_resume(V, o, d, ArrStack{sa}, sp, c, n) : q2 == 1;
                         if (res != a4 && bad4.fetch_add(1) < 10)
                             std::printf("MISMATCH4 resume budget %d ray %ld kind %d: %d vs %d\n", budget, r, kind, res, a4);
                     }
