@@ -2514,13 +2514,15 @@ static int far_closest_u() {
 // Largest slice of the scene one wave scans in the split any-hit brute scan.
 constexpr uint32_t kBruteSlice = 4096;
 
-// Waves a split brute scan aims at (ray groups x slices): RT580_BRUTE_WAVES
-// (A/B; the scan of a few far-origin rays is a full-GPU launch either way).
+// Waves a split brute scan aims at (ray groups x slices): RT580_BRUTE_WAVES.
+// North-star frame, 8192 vs 32768 over three boxes: 38.22 / 38.69 / 36.69 vs
+// 39.27 / 39.04 / 37.40 ms; the 8-way share 7.56 vs 7.59 (profiles/r04/ab/bw*,
+// kn2_*): fewer, longer waves per launch.
 static uint32_t brute_waves() {
     static long v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_BRUTE_WAVES");
-        v = e ? atol(e) : 32768;
+        v = e ? atol(e) : 8192;
     }
     return (uint32_t)v;
 }
