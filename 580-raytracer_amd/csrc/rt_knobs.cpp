@@ -67,6 +67,7 @@ const Knob kKnobs[] = {
     {"RT580_GPUS", INT_RANGE, 1, 16, nullptr, nullptr},
     {"RT580_REPLAY", INT_SET, 0, 0, k01, nullptr},
     {"RT580_GRAPH", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_LAT_SPLIT_PCT", INT_RANGE, 1, 99, nullptr, nullptr},
     // rt_bvh.cpp
     {"RT580_LEAF_MAX", INT_RANGE, 1, 8, nullptr, nullptr},
     {"RT580_BVH_INFLATE", FLOAT_NONNEG, 0, 0, nullptr, nullptr},

@@ -1298,16 +1298,22 @@ static int enqueue_split(const rt_render_params* p, int16_t* fb_out, hipStream_t
     w = dev_work();
     // The split row: the last part should hold few rows (its resolve and copy
     // are the tail of the call) and enough AO calls that its AO covers the
-    // first part's resolve and copy: the largest row r with at least 35 % of
-    // the frame's calls in rows [r, H). Taken from this frame's per-row counts
-    // once per (params, scene) -- they do not change between calls.
+    // first part's resolve and copy: the largest row r with at least 20 % of
+    // the frame's calls in rows [r, H) (config 2's Render(): 10 / 20 / 35 / 50 %
+    // 1.911 / 1.894 / 1.916-1.922 / 1.956 ms). Taken from this frame's per-row
+    // counts once per (params, scene) -- they do not change between calls.
     if (!(g.lat_gen == g.scene_gen && std::memcmp(&g.lat_params, p, sizeof *p) == 0)) {
         std::vector<uint32_t> rc((size_t)H);
         if (copy_d2h(rc.data(), SL.row_calls.p, (size_t)H * 4, s, "the per-row AO calls")) return RT_FAILURE;
         uint64_t tot = 0, tail = 0;
         for (uint32_t v : rc) tot += v;
         int r = H;
-        while (r > 1 && (tail < (tot * 35 + 99) / 100 || r > H - 1)) tail += rc[(size_t)--r];
+        static long pct = -1;  // RT580_LAT_SPLIT_PCT: the second part's share of the AO calls
+        if (pct < 0) {
+            const char* e = std::getenv("RT580_LAT_SPLIT_PCT");
+            pct = e ? std::atol(e) : 20;
+        }
+        while (r > 1 && (tail < (tot * (uint64_t)pct + 99) / 100 || r > H - 1)) tail += rc[(size_t)--r];
         g.lat_params = *p;
         g.lat_gen = g.scene_gen;
         g.lat_row = r;
