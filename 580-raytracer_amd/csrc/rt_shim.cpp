@@ -1714,6 +1714,8 @@ void shutdown_ctx() {
     for (auto& ev : g.user_mark)
         if (ev) (void)hipEventDestroy(ev);
     if (g.aux) (void)hipStreamDestroy(g.aux);
+    for (auto& fg : g.fgraph)  // the latency path's frame graphs
+        if (fg.exec) (void)hipGraphExecDestroy(fg.exec);
     if (g.aux_go) (void)hipEventDestroy(g.aux_go);
     if (g.aux_done) (void)hipEventDestroy(g.aux_done);
     for (auto& ev : g.ev_default)
