@@ -265,6 +265,15 @@ def test_graph_replayed_small_frames_match_oracle():
             buf[:] = -1
             rt580.check(lib.rt_gpu_render(ctypes.byref(rts[k][1]), buf.ctypes.data), "render")
             assert np.array_equal(buf.reshape(h, w, 3), want[k]), "config %d buffer %d differs" % (k, b)
+        # the captured graphs go with a shutdown; a fresh context captures its own
+        lib.rt_gpu_shutdown()
+        rt580.check(lib.rt_gpu_init(0), "init")
+        rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+        for _ in range(5):
+            buf = bufs[0][1]
+            buf[:] = -1
+            rt580.check(lib.rt_gpu_render(ctypes.byref(rts[0][1]), buf.ctypes.data), "render after re-init")
+            assert np.array_equal(buf.reshape(h, w, 3), want[0])
     finally:
         for _, buf, _ in bufs:
             lib.rt_gpu_host_unregister(buf.ctypes.data)
