@@ -1674,7 +1674,9 @@ __device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o,
 // have a far hit below it), each lane evaluating the exact tests of rt_isect.h
 // for its own ray. Same candidates, same full tests as bvh_any's far search.
 #ifndef FAR_ANY_WPE
-#define FAR_ANY_WPE 8
+// 6 waves/SIMD for the far any-hit and cell passes (their 8-wave build spills):
+// north-star 36.36 / 36.52 vs 36.75 / 37.11 ms (profiles/r04/ab/w6_*.json)
+#define FAR_ANY_WPE 6
 #endif
 // flag != null: shadow rays (tag = flag index, the flag is set on a hit);
 // else AO rays (tag = AO call, its occlusion count is incremented).
