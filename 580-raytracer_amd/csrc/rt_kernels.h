@@ -162,6 +162,8 @@ struct CountSchedule {
     enum Mode { OFF, RECORD, REPLAY };
     Mode mode = OFF;
     std::vector<uint32_t> vals;
+    std::vector<const char*> where;  // the launcher step that read each count (RECORD), for error messages
+    uint32_t tag = 0;                // which schedule (the device check reports index | tag << 16)
     size_t pos = 0;
     uint32_t* bad = nullptr;  // device word (REPLAY)
     bool broken = false;      // REPLAY asked for more counts than were recorded

@@ -1242,7 +1242,36 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
 // BUDGET > 0: a lane gives up after BUDGET leaf visits; its item goes to
 // W.ao_late (ao_late_kernel re-runs the full query), so a wave is not held by
 // its few long traversals (tools/simd_sim.cpp "budget").
-template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0>
+// XQ = 1: blocks of work are taken from per-XCD queues instead of a static
+// grid stride: the chunk's blocks are cut into 8 contiguous bands (of AO calls,
+// i.e. of raster order), the workgroups of XCD x take the next block of band
+// x (xcd_take) and, once it is empty, of the other bands. At any moment an
+// XCD's resident workgroups trace neighbouring blocks, so its 4 MiB L2 holds
+// the BVH nodes and leaves of a narrow band of the image instead of a slice of
+// the whole chip's window, and the bands balance dynamically (a static
+// XCD-ordered grid, xcd_block, lost to its tail). Speed only: every block is
+// taken exactly once whatever the placement.
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v & 7u;
+}
+
+// The next block [0, nblk) for this workgroup from the per-XCD queues q[0..7]
+// (zeroed before the launch); ~0u when every band is empty. Lane 0 only.
+__device__ __forceinline__ uint32_t xcd_take(uint32_t* q, uint32_t nblk) {
+    const uint32_t x = xcc_id();
+    for (uint32_t t = 0; t < 8u; t++) {
+        const uint32_t b = (x + t) & 7u;
+        const uint32_t lo = (uint32_t)((uint64_t)nblk * b / 8u), hi = (uint32_t)((uint64_t)nblk * (b + 1u) / 8u);
+        if (__atomic_load_n(&q[b], __ATOMIC_RELAXED) >= hi - lo) continue;  // a hint: the count only grows
+        const uint32_t c = atomicAdd(&q[b], 1u);
+        if (c < hi - lo) return lo + c;
+    }
+    return ~0u;
+}
+
+template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0, int XQ = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
@@ -1250,8 +1279,21 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     constexpr int NB = 1 << (2 * KL);  // direction cells
     __shared__ uint32_t s_order[SN];
     __shared__ uint32_t s_bin[SORT > 0 ? NB + 1 : 1];
+    __shared__ uint32_t s_take;
     const uint64_t span = SORT > 0 ? (uint64_t)SN : (uint64_t)TB;
-    for (uint64_t blk = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * span; blk < n; blk += (uint64_t)gridDim.x * span)
+    const uint32_t nblk = (uint32_t)((n + span - 1) / span);
+    uint64_t blk = XQ ? 0 : (uint64_t)xcd_block(blockIdx.x, gridDim.x) * span;
+    for (;;) {
+    if (XQ) {
+        __syncthreads();  // the previous block's last reads of s_take / s_order are done
+        if (threadIdx.x == 0) s_take = xcd_take(W.ao_late_count + 8, nblk);
+        __syncthreads();
+        const uint32_t tb = s_take;
+        if (tb == ~0u) break;
+        blk = (uint64_t)tb * span;
+    } else if (blk >= n) {
+        break;
+    }
     for (int round = 0; round < (SORT > 0 ? SORT : 1); round++) {
         uint64_t i = blk + threadIdx.x;
         if (SORT > 0) {
@@ -1356,6 +1398,8 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
         ao_finish<true>(S, W, SORT > 0 ? 1u : N, active && !late, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o,
                         d);
     }
+    if (!XQ) blk += (uint64_t)gridDim.x * span;
+    }
 }
 
 // The chunk's AO rays that ran out of ao_trace_kernel's step budget: the full
@@ -1432,7 +1476,19 @@ ao_late_kernel(DevScene S, DevWork W) {
         } else {
             hit = live && bvh4_any_near_s(S.bv, o, d, stk);
         }
-        ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w), o, d);
+        // The ray's record again (a volatile read: a real load, not the
+        // registers of the one above), so that nothing of the ray but its index
+        // is live across the traversal. The 64-VGPR build of this kernel
+        // (RT580_LATE_WPE=8) queued ~2 % of its far-pass rays with origins not
+        // their own when the origin stayed live here (the
+        // replayed-count mismatch of round 4); every answer it computed was right.
+        if (live) {
+            const volatile float4* rv = W.ao_rays + 2 * (size_t)i;
+            r0 = make_float4(rv[0].x, rv[0].y, rv[0].z, rv[0].w);
+            r1 = make_float4(rv[1].x, rv[1].y, rv[1].z, rv[1].w);
+        }
+        ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w), v3(r0.x, r0.y, r0.z),
+                        v3(r1.x, r1.y, r1.z));
     }
 }
 
@@ -1445,6 +1501,197 @@ ao_late_kernel(DevScene S, DevWork W) {
 // for this kernel on cornell10k's AO; the SIMD-efficiency model
 // tools/simd_sim.cpp predicts fewer lock-step iterations for them, but their
 // extra live state spills. Not kept.)
+
+#ifdef RT580_DIAGNOSTICS
+// DIAGNOSTIC build only (RT580_AO_VERIFY=1): an audit of the budgeted AO
+// trace + late passes of each chunk that does not touch those kernels (their
+// code is the product's). Every near-query AO ray of the chunk (flag 1) is
+// answered again by the unbudgeted 4-wide query with a plain per-lane stack
+// (ao_audit_expect_kernel): the near hits it implies per AO call, and the far
+// queue it implies (every miss and every far-origin ray: count, and an
+// order-free checksum of each entry's ray, call and key). ao_audit_compare_kernel
+// then checks the occlusion counts the passes added and the queue they wrote.
+// out[0] rays checked, [1] calls whose near hits differ, [2] far-queue count
+// differs (chunks), [3] far-queue checksum differs (chunks), [4] chunks
+// audited, [5] expected near hits, [6] queued rays, [7] queue entries that no
+// ray of the chunk explains; [8 + 2k], [9 + 2k]: the first 8 differing calls
+// (call | got << 32, want); [24] the OR of those entries' reasons, [25] their
+// count, [26 + 18k]: the first 2 such entries (ao_audit_compare_kernel).
+__device__ __forceinline__ unsigned long long audit_mix(float4 a, float4 b, uint32_t key) {
+    unsigned long long h = 0x9e3779b97f4a7c15ull;
+    const uint32_t w[8] = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), __float_as_uint(a.w),
+                           __float_as_uint(b.x), __float_as_uint(b.y), __float_as_uint(b.z), key};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        h ^= w[k];
+        h *= 0xff51afd7ed558ccdull;
+        h ^= h >> 33;
+    }
+    return h;
+}
+
+// exp[c - c_lo]: near hits of call c among the chunk's rays [0, n); aud[0..1]:
+// expected queue length and checksum
+__global__ void __launch_bounds__(TB) ao_audit_expect_kernel(DevScene S, DevWork W, uint64_t n, uint32_t c_lo,
+                                                             uint32_t* exp, unsigned long long* aud,
+                                                             unsigned long long* out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TB) {
+        const float4 r0 = W.ao_rays[2 * i], r1 = W.ao_rays[2 * i + 1];
+        const uint32_t flag = __float_as_uint(r1.w);
+        if (flag == 0u) continue;
+        const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
+        const uint32_t c = __float_as_uint(r0.w);
+        const bool hit = flag == 1u && bvh4_any_near(S.bv, o, d);
+        if (flag == 1u) atomicAdd(&out[0], 1ull);
+        if (hit) {
+            atomicAdd(&exp[c - c_lo], 1u);
+            atomicAdd(&out[5], 1ull);
+        } else if (S.bv.has_far) {
+            const uint32_t key = flag == 2u ? RT_KEY_BRUTE : far_key(S.bv, o, d);
+            atomicAdd(&aud[0], 1ull);
+            atomicAdd(&aud[1], audit_mix(make_float4(o.x, o.y, o.z, r0.w), make_float4(d.x, d.y, d.z, INFINITY), key));
+        }
+    }
+}
+
+// occ_before: W.occ[c_lo, c_lo + nc) before the chunk's passes
+__global__ void __launch_bounds__(TB) ao_audit_compare_kernel(DevScene S, DevWork W, uint32_t c_lo, uint32_t nc,
+                                                              uint32_t N, uint64_t item0, uint64_t n,
+                                                              const uint32_t* occ_before, const uint32_t* exp,
+                                                              unsigned long long* aud, unsigned long long* out) {
+    const uint32_t nq = S.bv.has_far ? W.far_count[0] : 0u;
+    for (uint32_t j = blockIdx.x * TB + threadIdx.x; j < nc; j += gridDim.x * TB) {
+        const uint32_t got = W.occ[c_lo + j] - occ_before[j];
+        if (got != exp[j]) {
+            const unsigned long long k = atomicAdd(&out[1], 1ull);
+            if (k < 8) {
+                out[8 + 2 * k] = (unsigned long long)(c_lo + j) | ((unsigned long long)got << 32);
+                out[9 + 2 * k] = exp[j];
+            }
+        }
+    }
+    for (uint32_t s = blockIdx.x * TB + threadIdx.x; s < nq; s += gridDim.x * TB) {
+        const float4 a = W.far_rays[2 * (size_t)s], b = W.far_rays[2 * (size_t)s + 1];
+        const uint32_t key = W.far_keys[s];
+        atomicAdd(&aud[2], audit_mix(a, b, key));
+        // the entry against the rays of its call in this chunk: which part of it
+        // (if any) no ray of the chunk has -- 1 call out of the chunk, 2 no
+        // sample of the call with this origin, 4 the origin's sample has another
+        // direction, 8 the key is not the ray's own
+        const uint32_t c = __float_as_uint(a.w);
+        uint32_t why = 0u;
+        int64_t found = -1;
+        if (c < c_lo || c >= c_lo + nc) {
+            why = 1u;
+        } else {
+            const int64_t j0 = (int64_t)c * N - (int64_t)item0, j1 = j0 + N;
+            why = 2u;
+            for (int64_t j = j0 < 0 ? 0 : j0; j < j1 && j < (int64_t)n; j++) {
+                const float4 r0 = W.ao_rays[2 * j], r1 = W.ao_rays[2 * j + 1];
+                if (__float_as_uint(r0.x) != __float_as_uint(a.x) || __float_as_uint(r0.y) != __float_as_uint(a.y) ||
+                    __float_as_uint(r0.z) != __float_as_uint(a.z))
+                    continue;
+                found = j;
+                const bool dsame = __float_as_uint(r1.x) == __float_as_uint(b.x) &&
+                                   __float_as_uint(r1.y) == __float_as_uint(b.y) &&
+                                   __float_as_uint(r1.z) == __float_as_uint(b.z);
+                if (!dsame) { why = 4u; continue; }
+                const uint32_t flag = __float_as_uint(r1.w);
+                const uint32_t want = flag == 2u ? RT_KEY_BRUTE : far_key(S.bv, v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z));
+                why = want == key ? 0u : 8u;
+                if (!why) break;
+            }
+        }
+        if (why) {
+            atomicAdd(&out[7], 1ull);
+            atomicOr(&out[24], (unsigned long long)why);
+            const unsigned long long k = atomicAdd(&out[25], 1ull);
+            if (k < 2) {  // the entry and the ray it was matched with (or none)
+                unsigned long long* d = out + 26 + 18 * k;
+                const float4 r0 = found >= 0 ? W.ao_rays[2 * found] : make_float4(0, 0, 0, 0);
+                const float4 r1 = found >= 0 ? W.ao_rays[2 * found + 1] : make_float4(0, 0, 0, 0);
+                const float v[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+                for (int t = 0; t < 16; t++) d[t] = __float_as_uint(v[t]);
+                d[16] = key | ((unsigned long long)why << 32);
+                d[17] = (unsigned long long)s | ((unsigned long long)(found >= 0 ? (uint32_t)found : 0xffffffffu) << 32);
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicAdd(&out[4], 1ull);
+        atomicAdd(&out[6], (unsigned long long)nq);
+    }
+}
+
+__global__ void ao_audit_finish_kernel(const DevScene S, const DevWork W, const unsigned long long* aud,
+                                       unsigned long long* out) {
+    if (threadIdx.x != 0) return;
+    const uint32_t nq = S.bv.has_far ? W.far_count[0] : 0u;
+    if (aud[0] != nq) out[2]++;
+    if (aud[1] != aud[2]) out[3]++;
+}
+
+static bool ao_verify_on() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_VERIFY");
+        v = e ? atoi(e) : 0;
+    }
+    return v != 0;
+}
+
+static unsigned long long* g_verify_out = nullptr;  // device, 64 words
+// per slot (keyed by its W.ao_rays): expected near hits per call, the calls'
+// counts before the chunk, the queue sums
+struct AuditBuf {
+    const void* key;
+    uint32_t cap;
+    uint32_t* exp;
+    uint32_t* before;
+    unsigned long long* aud;
+};
+static std::vector<AuditBuf*> g_audit_bufs;  // (never freed: diagnostic runs only)
+
+static const AuditBuf* audit_for(const DevWork& W) {
+    if (!ao_verify_on() || !W.ao_rays) return nullptr;
+    if (!g_verify_out) {
+        if (hipMalloc((void**)&g_verify_out, 64 * 8) != hipSuccess) return nullptr;
+        if (hipMemset(g_verify_out, 0, 64 * 8) != hipSuccess) return nullptr;
+    }
+    for (const AuditBuf* b : g_audit_bufs)
+        if (b->key == W.ao_rays && b->cap >= W.ao_cap) return b;
+    AuditBuf b{W.ao_rays, W.ao_cap, nullptr, nullptr, nullptr};
+    // a chunk of ao_cap rays spans at most ao_cap + 1 calls
+    if (hipMalloc((void**)&b.exp, ((size_t)W.ao_cap + 2) * 4) != hipSuccess ||
+        hipMalloc((void**)&b.before, ((size_t)W.ao_cap + 2) * 4) != hipSuccess ||
+        hipMalloc((void**)&b.aud, 4 * 8) != hipSuccess)
+        return nullptr;
+    g_audit_bufs.push_back(new AuditBuf(b));
+    return g_audit_bufs.back();
+}
+#endif
+
+// RT580_LATE_WPE=8 (A/B): ao_late_kernel built for 8 waves/SIMD (64 VGPRs, spills)
+// instead of 6
+static int late_wpe() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_LATE_WPE");
+        v = e ? atoi(e) : 6;
+    }
+    return v;
+}
+
+// RT580_AO_XCDQ=1 (A/B): ao_trace_kernel takes its blocks from per-XCD queues
+// over contiguous bands of the chunk (xcd_take)
+static int ao_xcdq() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_XCDQ");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
 
 static int ao_split() {
     static int v = -1;
@@ -2867,8 +3114,22 @@ const char* launch_where() { return g_where; }
 static thread_local CountSchedule* g_cs = nullptr;
 void set_count_schedule(CountSchedule* cs) { g_cs = cs; }
 
-__global__ void count_check_kernel(const uint32_t* dev, uint32_t e0, uint32_t e1, int n, uint32_t* bad) {
-    if (threadIdx.x == 0 && (dev[0] != e0 || (n > 1 && dev[1] != e1))) *bad = 1u;
+// A replayed count against the frame's own. bad[0] = 1 on any mismatch; the
+// first mismatch of the frame also records which count (bad[1] = its index in
+// the schedule + 1) and both values (bad[2..3] the frame's, bad[4..5] the
+// recorded ones), for the error message (rt_shim.cpp check_replay).
+__global__ void count_check_kernel(const uint32_t* dev, uint32_t e0, uint32_t e1, int n, uint32_t* bad,
+                                   uint32_t pos) {
+    if (threadIdx.x != 0) return;
+    const uint32_t a0 = dev[0], a1 = n > 1 ? dev[1] : 0u;
+    if (a0 == e0 && (n < 2 || a1 == e1)) return;
+    bad[0] = 1u;
+    if (atomicCAS(&bad[1], 0u, pos + 1u) == 0u) {
+        bad[2] = a0;
+        bad[3] = a1;
+        bad[4] = e0;
+        bad[5] = n > 1 ? e1 : 0u;
+    }
 }
 
 // n (1 or 2) device words -> out (pinned), through the count schedule. Each
@@ -2889,6 +3150,7 @@ static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStre
             g_cs->broken = true;
             return hipErrorInvalidValue;
         }
+        const uint32_t pos = (uint32_t)g_cs->pos | (g_cs->tag << 16);
         for (int i = 0; i < n; i++) out[i] = g_cs->vals[g_cs->pos++];
         if (counts_fit(out, n, cap0, cap1) != hipSuccess) return hipErrorInvalidValue;
         uint32_t e0 = out[0];
@@ -2902,14 +3164,18 @@ static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStre
             if (corrupt) e0 ^= 1u;
         }
 #endif
-        hipLaunchKernelGGL(count_check_kernel, dim3(1), dim3(64), 0, s, dev, e0, n > 1 ? out[1] : 0u, n, g_cs->bad);
+        hipLaunchKernelGGL(count_check_kernel, dim3(1), dim3(64), 0, s, dev, e0, n > 1 ? out[1] : 0u, n, g_cs->bad,
+                           pos);
         return hipGetLastError();
     }
     hipError_t e = hipMemcpyAsync(out, dev, (size_t)n * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess) e = counts_fit(out, n, cap0, cap1);
     if (e == hipSuccess && g_cs && g_cs->mode == CountSchedule::RECORD)
-        for (int i = 0; i < n; i++) g_cs->vals.push_back(out[i]);
+        for (int i = 0; i < n; i++) {
+            g_cs->vals.push_back(out[i]);
+            g_cs->where.push_back(g_where);
+        }
     return e;
 }
 
@@ -3462,9 +3728,13 @@ hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& 
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
     (void)hipGetLastError();  // launch checks below must not see a stale error
     if (!F.ao_enabled || S.n_ambient == 0 || F.n_rows == 0) return hipSuccess;
+#ifdef RT580_DIAGNOSTICS
+    const AuditBuf* audit = S.use_bvh ? audit_for(W) : nullptr;
+#endif
     if (S.use_bvh) {
         // chunks of the AO items: near pass + queue, sort the misses by
         // direction, wave-cooperative far pass
+        RT_STEP("AO-call total D2H");
         hipError_t e = read_counts(reinterpret_cast<const uint32_t*>(W.totals), 2, W.far_count_host + 4, s, W.call_cap, 0u);
         if (e != hipSuccess) return e;
         const uint64_t calls = (uint64_t)W.far_count_host[4] | ((uint64_t)W.far_count_host[5] << 32);
@@ -3480,6 +3750,17 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(W.aofix_count, 0, 4, s)) != hipSuccess) return e;
             const int wpe = near_wpe();
+#ifdef RT580_DIAGNOSTICS
+            const uint32_t c_lo = (uint32_t)(b / (uint64_t)F.ao_samples);
+            const uint32_t c_n = (uint32_t)((e1 - 1) / (uint64_t)F.ao_samples) + 1u - c_lo;
+            if (split && audit) {
+                if ((e = hipMemcpyAsync(audit->before, W.occ + c_lo, (size_t)c_n * 4, hipMemcpyDeviceToDevice, s)) !=
+                        hipSuccess ||
+                    (e = hipMemsetAsync(audit->exp, 0, (size_t)c_n * 4, s)) != hipSuccess ||
+                    (e = hipMemsetAsync(audit->aud, 0, 4 * 8, s)) != hipSuccess)
+                    return e;
+            }
+#endif
             if (split) {
                 constexpr int V = 512 | 1024 | 2048 | 4096 | 16384;
                 if (wpe == 5)
@@ -3499,9 +3780,13 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
                 else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
-                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
+                    // (the late counts and the per-XCD block queues of XQ = 1)
+                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 64, s)) != hipSuccess) return e;
                     const int bu = ao_budget();
-                    if (bu <= 2)
+                    if (ao_xcdq() && bu == 4)
+                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4, 1>), dim3(grid_for(e1 - b, 16384)),
+                                           dim3(TB), 0, s, S, W, (uint32_t)F.ao_samples, e1 - b);
+                    else if (bu <= 2)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 2>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     else if (bu == 3)
@@ -3521,7 +3806,10 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                         hipLaunchKernelGGL((ao_late_kernel<6, 16, 16, 0>), dim3(4096), dim3(TB), 0, s, S, W);
                         hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 1>), dim3(1024), dim3(TB), 0, s, S, W);
                     } else {
-                        hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
+                        if (late_wpe() == 8)
+                            hipLaunchKernelGGL((ao_late_kernel<8, 16>), dim3(4096), dim3(TB), 0, s, S, W);
+                        else
+                            hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
                     }
                 } else if (twpe == 6 && trace_lds() && so == 3)  // 2048 samples, 16 x 16 cells (default)
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S,
@@ -3554,6 +3842,17 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             }
             kt_end(s, e1 - b);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+#ifdef RT580_DIAGNOSTICS
+            if (split && audit) {  // (before the fix-up pass adds to the queue and the counts)
+                hipLaunchKernelGGL(ao_audit_expect_kernel, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W, e1 - b,
+                                   c_lo, audit->exp, audit->aud, g_verify_out);
+                hipLaunchKernelGGL(ao_audit_compare_kernel, dim3(4096), dim3(TB), 0, s, S, W, c_lo, c_n,
+                                   (uint32_t)F.ao_samples, b, e1 - b, audit->before, audit->exp, audit->aud,
+                                   g_verify_out);
+                hipLaunchKernelGGL(ao_audit_finish_kernel, dim3(1), dim3(64), 0, s, S, W, audit->aud, g_verify_out);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
+#endif
             // exact recompute of the fast pass's failing samples; their misses join the far queue
             if ((e = launch_ao_fix(S, F, W, b, e1, s)) != hipSuccess) return e;
             if (!S.bv.has_far) continue;
@@ -3716,3 +4015,14 @@ hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int ro
 }
 
 }  // namespace rt580
+
+#ifdef RT580_DIAGNOSTICS
+// DIAGNOSTIC build only: the RT580_AO_VERIFY totals (ao_verify_kernel's out[0..63])
+// since the last call, after a device-wide sync; then zeroed. 1: verification off.
+extern "C" int rt580_diag_ao_verify(unsigned long long* out64) {
+    if (!rt580::g_verify_out) return 1;
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    if (hipMemcpy(out64, rt580::g_verify_out, 64 * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    return hipMemset(rt580::g_verify_out, 0, 64 * 8) == hipSuccess ? 0 : 1;
+}
+#endif

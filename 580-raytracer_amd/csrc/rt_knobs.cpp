@@ -35,6 +35,7 @@ const long k234[] = {2, 3, 4, -1};
 const long kSort[] = {0, 1, 2, 3, -1};
 const long kTraceWpe[] = {4, 6, 8, -1};
 const long kNearWpe[] = {0, 5, 6, 8, -1};
+const long kLateWpe[] = {6, 8, -1};
 const long kFarMode[] = {0, 1, 2, 3, 4, -1};
 const long kFarU[] = {1, 2, 4, -1};
 const long kFarCU[] = {0, 1, 2, 4, -1};
@@ -80,8 +81,10 @@ const Knob kKnobs[] = {
     {"RT580_AO_BUDGET", INT_RANGE, 0, 64, nullptr, nullptr},
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
     {"RT580_AO_RESUME", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_AO_XCDQ", INT_SET, 0, 0, k01, nullptr},
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
     {"RT580_NEAR_WPE", INT_SET, 0, 0, kNearWpe, nullptr},
+    {"RT580_LATE_WPE", INT_SET, 0, 0, kLateWpe, nullptr},
     {"RT580_BRUTE_SPLIT", INT_SET, 0, 0, k0123, nullptr},
     {"RT580_BRUTE_RAYS", INT_SET, 0, 0, k148, nullptr},
     {"RT580_BRUTE_WAVES", INT_RANGE, 256, 1 << 20, nullptr, nullptr},
@@ -101,6 +104,7 @@ const Knob kKnobs[] = {
     {"RT580_DUMP_FAR", DIAG_ONLY, 0, 0, nullptr, nullptr},
     {"RT580_REPLAY_CORRUPT", DIAG_ONLY, 0, 0, nullptr, nullptr},
     {"RT580_CELL_SKIP", DIAG_ONLY, 0, 0, nullptr, nullptr},
+    {"RT580_AO_VERIFY", DIAG_ONLY, 0, 0, nullptr, nullptr},
     // read by the Python binding and the tests, not by the library
     {"RT580_LIB", NOT_LIBRARY, 0, 0, nullptr, nullptr},
     {"RT580_EXHAUSTIVE", NOT_LIBRARY, 0, 0, nullptr, nullptr},

@@ -17,6 +17,7 @@
 #include <cstring>
 #include <algorithm>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "../../include/rt580.h"
@@ -155,6 +156,7 @@ struct State {
     // stats of the last traced rows
     int last_rows = 0, last_width = 0, last_ao_samples = 0, last_ao_enabled = 0;
     bool last_valid = false;
+    int stats_slot = 0;  // the slot those rows' per-row counters are in
     // multi-rank split
     rt_render_params split_params{};
     bool split_ready = false;
@@ -436,6 +438,10 @@ int h2d(void* dst, const void* src, size_t bytes, const char* what) { return cop
 struct HostRange {
     const char* p;
     size_t bytes;
+    // the last frame copy enqueued into the range (rt_gpu_render_async): the
+    // next one waits for it, so frames land in call order
+    hipEvent_t copied = nullptr;
+    int copied_device = -1;
 };
 std::vector<HostRange> g_host_ranges;
 
@@ -775,7 +781,9 @@ int begin_schedule(CountSchedule& cs, bool replay) {
     } else {
         cs.mode = CountSchedule::RECORD;
         cs.vals.clear();
+        cs.where.clear();
     }
+    cs.tag = &cs == &g.sched_ao ? 1u : 0u;
     set_count_schedule(&cs);
     return RT_SUCCESS;
 }
@@ -795,9 +803,23 @@ int end_schedule(CountSchedule& cs, const char* what, hipError_t e) {
 int post_replay_check() {
     if (!g.replayed) return RT_SUCCESS;
     g.replayed = false;
-    HIP_TRY(hipMemcpyAsync(SL.bad_host, SL.bad.p, 4, hipMemcpyDeviceToHost, fs()));
+    HIP_TRY(hipMemcpyAsync(SL.bad_host, SL.bad.p, 24, hipMemcpyDeviceToHost, fs()));
     SL.check_pending = true;
     return RT_SUCCESS;
+}
+
+// Which count of which schedule a failed device check names (bad[1] = its
+// index + 1, count_check_kernel), with the launcher step that recorded it.
+std::string replay_mismatch_detail(const uint32_t* bad) {
+    if (bad[1] == 0) return "";
+    const size_t pos = (bad[1] - 1) & 0xffffu;
+    const CountSchedule& cs = (bad[1] - 1) >> 16 ? g.sched_ao : g.sched_trace;
+    const char* sched = &cs == &g.sched_ao ? "AO" : "trace";
+    const char* where = pos < cs.where.size() ? cs.where[pos] : "?";
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "; first mismatch: count #%zu (%s schedule, %s): this frame %u/%u, recorded %u/%u",
+                  pos, sched, where, bad[2], bad[3], bad[4], bad[5]);
+    return buf;
 }
 
 // The replay check of the slot's last frame (waits for that frame).
@@ -807,11 +829,24 @@ int check_replay(Slot& sl) {
     else HIP_TRY(hipStreamSynchronize(g.stream));
     sl.check_pending = false;
     if (*sl.bad_host == 0) return RT_SUCCESS;
-    *sl.bad_host = 0;
+    const std::string detail = replay_mismatch_detail(sl.bad_host);
+    std::memset(sl.bad_host, 0, 24);
     HIP_TRY(hipMemset(sl.bad.p, 0, 64));
     g.trace_valid = g.ao_valid = false;
     return fail("a replayed count schedule did not match its frame's counts (the last frame enqueued on this "
-                "slot, %d frame calls back at most; schedules dropped)", g.nslots);
+                "slot, %d frame calls back at most; schedules dropped)%s", g.nslots, detail.c_str());
+}
+
+// The host-side record of the frame being enqueued (rt_gpu_last_stats,
+// rt_gpu_accel_active): its rows, their slot, the parameters the stats need.
+void note_rows(const rt_render_params* p, int n_rows, bool accel) {
+    g.last_accel = accel;
+    g.last_rows = n_rows;
+    g.last_width = p->width;
+    g.last_ao_samples = p->ao_samples;
+    g.last_ao_enabled = p->ao_enabled;
+    g.last_valid = true;
+    g.stats_slot = g.cur;
 }
 
 // Phase 1: trace every level of the selected rows and count their AO calls.
@@ -839,11 +874,7 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     }
     HIP_TRY(launch_row_counts(sc, f, dev_work(), fs()));
     HIP_TRY(hipEventRecord(g.ev[EV_TRACE], fs()));
-    g.last_rows = n_rows;
-    g.last_width = p->width;
-    g.last_ao_samples = p->ao_samples;
-    g.last_ao_enabled = p->ao_enabled;
-    g.last_valid = true;
+    note_rows(p, n_rows, sc.use_bvh != 0);
     return RT_SUCCESS;
 }
 
@@ -1199,10 +1230,48 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
 
 uint64_t rt_gpu_scene_id(void) { return g.inited && g.have_scene ? g.scene_gen : 0; }
 
+// The frame of rt_gpu_render_device; with fb_host (a registered range of the
+// selected rows' bytes) also its D2H copy on the frame's slot stream, before
+// the slot's end, so the caller's stream waits for the copy too.
+static int render_device_frame(const rt_render_params* p, int16_t** fb_device, int16_t* fb_host);
+
 int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     RT_WORK("rt_gpu_render_device");
+    return render_device_frame(p, fb_device, nullptr);
+}
+
+int rt_gpu_render_async(const rt_render_params* p, int16_t* fb_host) {
+    RT_WORK("rt_gpu_render_async");
+    if (!fb_host) return fail("rt_gpu_render_async: NULL framebuffer");
+    return render_device_frame(p, nullptr, fb_host);
+}
+
+static HostRange* host_range(const void* p, size_t bytes) {
+    const char* c = (const char*)p;
+    for (HostRange& r : g_host_ranges)
+        if (c >= r.p && c + bytes <= r.p + r.bytes) return &r;
+    return nullptr;
+}
+
+static int render_device_frame(const rt_render_params* p, int16_t** fb_device, int16_t* fb_host) {
     if (check_params(p)) return RT_FAILURE;
     HIP_TRY(hipSetDevice(g.device));
+    HostRange* hr = nullptr;
+    if (fb_host) {
+        hr = host_range(fb_host, (size_t)n_selected_rows(p) * p->width * 6);
+        if (!hr)
+            return fail("rt_gpu_render_async: the framebuffer is not a registered range of %zu bytes "
+                        "(rt_gpu_host_register)", (size_t)n_selected_rows(p) * p->width * 6);
+        if (hr->copied && hr->copied_device != g.device) {
+            (void)hipEventDestroy(hr->copied);
+            hr->copied = nullptr;
+        }
+        if (!hr->copied) {
+            HIP_TRY(hipEventCreateWithFlags(&hr->copied, hipEventDisableTiming));
+            hr->copied_device = g.device;
+            HIP_TRY(hipEventRecord(hr->copied, g.stream));
+        }
+    }
     const int n_sel = n_selected_rows(p);
     const bool prefix = p->row_begin == 0 && p->row_step == 1;
     // The RNG offsets need every row before a selected one: render the prefix
@@ -1231,6 +1300,11 @@ int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
         bool retry = false;
         if (check_capacity(p, retry)) return RT_FAILURE;
         if (!retry) {
+            if (hr) {  // the frame to the host, after the previous copy into the same range
+                HIP_TRY(hipStreamWaitEvent(fs(), hr->copied, 0));
+                HIP_TRY(hipMemcpyAsync(fb_host, SL.fb.p, (size_t)n_sel * p->width * 6, hipMemcpyDeviceToHost, fs()));
+                HIP_TRY(hipEventRecord(hr->copied, fs()));
+            }
             if (end_slot()) return RT_FAILURE;
             if (fb_device) *fb_device = (int16_t*)SL.fb.p;
             return RT_SUCCESS;
@@ -1339,6 +1413,21 @@ static int enqueue_split(const rt_render_params* p, int16_t* fb_out, hipStream_t
     return RT_SUCCESS;
 }
 
+// A captured render_split frame. The graph holds the kernels and copies, not
+// the host-side bookkeeping of trace_rows and not the frame's timing events
+// (events recorded during a capture only order the capture): both are done
+// here, the frame's whole time going to its render phase (ms_render).
+static int launch_frame_graph(hipGraphExec_t exec, const rt_render_params* p, hipStream_t s) {
+    for (int e : {EV_START, EV_TRACE, EV_RANK}) HIP_TRY(hipEventRecord(g.ev[e], s));
+    HIP_TRY(hipGraphLaunch(exec, s));
+    for (int e : {EV_AO, EV_RESOLVE}) HIP_TRY(hipEventRecord(g.ev[e], s));
+    g.traced_rows[0] = 0;
+    g.traced_rows[1] = 1;
+    g.traced_rows[2] = p->height;
+    note_rows(p, p->height, false);
+    return RT_SUCCESS;
+}
+
 // rt_gpu_render's latency path for small-scene whole frames into a registered
 // host framebuffer: after the trace and the AO-call numbering, the frame's
 // rows split in two at row r (the calls of rows [0, r) are the first ones of
@@ -1379,7 +1468,7 @@ static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) 
     const bool graph_ok = graphs && !g.graphs_off && !g.profiling && p->rng_engine != RT_RNG_MT19937 &&
                           g.lat_gen == g.scene_gen && std::memcmp(&g.lat_params, p, sizeof *p) == 0;
     if (graph_ok && key && G.exec) {
-        HIP_TRY(hipGraphLaunch(G.exec, s));
+        if (launch_frame_graph(G.exec, p, s)) return RT_FAILURE;
     } else if (graph_ok && key && G.seen) {
         if (G.exec) (void)hipGraphExecDestroy(G.exec);
         G.exec = nullptr;
@@ -1396,7 +1485,7 @@ static int render_split(const rt_render_params* p, int16_t* fb_out, bool& done) 
             g.graphs_off = true;
             if (enqueue_split(p, fb_out, s)) return RT_FAILURE;
         } else {
-            HIP_TRY(hipGraphLaunch(G.exec, s));
+            if (launch_frame_graph(G.exec, p, s)) return RT_FAILURE;
         }
     } else {
         if (enqueue_split(p, fb_out, s)) return RT_FAILURE;
@@ -1456,6 +1545,16 @@ int rt_gpu_host_unregister(void* host_ptr) {
                     (void)sync_all();
                     g_cur = cur;
                 }
+            // frame graphs whose captured copies land in the range go with its registration
+            const char* lo = g_host_ranges[i].p;
+            const char* hi = lo + g_host_ranges[i].bytes;
+            for (int k = 0; k < kMaxCtx; k++)
+                for (State::FrameGraph& G : g_ctx[k].fgraph)
+                    if (G.fb && (const char*)G.fb >= lo && (const char*)G.fb < hi) {
+                        if (G.exec) (void)hipGraphExecDestroy(G.exec);
+                        G = State::FrameGraph{};
+                    }
+            if (g_host_ranges[i].copied) (void)hipEventDestroy(g_host_ranges[i].copied);
             g_host_ranges.erase(g_host_ranges.begin() + (long)i);
             HIP_TRY(hipHostUnregister(host_ptr));
             return RT_SUCCESS;
@@ -1589,10 +1688,12 @@ int rt_gpu_last_stats(rt_render_stats* st) {
     if (!g.last_valid) return fail("no frame rendered yet");
     if (sync_all()) return RT_FAILURE;
     const int n = g.last_rows;
+    const Slot& ls = g.slot[g.stats_slot];
+    if ((size_t)n * 4 > ls.row_calls.bytes) return fail("rt_gpu_last_stats: the last frame's counters are gone");
     std::vector<uint32_t> rc(n), rh(n), rn(n);
-    if (n && (copy_d2h(rc.data(), SL.row_calls.p, (size_t)n * 4, g.stream, "the per-row AO calls") ||
-              copy_d2h(rh.data(), SL.row_hits.p, (size_t)n * 4, g.stream, "the per-row hits") ||
-              copy_d2h(rn.data(), SL.row_nodes.p, (size_t)n * 4, g.stream, "the per-row tree nodes")))
+    if (n && (copy_d2h(rc.data(), ls.row_calls.p, (size_t)n * 4, g.stream, "the per-row AO calls") ||
+              copy_d2h(rh.data(), ls.row_hits.p, (size_t)n * 4, g.stream, "the per-row hits") ||
+              copy_d2h(rn.data(), ls.row_nodes.p, (size_t)n * 4, g.stream, "the per-row tree nodes")))
         return RT_FAILURE;
     uint64_t calls = 0, hits = 0, tree = 0;
     for (int i = 0; i < n; i++) { calls += rc[i]; hits += rh[i]; tree += rn[i]; }

@@ -61,6 +61,7 @@ SIGNATURES = [
     ("rt_gpu_own_stream", ctypes.c_void_p, []),
     ("rt_gpu_render", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
     ("rt_gpu_render_device", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.POINTER(ctypes.c_void_p)]),
+    ("rt_gpu_render_async", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
     ("rt_gpu_count_rows", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
     ("rt_gpu_shade_rows", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_void_p]),
     ("rt_gpu_last_stats", ctypes.c_int, [ctypes.POINTER(RenderStats)]),

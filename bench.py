@@ -6,8 +6,9 @@ A step = one frame of BASELINE config 2 (simpleSphereScene.json, 1920x1080,
 depth 4, 64 AO samples; the reference's own scene file) rendered from scratch
 by the reference's Render() loop (Raytracer.cpp:916-935): trace of the
 recursion tree, AO-call count + RNG-offset scan, AO kernel, resolve (+ for
-N > 1 the all-gather of per-row AO counts and the gather of the row tiles).
-The scene is resident in HBM.
+N > 1 the all-gather of per-row AO counts and the gather of the row tiles),
+and the int16 framebuffer copied into host memory. The scene is resident in
+HBM.
 
     python bench.py [--gpus N [--rehearse]] [--steps K] [--warmup W]
                     [--workload config2|cornell10k|field100k_1080p|field100k|field1m]
@@ -15,8 +16,9 @@ The scene is resident in HBM.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Parallel modes (the row split of SURVEY §8e, byte-identical frames for every N):
-  * N = 1: rt_gpu_render_device, up to three frames in flight, framebuffer left in HBM
-    (device throughput); the blocking Render() latency is reported beside it.
+  * N = 1: rt_gpu_render_async into page-locked host buffers, up to three frames
+    in flight (each frame's D2H overlaps the next frames' kernels); the blocking
+    Render() latency is reported beside it.
   * --gpus N without a launcher: rt_gpu_render_multi over devices 0..N-1 in this
     process (what the drop-in Render() calls: single-process RCCL, framebuffer
     on the host every step). N above the visible devices is an error;
@@ -28,9 +30,11 @@ Parallel modes (the row split of SURVEY §8e, byte-identical frames for every N)
 
 Rank 0 prints ONE JSON line on stdout: metric, value = whole-job Mrays/s,
 ms_per_step, roofline of the AO ray kernel, cpu_baseline (N = 1), the frame
-check of the last timed frame (config 2: the reference's sha256), and the
-north_star sub-record: the 100k-triangle 1920x1080 depth-4 AO-64 frame that
-BASELINE's target names, measured the same way in the same run.
+check of the last timed frame (config 2: the reference's sha256), the
+north_star sub-record (the 100k-triangle 1920x1080 depth-4 AO-64 frame that
+BASELINE's target names) and the config3 sub-record (BASELINE config 3, the
+10k-triangle Cornell box at 1920x1080 depth 4 AO 64), both measured the same
+way in the same run.
 """
 import argparse
 import contextlib
@@ -174,7 +178,6 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     n_tri = sum(1 for i in range(sc.n_prims) if sc.prims[i].kind == 0)
     log("%s: scene uploaded (%d primitives, %.1f s incl. acceleration build)" % (name, sc.n_prims, upload_s))
 
-    fbp = ctypes.c_void_p()
     host = None
     dframe = None
     dist_mod = helpers.rt580_dist() if ctx.dist_on else None
@@ -186,6 +189,17 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     if ctx.multi:
         host = np.zeros(W * H * 3, dtype=np.int16)
         devs = (ctypes.c_int * ctx.multi)(*ctx.devices)
+    # N = 1: each step's frame lands in host memory (SURVEY 8d's ms/frame ends
+    # with the framebuffer on the host): a ring of page-locked int16 buffers,
+    # one per frame in flight; rt_gpu_render_async queues the frame and its D2H
+    # copy, which overlaps the next frames' kernels
+    ring = []
+    if not ctx.dist_on and not ctx.multi and ctx.row_sample == 1:
+        for _ in range(RING):
+            raw, buf, span = registered_int16(W * H * 3)
+            rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "rt_gpu_host_register")
+            ring.append((raw, buf))
+    step_i = [0]
 
     def step():
         if K > 1:
@@ -201,8 +215,10 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
             rt580.check(lib.rt_gpu_render_multi(ctypes.byref(params), host.ctypes.data, ctx.multi, devs),
                         "rt_gpu_render_multi")
             return None
-        rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(fbp)), "rt_gpu_render_device")
-        return None
+        buf = ring[step_i[0] % RING][1]
+        step_i[0] += 1
+        rt580.check(lib.rt_gpu_render_async(ctypes.byref(params), buf.ctypes.data), "rt_gpu_render_async")
+        return buf
 
     def finish():
         return dframe.finish() if dframe is not None else None
@@ -277,7 +293,8 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
         elif ctx.multi:
             frame_np = host.reshape(H, W, 3)
         else:
-            frame_np = rt580.copy_to_host(fbp.value, W * H * 6, np.int16).reshape(H, W, 3)
+            rt580.check(lib.rt_gpu_synchronize(), "rt_gpu_synchronize")
+            frame_np = last.copy().reshape(H, W, 3)
 
     if ctx.dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
@@ -320,7 +337,9 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
             "scene_query": "exact BVH + plane tree (rt_bvh.h)" if lib.rt_gpu_accel_active() else
                            "brute force (every primitive per ray, as the reference)",
         },
-        "step": ("one frame; framebuffer left in HBM, up to three frames in flight (device throughput)" if not
+        "step": ("one frame into host memory: rt_gpu_render_async, the int16 framebuffer copied into a page-locked "
+                 "host buffer (a ring of %d), up to three frames in flight (each frame's D2H overlaps the next "
+                 "frames' kernels)" % RING if not
                  (ctx.dist_on or ctx.multi) else
                  "one frame, whole Render(): framebuffer on device 0's host copy" if ctx.multi else
                  "one frame on every rank; rank 0 holds the gathered u8 frame"),
@@ -354,6 +373,8 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
                 out["frame_check"].update(oracle_rows_check(ctx, name, root, frame_np, row_counts, n_px))
     if not ctx.dist_on and not ctx.multi and K == 1:
         out["render_call_ms"] = render_latency(lib, rt580, params, torch)
+    for _, buf in ring:
+        rt580.check(lib.rt_gpu_host_unregister(buf.ctypes.data), "rt_gpu_host_unregister")
     if cpu_baseline_on and ctx.n_gpus == 1 and not ctx.dist_on:
         gpu_px = frame_np.reshape(-1, 3) if frame_np is not None and frame_np.dtype == np.int16 else None
         out["cpu_baseline"] = cpu_baseline(ctx, name, root, params, gpu_px, row_counts)
@@ -506,6 +527,19 @@ def roofline(workload, k_ms, k_launches, k_rays, iso=None):
     return res
 
 
+RING = 3  # host framebuffers of the N = 1 step (one per frame slot in flight)
+
+
+def registered_int16(n_val):
+    """A page-aligned, page-rounded int16 host buffer of n_val values (a
+    registration must not share pages with other allocations) -> (owner, view, span)."""
+    import numpy as np
+    span = (n_val * 2 + 4095) // 4096 * 4096
+    raw = np.zeros(span + 4096, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    return raw, raw[off:off + span].view(np.int16)[:n_val], span
+
+
 def render_latency(lib, rt580, params, torch, n=5, warm=4):
     """Blocking rt_gpu_render (what Render() calls): first launch -> int16
     framebuffer on the host (SURVEY §8d ms/frame), excluding scene load/upload
@@ -515,14 +549,8 @@ def render_latency(lib, rt580, params, torch, n=5, warm=4):
     after `warm` untimed calls (a small-scene frame is captured as a HIP graph
     on each slot's second call, rt_shim.cpp render_split: the steady state of
     repeated renders)."""
-    import numpy as np
     # page-aligned and page-rounded, like the class surface's own framebuffer
-    # (a registration must not share pages with other allocations)
-    n_val = params.width * params.height * 3
-    span = (n_val * 2 + 4095) // 4096 * 4096
-    raw = np.zeros(span + 4096, dtype=np.uint8)
-    off = (-raw.ctypes.data) % 4096
-    host = raw[off:off + span].view(np.int16)[:n_val]
+    raw, host, span = registered_int16(params.width * params.height * 3)
     rt580.check(lib.rt_gpu_host_register(host.ctypes.data, span), "rt_gpu_host_register")
     try:
         for _ in range(warm):
@@ -630,6 +658,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=None, help="default 3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true", help="skip the north_star sub-record (config2)")
+    ap.add_argument("--no-config3", action="store_true", help="skip the config3 sub-record (config2)")
     ap.add_argument("--no-check", action="store_true", help="skip the reference-hash check of the last frame")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     ap.add_argument("--dist", action="store_true",
@@ -664,6 +693,11 @@ def main():
         ns = run_workload(ctx, "field100k_1080p", 10, 3, not args.no_cpu_baseline, not args.no_check)
         if out is not None:
             out["north_star"] = ns
+    if args.workload == "config2" and not args.no_config3:
+        # BASELINE config 3, the other 1 x MI355X configuration, measured the same way
+        c3 = run_workload(ctx, "cornell10k", 10, 3, not args.no_cpu_baseline, not args.no_check)
+        if out is not None:
+            out["config3"] = c3
     if out is not None:
         print(json.dumps(out), file=json_out, flush=True)
     if ctx.dist_on:

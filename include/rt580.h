@@ -166,6 +166,14 @@ int rt_gpu_render(const rt_render_params* params, int16_t* fb_out);
  * mismatch is reported by the call that next uses the frame's slot (up to
  * RT580_SLOTS calls later) or by rt_gpu_synchronize. */
 int rt_gpu_render_device(const rt_render_params* params, int16_t** fb_device);
+/* Throughput form of rt_gpu_render: the frame and its copy into fb_host are
+ * queued and the call returns (frames in flight on the shim's slots; each
+ * frame's D2H overlaps the next frames' kernels). fb_host must lie in a range
+ * registered with rt_gpu_host_register; copies into one range land in call
+ * order. The frame is in fb_host once the shim's stream (rt_gpu_set_stream)
+ * reaches the point of this call: rt_gpu_synchronize, or a sync of that
+ * stream. Replayed-count checks are reported as for rt_gpu_render_device. */
+int rt_gpu_render_async(const rt_render_params* params, int16_t* fb_host);
 /* Page-lock a host buffer that will receive frames (rt_gpu_render's fb_out):
  * a frame copied into a registered range lands there with one DMA instead of
  * through the shim's pinned staging buffer. The caller keeps the buffer alive

@@ -204,6 +204,8 @@ def test_replay_count_mismatch_fails_the_frame(tmp_path):
     assert line, r.stdout + r.stderr
     assert line[0].startswith("CODES [0, 1, 0, 1]"), line[0]
     assert "replayed count schedule" in line[0], line[0]
+    # the device check names the count that differed (schedule, index, launcher step, both values)
+    assert "first mismatch: count #" in line[0] and "recorded" in line[0], line[0]
 
 
 def test_accel_toggle_on_repeated_frame_keeps_rendering():
@@ -317,3 +319,70 @@ def test_fine_direction_grid_small_frames_match_oracle(tmp_path, scene):
     line = [l for l in r.stdout.splitlines() if l.startswith("MATCH")]
     assert line, r.stdout + r.stderr
     assert line[0] == "MATCH [True, True]", line[0]
+
+
+def test_render_async_frames_land_in_registered_buffers():
+    """rt_gpu_render_async (the bench's N = 1 step): frames queued with their
+    D2H copies into registered host buffers, several in flight, two
+    configurations interleaved over a ring of buffers -- after a synchronize
+    every buffer holds the last frame queued into it, equal to the oracle's; an
+    unregistered buffer is refused."""
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    root = helpers.synthetic_root("cornell10k")
+    w, h = 48, 27
+    cfg = [(4, 8), (2, 4)]
+    want = [helpers.oracle_render("cornell10k.json", w, h, d, a, True, root=root)[0] for d, a in cfg]
+    rts = [_params("cornell10k.json", w, h, d, a, root) for d, a in cfg]
+    s = rts[0][0].scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    bufs = [_registered(w * h * 3) for _ in range(3)]
+    for _, buf, span in bufs:
+        rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "host_register")
+    try:
+        last = {}
+        for _, buf, _ in bufs:
+            buf[:] = -1
+        for i in range(11):
+            k, b = i % 2, i % 3
+            rt580.check(lib.rt_gpu_render_async(ctypes.byref(rts[k][1]), bufs[b][1].ctypes.data), "render_async")
+            last[b] = k
+        rt580.check(lib.rt_gpu_synchronize(), "synchronize")
+        for b, k in last.items():
+            assert np.array_equal(bufs[b][1].reshape(h, w, 3), want[k]), "buffer %d (config %d)" % (b, k)
+        plain = np.zeros(w * h * 3, dtype=np.int16)
+        assert lib.rt_gpu_render_async(ctypes.byref(rts[0][1]), plain.ctypes.data) != 0
+    finally:
+        for _, buf, _ in bufs:
+            lib.rt_gpu_host_unregister(buf.ctypes.data)
+    rts[0][0].close()
+    rts[1][0].close()
+
+
+
+@pytest.mark.parametrize("late_wpe", ["6", "8"])
+def test_ao_audit_of_the_product_trace_and_late_passes(tmp_path, late_wpe):
+    """Diagnostic build, RT580_AO_VERIFY=1 (rt_kernels.hip ao_audit_*): on the
+    north-star frame, every near-query AO ray is answered again by the
+    unbudgeted query, and the occlusion counts and far queue that implies are
+    compared with what ao_trace_kernel / ao_late_kernel wrote -- their code is
+    the product's (the audit adds kernels only). Both builds of the late pass:
+    the 64-VGPR one (RT580_LATE_WPE=8) queued origins not their own before the
+    ray record was re-read after the traversal (round 5)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    diag = os.path.join(helpers.REPO, "580-raytracer_amd", "lib580rt_diag.so")
+    if not os.path.exists(diag):
+        pytest.skip("diagnostic build absent (make diag)")
+    env = dict(os.environ, RT580_LIB=diag, RT580_AO_VERIFY="1", RT580_LATE_WPE=late_wpe)
+    r = subprocess.run([sys.executable, os.path.join(helpers.REPO, "tools", "ao_verify.py"), "field100k_1080p", "2"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    v = res["verify"]
+    assert v["ok"] and v["entries_unexplained"] == 0 and v["rays_checked"] > 2e8, v
+    assert res["frames_agree"] and not res["replay_errors"], res
+    # the frame the bench's oracle frame check pins (profiles/r04/bench_final.json north_star)
+    assert res["hashes"][0] == "42f02c04df52fe3694345c940b4fe94bbfeefec47a04617c7c82508d4d06c24f", res["hashes"]

@@ -74,7 +74,7 @@ shares)
   : > $OUT
   for K in $KS; do
     for ((r = 0; r < K; r++)); do
-      timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --no-north-star --no-check --steps $S --warmup 2 \
+      timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --no-north-star --no-config3 --no-check --steps $S --warmup 2 \
         --row-sample $K --row-rank $r > gpurun_out/share.json 2> gpurun_out/share.err || { tail -5 gpurun_out/share.err; exit 1; }
       python3 -c "import json; d=json.load(open('gpurun_out/share.json')); print(json.dumps({'K': $K, 'r': $r, 'ms': d['ms_per_step'], 'rays': d['config']['rays_per_frame']}))" >> $OUT
       tail -1 $OUT
@@ -94,7 +94,7 @@ profile)
   TAG=$1; shift
   OUT=gpurun_out/prof_$TAG
   mkdir -p $OUT
-  BENCH="python3 bench.py --no-cpu-baseline --no-north-star --no-check $*"
+  BENCH="python3 bench.py --no-cpu-baseline --no-north-star --no-config3 --no-check $*"
   case "$*" in *--steps*) ;; *) BENCH="$BENCH --steps 3 --warmup 1";; esac
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o trace -- $BENCH > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 1; }
   i=0
@@ -121,7 +121,7 @@ trace)
   TAG=$1; shift
   OUT=gpurun_out/trace_$TAG
   mkdir -p $OUT
-  BENCH="python3 bench.py --no-cpu-baseline --no-north-star --no-check $*"
+  BENCH="python3 bench.py --no-cpu-baseline --no-north-star --no-config3 --no-check $*"
   case "$*" in *--steps*) ;; *) BENCH="$BENCH --steps 6 --warmup 3";; esac
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o trace -- $BENCH > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 1; }
   python3 tools/trace_gaps.py $OUT/trace_kernel_trace.csv 4 > $OUT/gaps.txt && head -25 $OUT/gaps.txt
