@@ -91,7 +91,8 @@ struct DevWork {
     uint32_t* call_node;   // [call_cap]
     uint64_t* call_rng;    // [call_cap] minstd state at the call's first draw / mt19937 global call index
     uint32_t* occ;         // [call_cap] occluded samples
-    const uint32_t* mt_stream;  // mt19937 draws (absolute index), else null
+    const uint32_t* mt_stream;  // mt19937 draws [mt_base, ...) of the serial stream, else null
+    uint64_t mt_base;           // absolute index of mt_stream[0]
     uint32_t node_cap;
     uint32_t call_cap;
     // BVH scenes: AO rays that miss every near triangle, queued for the sorted
@@ -197,6 +198,11 @@ hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int h
                             hipStream_t s);
 hipError_t upload_gamma_lut(const uint8_t* lut, hipStream_t s);
 hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
+// mt19937 draws [lo, hi) of the serial stream into out[0, hi - lo): one
+// workgroup per checkpoint block k in [k0, k0 + nblk) (rt_mt.h: windows[j] =
+// W_{(k0 + j) kMtBlock}), each running the twist from its window.
+hipError_t launch_mt_generate(const uint32_t* windows, uint64_t k0, uint32_t nblk, uint64_t lo, uint64_t hi,
+                              uint32_t* out, hipStream_t s);
 hipError_t launch_powf_eval(const float* x, float y, float* out, uint64_t n, hipStream_t s);
 hipError_t launch_math_selftest(uint64_t seed, uint64_t n, unsigned long long* bad, hipStream_t s);
 // Per-launch HIP-event timing of the AO ray kernel (profiling; see rt_kernels.hip).

@@ -37,6 +37,7 @@
 
 #include "../../include/rt580.h"
 #include "rt_kernels.h"
+#include "rt_mt.h"
 #include "rt_isect.h"
 #include "rt_libm.h"
 #include "rt_math.h"
@@ -937,7 +938,7 @@ __device__ __forceinline__ void ao_draws(const DevFrame& F, const DevWork& W, ui
         st = mersenne31_mul(st, 16807u);
         u1 = canon_minstd(st);
     } else {
-        const uint64_t k = rbase * 2ull * (uint64_t)F.ao_samples + 2ull * s;
+        const uint64_t k = rbase * 2ull * (uint64_t)F.ao_samples + 2ull * s - W.mt_base;
         u0 = canon_mt(W.mt_stream[k]);
         u1 = canon_mt(W.mt_stream[k + 1]);
     }
@@ -1242,36 +1243,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
 // BUDGET > 0: a lane gives up after BUDGET leaf visits; its item goes to
 // W.ao_late (ao_late_kernel re-runs the full query), so a wave is not held by
 // its few long traversals (tools/simd_sim.cpp "budget").
-// XQ = 1: blocks of work are taken from per-XCD queues instead of a static
-// grid stride: the chunk's blocks are cut into 8 contiguous bands (of AO calls,
-// i.e. of raster order), the workgroups of XCD x take the next block of band
-// x (xcd_take) and, once it is empty, of the other bands. At any moment an
-// XCD's resident workgroups trace neighbouring blocks, so its 4 MiB L2 holds
-// the BVH nodes and leaves of a narrow band of the image instead of a slice of
-// the whole chip's window, and the bands balance dynamically (a static
-// XCD-ordered grid, xcd_block, lost to its tail). Speed only: every block is
-// taken exactly once whatever the placement.
-__device__ __forceinline__ uint32_t xcc_id() {
-    uint32_t v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-    return v & 7u;
-}
-
-// The next block [0, nblk) for this workgroup from the per-XCD queues q[0..7]
-// (zeroed before the launch); ~0u when every band is empty. Lane 0 only.
-__device__ __forceinline__ uint32_t xcd_take(uint32_t* q, uint32_t nblk) {
-    const uint32_t x = xcc_id();
-    for (uint32_t t = 0; t < 8u; t++) {
-        const uint32_t b = (x + t) & 7u;
-        const uint32_t lo = (uint32_t)((uint64_t)nblk * b / 8u), hi = (uint32_t)((uint64_t)nblk * (b + 1u) / 8u);
-        if (__atomic_load_n(&q[b], __ATOMIC_RELAXED) >= hi - lo) continue;  // a hint: the count only grows
-        const uint32_t c = atomicAdd(&q[b], 1u);
-        if (c < hi - lo) return lo + c;
-    }
-    return ~0u;
-}
-
-template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0, int XQ = 0>
+template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
@@ -1279,21 +1251,8 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     constexpr int NB = 1 << (2 * KL);  // direction cells
     __shared__ uint32_t s_order[SN];
     __shared__ uint32_t s_bin[SORT > 0 ? NB + 1 : 1];
-    __shared__ uint32_t s_take;
     const uint64_t span = SORT > 0 ? (uint64_t)SN : (uint64_t)TB;
-    const uint32_t nblk = (uint32_t)((n + span - 1) / span);
-    uint64_t blk = XQ ? 0 : (uint64_t)xcd_block(blockIdx.x, gridDim.x) * span;
-    for (;;) {
-    if (XQ) {
-        __syncthreads();  // the previous block's last reads of s_take / s_order are done
-        if (threadIdx.x == 0) s_take = xcd_take(W.ao_late_count + 8, nblk);
-        __syncthreads();
-        const uint32_t tb = s_take;
-        if (tb == ~0u) break;
-        blk = (uint64_t)tb * span;
-    } else if (blk >= n) {
-        break;
-    }
+    for (uint64_t blk = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * span; blk < n; blk += (uint64_t)gridDim.x * span)
     for (int round = 0; round < (SORT > 0 ? SORT : 1); round++) {
         uint64_t i = blk + threadIdx.x;
         if (SORT > 0) {
@@ -1398,8 +1357,6 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
         ao_finish<true>(S, W, SORT > 0 ? 1u : N, active && !late, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o,
                         d);
     }
-    if (!XQ) blk += (uint64_t)gridDim.x * span;
-    }
 }
 
 // The chunk's AO rays that ran out of ao_trace_kernel's step budget: the full
@@ -1409,7 +1366,9 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
 // own second level, at W.ao_late + ao_cap / 2). BUDGET2 > 0 (with SRC 0): a
 // second budget, the rays still undecided go to queue 1 for a last launch
 // (RT580_AO_BUDGET2, A/B); skipped when queue 0 fills more than half the buffer.
-template <int WPE, int LDS_D, int BUDGET2 = 0, int SRC = 0>
+// REREAD = 0 (diagnostic builds only, RT580_LATE_REREAD=0): the round-4 form
+// that queues the ray from the registers of the traversal (see below).
+template <int WPE, int LDS_D, int BUDGET2 = 0, int SRC = 0, int REREAD = 1>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_late_kernel(DevScene S, DevWork W) {
     __shared__ uint32_t lstk[LDS_D][TB];
@@ -1482,13 +1441,16 @@ ao_late_kernel(DevScene S, DevWork W) {
         // (RT580_LATE_WPE=8) queued ~2 % of its far-pass rays with origins not
         // their own when the origin stayed live here (the
         // replayed-count mismatch of round 4); every answer it computed was right.
-        if (live) {
+        if (REREAD && live) {
             const volatile float4* rv = W.ao_rays + 2 * (size_t)i;
             r0 = make_float4(rv[0].x, rv[0].y, rv[0].z, rv[0].w);
             r1 = make_float4(rv[1].x, rv[1].y, rv[1].z, rv[1].w);
         }
-        ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w), v3(r0.x, r0.y, r0.z),
-                        v3(r1.x, r1.y, r1.z));
+        if (REREAD)
+            ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w),
+                            v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z));
+        else
+            ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w), o, d);
     }
 }
 
@@ -1588,6 +1550,13 @@ __global__ void __launch_bounds__(TB) ao_audit_compare_kernel(DevScene S, DevWor
             why = 2u;
             for (int64_t j = j0 < 0 ? 0 : j0; j < j1 && j < (int64_t)n; j++) {
                 const float4 r0 = W.ao_rays[2 * j], r1 = W.ao_rays[2 * j + 1];
+                if (why == 2u && a.x != a.z && __float_as_uint(r0.z) == __float_as_uint(a.x) &&
+                    __float_as_uint(r0.y) == __float_as_uint(a.y) && __float_as_uint(r0.x) == __float_as_uint(a.z))
+                    why = 16u;  // a sample of the call has this origin with x and z exchanged
+                if (why == 16u) { found = j; continue; }
+                if (why == 2u && found < 0 && __float_as_uint(r1.x) == __float_as_uint(b.x) &&
+                    __float_as_uint(r1.y) == __float_as_uint(b.y) && __float_as_uint(r1.z) == __float_as_uint(b.z))
+                    found = j;  // (reported: the sample with this direction, when no origin matches)
                 if (__float_as_uint(r0.x) != __float_as_uint(a.x) || __float_as_uint(r0.y) != __float_as_uint(a.y) ||
                     __float_as_uint(r0.z) != __float_as_uint(a.z))
                     continue;
@@ -1629,6 +1598,16 @@ __global__ void ao_audit_finish_kernel(const DevScene S, const DevWork W, const 
     const uint32_t nq = S.bv.has_far ? W.far_count[0] : 0u;
     if (aud[0] != nq) out[2]++;
     if (aud[1] != aud[2]) out[3]++;
+}
+
+// RT580_LATE_REREAD=0: the 8-wave late pass without the re-read (its round-4 form)
+static int late_reread() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_LATE_REREAD");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
 }
 
 static bool ao_verify_on() {
@@ -1678,17 +1657,6 @@ static int late_wpe() {
     if (v < 0) {
         const char* e = getenv("RT580_LATE_WPE");
         v = e ? atoi(e) : 6;
-    }
-    return v;
-}
-
-// RT580_AO_XCDQ=1 (A/B): ao_trace_kernel takes its blocks from per-XCD queues
-// over contiguous bands of the chunk (xcd_take)
-static int ao_xcdq() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_XCDQ");
-        v = e ? atoi(e) : 0;
     }
     return v;
 }
@@ -2082,8 +2050,13 @@ __device__ __forceinline__ void cell_full_tests(const DevScene& S, const float4 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// rays_min > 0: items of at least rays_min rays take the ray-per-lane form --
+// each lane holds its ray in registers and the cell's candidates are read one
+// after the other as wave-uniform scalar loads (no LDS reads per pair); items
+// with fewer rays keep the (candidate, ray)-pair lanes, which fill the wave
+// whatever the item's shape.
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
-far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
+far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag, uint32_t rays_min) {
     __shared__ float4 sray[TB / 64][64][2];
     __shared__ uint32_t shit[TB / 64][64];
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
@@ -2129,6 +2102,41 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                 FarRay fr;
                 fr.R = bt.w;
                 hit = far_tree_any_wave(S, live, v3(at.x, at.y, at.z), v3(bt.x, bt.y, bt.z), fr, stk[wave]);
+            } else if (rays_min && nr >= rays_min) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const rv3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+                const FarRay fr = far_ray(V, o);
+                bool alive = live;  // not yet occluded
+                uint32_t qn = 0;
+                const cu32_ptr always = (cu32_ptr)V.grid_always;
+                const cu32_ptr items = (cu32_ptr)(V.grid_items + cur.lb);
+                for (int kc = 0; kc < (CELL_SKIP(1) ? 0 : n_cand); kc++) {
+                    const uint32_t ti = kc < V.n_always ? always[kc] : items[kc - V.n_always];
+                    const FarTri ft = load_far_tri(V.far_tris, (int)ti);
+                    const bool fc = alive && far_candidate(ft, fr, o, d);
+                    RT_CELL_STAT(2, fc ? 1 : 0);
+                    const uint64_t m = __ballot(fc);
+                    if (m == 0) continue;
+                    if (fc) {
+                        const uint32_t slot = qn + (uint32_t)__popcll(m & lanemask_lt());
+                        pq_id[wave][slot] = ft.id;
+                        pq_j[wave][slot] = (uint8_t)lane;
+                    }
+                    qn += (uint32_t)__popcll(m);
+                    if (qn >= 64u) {
+                        cell_full_tests(S, sray[wave], shit[wave], pq_id[wave], pq_j[wave], qn);
+                        qn = 0;
+                        alive = live && shit[wave][lane] == 0u;
+                        if (__ballot(alive) == 0) break;
+                    }
+                }
+                if (qn) cell_full_tests(S, sray[wave], shit[wave], pq_id[wave], pq_j[wave], qn);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                hit = live && shit[wave][lane] != 0u;
             } else {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
@@ -3230,6 +3238,17 @@ __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, ui
     }
 }
 
+// RT580_CELL_RAYS=k (A/B): items of >= k rays in far_cell_any_kernel's
+// ray-per-lane form (0: every item in the pair form)
+static uint32_t cell_rays_min() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_CELL_RAYS");
+        v = e ? atoi(e) : 0;
+    }
+    return (uint32_t)v;
+}
+
 // The any-hit far pass over the sorted queue [0, n) (far-origin rays
 // excluded): segments of one key (run-length encoding of the sorted keys into
 // far_keys / far_vals -- the sort's inputs, free now -- and the exclusive scan
@@ -3267,7 +3286,7 @@ static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t
     if (closest)
         hipLaunchKernelGGL(far_cell_closest_kernel, cgrid, dim3(TB), 0, s, S, W);
     else
-        hipLaunchKernelGGL(far_cell_any_kernel, cgrid, dim3(TB), 0, s, S, W, n, flag);
+        hipLaunchKernelGGL(far_cell_any_kernel, cgrid, dim3(TB), 0, s, S, W, n, flag, cell_rays_min());
 #ifdef RT580_DIAGNOSTICS
     {
         uint32_t nw[2] = {0, 0};
@@ -3362,6 +3381,61 @@ __global__ void math_selftest_kernel(uint64_t seed, uint64_t n, unsigned long lo
 // The device restatement of glibc powf (rt_libm.h), as CalculateLocalColor
 // calls it (Raytracer.cpp:253), over caller-given inputs: checked against the
 // host's glibc by tests/test_gpu_libm.py.
+// ---------------------------------------------------------------- mt19937 windows
+// The twist of a 624-word window (rt_mt.h: W_n = y_n .. y_{n+623} -> the next
+// 624 words, draws n .. n+623), in phases over a workgroup: words [0, 227) read
+// only old words, [227, 454) and [454, 623) the new words 227 before them, 623
+// also the new word 0 -- then every draw tempered (libstdc++ random.tcc / MSVC).
+__device__ __forceinline__ uint32_t mt_twist(uint32_t yn, uint32_t yn1, uint32_t yn397) {
+    const uint32_t y = (yn & 0x80000000u) | (yn1 & 0x7fffffffu);
+    return yn397 ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+__global__ void __launch_bounds__(TB) mt_generate_kernel(const uint32_t* __restrict__ windows, uint64_t k0,
+                                                         uint64_t lo, uint64_t hi, uint32_t* __restrict__ out) {
+    __shared__ uint32_t buf[2][624];
+    const uint64_t blk = (uint64_t)kMtBlock;
+    const uint64_t start = (k0 + blockIdx.x) * blk;  // absolute index of this block's first draw
+    const uint32_t* w = windows + (size_t)blockIdx.x * 624;
+    for (int i = threadIdx.x; i < 624; i += TB) buf[0][i] = w[i];
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t d0 = start; d0 < start + blk && d0 < hi; d0 += 624) {
+        const uint32_t* o = buf[cur];
+        uint32_t* n = buf[cur ^ 1];
+        const int i = threadIdx.x;
+        if (i < 227) n[i] = mt_twist(o[i], o[i + 1], o[i + 397]);
+        __syncthreads();
+        if (i < 227) n[227 + i] = mt_twist(o[227 + i], o[228 + i], n[i]);
+        __syncthreads();
+        if (i < 169) n[454 + i] = mt_twist(o[454 + i], o[455 + i], n[227 + i]);
+        __syncthreads();
+        if (i == 0) n[623] = mt_twist(o[623], n[0], n[396]);
+        __syncthreads();
+        for (int k = threadIdx.x; k < 624; k += TB) {
+            const uint64_t d = d0 + (uint64_t)k;
+            if (d >= lo && d < hi) out[d - lo] = mt_temper(n[k]);
+        }
+        cur ^= 1;
+        // (the next twist writes buf[cur ^ 1], which this one read: the barriers above order it)
+        __syncthreads();
+    }
+}
+
+hipError_t launch_mt_generate(const uint32_t* windows, uint64_t k0, uint32_t nblk, uint64_t lo, uint64_t hi,
+                              uint32_t* out, hipStream_t s) {
+    if (nblk == 0 || hi <= lo) return hipSuccess;
+    hipLaunchKernelGGL(mt_generate_kernel, dim3(nblk), dim3(TB), 0, s, windows, k0, lo, hi, out);
+    return hipGetLastError();
+}
+
 __global__ void powf_eval_kernel(const float* __restrict__ x, float y, float* __restrict__ out, uint64_t n) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         out[i] = rt_glibc_powf(x[i], y);
@@ -3780,13 +3854,9 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
                 else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
-                    // (the late counts and the per-XCD block queues of XQ = 1)
-                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 64, s)) != hipSuccess) return e;
+                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
                     const int bu = ao_budget();
-                    if (ao_xcdq() && bu == 4)
-                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4, 1>), dim3(grid_for(e1 - b, 16384)),
-                                           dim3(TB), 0, s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    else if (bu <= 2)
+                    if (bu <= 2)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 2>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     else if (bu == 3)
@@ -3806,6 +3876,11 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                         hipLaunchKernelGGL((ao_late_kernel<6, 16, 16, 0>), dim3(4096), dim3(TB), 0, s, S, W);
                         hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 1>), dim3(1024), dim3(TB), 0, s, S, W);
                     } else {
+#ifdef RT580_DIAGNOSTICS
+                        if (late_wpe() == 8 && late_reread() == 0)
+                            hipLaunchKernelGGL((ao_late_kernel<8, 16, 0, 0, 0>), dim3(4096), dim3(TB), 0, s, S, W);
+                        else
+#endif
                         if (late_wpe() == 8)
                             hipLaunchKernelGGL((ao_late_kernel<8, 16>), dim3(4096), dim3(TB), 0, s, S, W);
                         else

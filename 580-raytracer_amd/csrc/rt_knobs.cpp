@@ -81,7 +81,6 @@ const Knob kKnobs[] = {
     {"RT580_AO_BUDGET", INT_RANGE, 0, 64, nullptr, nullptr},
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
     {"RT580_AO_RESUME", INT_SET, 0, 0, k01, nullptr},
-    {"RT580_AO_XCDQ", INT_SET, 0, 0, k01, nullptr},
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
     {"RT580_NEAR_WPE", INT_SET, 0, 0, kNearWpe, nullptr},
     {"RT580_LATE_WPE", INT_SET, 0, 0, kLateWpe, nullptr},
@@ -91,6 +90,7 @@ const Knob kKnobs[] = {
     {"RT580_FAR_MODE", INT_SET, 0, 0, kFarMode, nullptr},
     {"RT580_FAR_U", INT_SET, 0, 0, kFarU, nullptr},
     {"RT580_FAR_CLOSEST_U", INT_SET, 0, 0, kFarCU, nullptr},
+    {"RT580_CELL_RAYS", INT_RANGE, 0, 64, nullptr, nullptr},
     {"RT580_SORT_BITS", INT_SET, 0, 0, k01, nullptr},
     {"RT580_DEEP_GRID", INT_RANGE, 64, 65536, nullptr, nullptr},
     {"RT580_AO_GRID", INT_RANGE, 256, 1 << 20, nullptr, nullptr},
@@ -105,6 +105,7 @@ const Knob kKnobs[] = {
     {"RT580_REPLAY_CORRUPT", DIAG_ONLY, 0, 0, nullptr, nullptr},
     {"RT580_CELL_SKIP", DIAG_ONLY, 0, 0, nullptr, nullptr},
     {"RT580_AO_VERIFY", DIAG_ONLY, 0, 0, nullptr, nullptr},
+    {"RT580_LATE_REREAD", DIAG_ONLY, 0, 0, nullptr, nullptr},
     // read by the Python binding and the tests, not by the library
     {"RT580_LIB", NOT_LIBRARY, 0, 0, nullptr, nullptr},
     {"RT580_EXHAUSTIVE", NOT_LIBRARY, 0, 0, nullptr, nullptr},

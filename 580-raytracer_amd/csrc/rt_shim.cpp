@@ -24,6 +24,7 @@
 #include "rt_bvh.h"
 #include "rt_kernels.h"
 #include "rt_knobs.h"
+#include "rt_mt.h"
 
 using namespace rt580;
 
@@ -42,7 +43,8 @@ struct Slot {
     hipEvent_t ao_done = nullptr;  // end of the AO kernels of the slot's last frame
     DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
         row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream, aofix_items, aofix_count,
-        call_hint;
+        call_hint, mt_windows;
+    uint64_t mt_base = 0;  // absolute index of mt_stream's first draw
     // BVH frames: the far queue, the AO ray records and the split trace's
     // provisional hits -- per slot, so that consecutive BVH frames overlap
     // like the others (count schedule replay, see trace_rows)
@@ -599,6 +601,7 @@ DevWork dev_work() {
     w.call_rng = (uint64_t*)SL.call_rng.p;
     w.occ = (uint32_t*)SL.occ.p;
     w.mt_stream = (const uint32_t*)SL.mt_stream.p;
+    w.mt_base = SL.mt_base;
     w.node_cap = g.node_cap;
     w.call_cap = g.call_cap;
     w.far_rays = (float4*)SL.far_rays.p;
@@ -878,47 +881,51 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     return RT_SUCCESS;
 }
 
-// mt19937: the reference's serial stream is generated on the host up to the
-// last draw these rows need, then uploaded (draws are addressed by absolute
-// index). Single call: the local total; multi-rank rows: max over the rows of
-// (global row base + the row's AO calls).
+// mt19937: the draws these rows need, [lo, hi) of the reference's serial
+// stream (single call: [0, the local total); multi-rank rows: from the lowest
+// to the highest draw of their global row bases), generated on the device:
+// the host supplies the stream's checkpoint windows at every kMtBlock draws
+// (rt_mt.h block jump-ahead, cached per seed for later frames), one workgroup
+// per block runs the twist (launch_mt_generate). Draws are addressed by
+// absolute index minus the window's base.
+constexpr uint64_t kMtMaxWindow = 1ull << 34;  // draws held at once (64 GiB of the 288 GB)
+
 int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global, int n_rows) {
     if (p->rng_engine != RT_RNG_MT19937 || !p->ao_enabled || g.n_ambient == 0) return RT_SUCCESS;
-    uint64_t total = 0;
+    uint64_t lo_call = 0, hi_call = 0;
     if (!row_base_global) {
-        if (copy_d2h(&total, SL.totals.p, 8, fs(), "the AO-call total")) return RT_FAILURE;
+        if (copy_d2h(&hi_call, SL.totals.p, 8, fs(), "the AO-call total")) return RT_FAILURE;
     } else if (n_rows > 0) {
         std::vector<uint64_t> base((size_t)n_rows);
         std::vector<uint32_t> calls((size_t)n_rows);
         if (copy_d2h(base.data(), row_base_global, (size_t)n_rows * 8, fs(), "the row bases") ||
             copy_d2h(calls.data(), SL.row_calls.p, (size_t)n_rows * 4, fs(), "the per-row AO calls"))
             return RT_FAILURE;
-        for (int i = 0; i < n_rows; i++) total = std::max(total, base[i] + calls[i]);
+        lo_call = ~0ull;
+        for (int i = 0; i < n_rows; i++)
+            if (calls[(size_t)i]) {
+                lo_call = std::min(lo_call, base[(size_t)i]);
+                hi_call = std::max(hi_call, base[(size_t)i] + calls[(size_t)i]);
+            }
+        if (lo_call > hi_call) lo_call = hi_call;
     }
-    const uint64_t n = total * 2ull * (uint64_t)p->ao_samples;
-    // the stream is generated serially and lives on the device whole: bounded
-    // (16 GiB) until the engine has a block jump-ahead
-    constexpr uint64_t kMtMaxDraws = 1ull << 32;
-    if (n > kMtMaxDraws)
-        return fail("mt19937: these rows need %llu serial draws, above the %llu this build generates (use "
+    const uint64_t per_call = 2ull * (uint64_t)p->ao_samples;
+    const uint64_t lo = lo_call * per_call, hi = hi_call * per_call;
+    if (hi - lo > kMtMaxWindow)
+        return fail("mt19937: these rows need draws [%llu, %llu), more than the %llu one window holds (use "
                     "minstd_rand0, or fewer rows per call)",
-                    (unsigned long long)n, (unsigned long long)kMtMaxDraws);
-    if (ensure(SL.mt_stream, n * 4 + 8) || xfer_ready()) return RT_FAILURE;
-    // generated straight into the pinned transfer buffer, chunk by chunk
-    std::mt19937 gen(p->rng_seed);
-    const size_t per = kXferHalf / 4;
-    bool used[2] = {false, false};
-    int h = 0;
-    for (uint64_t off = 0; off < n; off += per, h ^= 1) {
-        const size_t c = n - off < per ? (size_t)(n - off) : per;
-        if (used[h]) HIP_TRY(hipEventSynchronize(g.xfer_ev[h]));
-        uint32_t* b = reinterpret_cast<uint32_t*>(g.xfer + (size_t)h * kXferHalf);
-        for (size_t i = 0; i < c; i++) b[i] = (uint32_t)gen();
-        HIP_TRY(hipMemcpyAsync((uint32_t*)SL.mt_stream.p + off, b, c * 4, hipMemcpyHostToDevice, fs()));
-        HIP_TRY(hipEventRecord(g.xfer_ev[h], fs()));
-        used[h] = true;
-    }
-    return stream_sync(fs(), "by the upload of the mt19937 stream");
+                    (unsigned long long)lo, (unsigned long long)hi, (unsigned long long)kMtMaxWindow);
+    SL.mt_base = lo;
+    if (hi == lo) return RT_SUCCESS;
+    const uint64_t k0 = lo / kMtBlock, k1 = (hi + kMtBlock - 1) / kMtBlock;
+    const uint32_t nblk = (uint32_t)(k1 - k0);
+    if (ensure(SL.mt_stream, (hi - lo) * 4 + 8) || ensure(SL.mt_windows, (size_t)nblk * sizeof(MtWindow)))
+        return RT_FAILURE;
+    const MtWindow* cps = mt_checkpoints(p->rng_seed, k0, k1);
+    if (copy_h2d(SL.mt_windows.p, cps, (size_t)nblk * sizeof(MtWindow), fs(), "the mt19937 checkpoint windows"))
+        return RT_FAILURE;
+    HIP_TRY(launch_mt_generate((const uint32_t*)SL.mt_windows.p, k0, nblk, lo, hi, (uint32_t*)SL.mt_stream.p, fs()));
+    return RT_SUCCESS;
 }
 
 // AO phases in frame order (RT580_AO_ORDER=1, rt580_set_ao_order): a frame's
@@ -1801,7 +1808,7 @@ void shutdown_ctx() {
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
                           &sl.row_calls, &sl.row_hits, &sl.row_nodes, &sl.row_base_local, &sl.totals, &sl.call_node,
-                          &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.mt_stream, &sl.aofix_items, &sl.aofix_count,
+                          &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.mt_stream, &sl.mt_windows, &sl.aofix_items, &sl.aofix_count,
                           &sl.call_hint, &sl.ao_rays, &sl.ao_state, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
                           &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.far_count, &sl.far_seg_off,
                           &sl.far_seg_n, &sl.far_wofs, &sl.far_work, &sl.sort_tmp, &sl.hit4, &sl.hit_prim, &sl.shadow,

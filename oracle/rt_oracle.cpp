@@ -397,7 +397,8 @@ static int load_scene(Scene& sc, const std::string& root, const std::string& pat
 // (random.h, random.tcc:3348-3378). MSVC: mt19937, seed 5489.
 struct DrawSource {
     int engine = 0;
-    std::vector<uint32_t> stream;  // engine 1: pre-generated outputs
+    std::vector<uint32_t> stream;  // engine 1: pre-generated outputs [lo, lo + size)
+    uint64_t lo = 0;
     static uint64_t mulmod(uint64_t a, uint64_t b) { return (a * b) % 2147483647ull; }
     static uint64_t powmod(uint64_t a, uint64_t e) {
         uint64_t r = 1;
@@ -419,7 +420,7 @@ struct RngCursor {  // one thread's position in the global draw stream
             state = (state * 16807ull) % 2147483647ull;
             ret = (float)(unsigned long)(state - 1) / 2147483648.0f;
         } else {
-            uint32_t x = src->stream[index];
+            uint32_t x = src->stream[index - src->lo];
             ret = (float)(unsigned long)x / 4294967296.0f;
         }
         index++;
@@ -1072,6 +1073,10 @@ extern "C" int oracle_time_prefix(const char* assets_root, const char* scene, in
 // pixel and the row's AO-call total (-> row_calls[k], compared with the GPU's
 // count by the caller); then the segments' pixels are shaded. Work items are
 // pixels on `threads` threads. fb: sum(n) x 3 int16, segment after segment.
+// RNG engine of oracle_render_segments: 0 minstd_rand0 (default), 1 mt19937.
+static int g_seg_engine = 0;
+extern "C" void oracle_set_segments_engine(int engine) { g_seg_engine = engine == 1 ? 1 : 0; }
+
 extern "C" int oracle_render_segments(const char* assets_root, const char* scene, int w, int h, int depth,
                                       int ao_samples, int threads, int n_seg, const int32_t* seg_y,
                                       const int32_t* seg_x0, const int32_t* seg_n, const uint64_t* row_base,
@@ -1126,9 +1131,24 @@ extern "C" int oracle_render_segments(const char* assets_root, const char* scene
         row_calls[k] = tot;
     }
     DrawSource src;
-    src.engine = 0;
+    src.engine = g_seg_engine;
     const uint64_t per_call = 2ull * (uint64_t)ao_samples;
     const int64_t npx = off[(size_t)n_seg];
+    if (src.engine == 1 && n_seg > 0) {
+        // mt19937 (seed 5489): the draws of the segments' rows, [lo, hi) of the
+        // serial stream, by the engine itself (discard = the reference's own
+        // stepping, however far out the rows start)
+        uint64_t lo = ~0ull, hi = 0;
+        for (int k = 0; k < n_seg; k++) {
+            lo = std::min(lo, row_base[k] * per_call);
+            hi = std::max(hi, (row_base[k] + row_calls[k]) * per_call);
+        }
+        std::mt19937 g;
+        g.discard(lo);
+        src.lo = lo;
+        src.stream.resize((size_t)(hi - lo));
+        for (auto& x : src.stream) x = (uint32_t)g();
+    }
     std::vector<Counters> pc((size_t)npx);
     {
         std::atomic<int64_t> next{0};

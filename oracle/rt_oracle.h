@@ -59,6 +59,9 @@ int oracle_time_prefix(const char* assets_root, const char* scene, int w, int h,
 // seg_n[k]) of rows seg_y[k], row k's first AO call at row_base[k] (absolute
 // index, minstd_rand0). row_calls[k] <- the AO calls of the whole row seg_y[k].
 // fb: sum(seg_n) x 3 int16; counters as oracle_render (segment pixels only).
+/* RNG engine of oracle_render_segments: 0 minstd_rand0 (default), 1 mt19937 (the draws
+ * of the segments' rows generated from the serial stream at their row bases). */
+void oracle_set_segments_engine(int engine);
 int oracle_render_segments(const char* assets_root, const char* scene, int w, int h, int depth, int ao_samples,
                            int threads, int n_seg, const int32_t* seg_y, const int32_t* seg_x0,
                            const int32_t* seg_n, const uint64_t* row_base, int16_t* fb, uint64_t* row_calls,

@@ -175,10 +175,12 @@ def oracle_time_prefix(scene, w, h, depth, ao_samples, p0, max_pixels, budget_s=
     return fb[:done.value], dict(zip(keys, (int(x) for x in cnt))), secs.value
 
 
-def oracle_render_segments(scene, w, h, depth, ao_samples, segments, row_base, threads=0, root=ASSETS_ROOT):
+def oracle_render_segments(scene, w, h, depth, ao_samples, segments, row_base, threads=0, root=ASSETS_ROOT,
+                           engine=0):
     """Pixels of a full w x h frame at segments [(y, x0, n), ...] (hoisted mode,
     threaded), row y's first AO call at row_base[k] -> (list of int16 (n, 3)
-    arrays, the AO calls of each segment's whole row, counters, seconds)."""
+    arrays, the AO calls of each segment's whole row, counters, seconds).
+    engine 1: mt19937, the rows' draws taken from the serial stream at their bases."""
     lib = oracle_lib()
     f = lib.oracle_render_segments
     f.restype = ctypes.c_int
@@ -195,9 +197,13 @@ def oracle_render_segments(scene, w, h, depth, ao_samples, segments, row_base, t
     cnt = np.zeros(6, dtype=np.uint64)
     secs = ctypes.c_double(0)
     lib.oracle_set_mode(0)
-    st = f(os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples, threads, len(segments), ys.ctypes.data,
-           x0.ctypes.data, ns.ctypes.data, base.ctypes.data, fb.ctypes.data, calls.ctypes.data, cnt.ctypes.data,
-           ctypes.byref(secs))
+    lib.oracle_set_segments_engine(engine)
+    try:
+        st = f(os.fsencode(root), os.fsencode(scene), w, h, depth, ao_samples, threads, len(segments), ys.ctypes.data,
+               x0.ctypes.data, ns.ctypes.data, base.ctypes.data, fb.ctypes.data, calls.ctypes.data, cnt.ctypes.data,
+               ctypes.byref(secs))
+    finally:
+        lib.oracle_set_segments_engine(0)
     assert st == 0, "oracle_render_segments failed"
     out, o = [], 0
     for n in ns:

@@ -119,3 +119,45 @@ def test_render_multi_follows_scene_and_device_set():
         full, _ = render_gpu(scene, w, h, depth, ao, True, root=r)
         got = _multi(scene, w, h, depth, ao, G, root=r)
         assert np.array_equal(got, full), (scene, G)
+
+
+def test_mt19937_rows_past_two_to_the_32_draws():
+    """MSVC's engine from far out in the serial stream (the host
+    stream stopped at 2^32 draws): rows shaded through the multi-rank split
+    with row bases moved 2^32 / 8 + 12,345 AO calls out (8 draws per call at AO
+    4), so every draw lies beyond 2^32 -- the device generates them from the
+    block jump-ahead's checkpoint windows -- against the oracle, which steps
+    std::mt19937 itself to the rows' first draw."""
+    import torch
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    d = helpers.rt580_dist()
+    scene, w, h, depth, ao = "simpleSphereScene.json", 48, 32, 2, 4
+    rt = rt580.Raytracer(w, h, helpers.ASSETS_ROOT)
+    assert rt.LoadSceneJSON(scene) == 0
+    rt.set_depth(depth)
+    rt.set_ao(ao, True)
+    rt.set_rng(1)
+    assert rt.InitializeRenderer() == 0
+    params = rt.render_params()
+    s = rt.scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    dev = torch.device("cuda", 0)
+    rt580.check(lib.rt_gpu_set_stream(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "stream")
+    offset = (1 << 32) // 8 + 12345
+    try:
+        rows = d.GpuRows(rt580, params, torch, dev)
+        cnt = rows.count(0, 1)[:h].to(torch.int64)
+        base = torch.cumsum(cnt, 0) - cnt + offset
+        fb = rows.shade(0, 1, base).view(h, w, 3).cpu().numpy()
+        torch.cuda.synchronize()
+    finally:
+        lib.rt_gpu_set_stream(lib.rt_gpu_own_stream())
+    ys = [y for y in range(h) if int(cnt[y])]
+    assert ys and int(base[ys[0]]) * 8 > (1 << 32)
+    px, calls, _, _ = helpers.oracle_render_segments(scene, w, h, depth, ao, [(y, 0, w) for y in ys],
+                                                     [int(base[y]) for y in ys], engine=1)
+    assert calls == [int(cnt[y]) for y in ys]
+    for y, p in zip(ys, px):
+        assert np.array_equal(fb[y], p), "row %d" % y
+    rt.close()

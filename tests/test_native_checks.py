@@ -100,3 +100,16 @@ def test_bvh_queries_equal_brute_force(scene, rays, far):
     assert "bvh4 nodes=0\n" not in out and "bvh4_mismatches=0" in out, out  # the 4-wide any-hit tree
     if scene == "cornell10k":
         assert "differ_without_far_search=0 " not in out, out
+
+
+def test_mt19937_block_jump_ahead_equals_the_engine():
+    """rt_mt.h: the window W_J reached by the polynomial jump (x^(J-1) mod phi,
+    phi from Berlekamp-Massey) yields std::mt19937's draws J, J+1, ... after
+    discard(J), around the twist boundaries and 2e8 draws out; block
+    checkpoints equal direct jumps; a jump to 2^33 + 5 split in two equals the
+    whole one (the device generator starts from these windows)."""
+    exe = os.path.join(BUILD, "mt_check")
+    os.makedirs(BUILD, exist_ok=True)
+    subprocess.run(["g++"] + FLAGS + ["-o", exe, os.path.join(NATIVE, "mt_check.cpp"),
+                                      os.path.join(helpers.PKG, "csrc", "rt_mt.cpp")], check=True)
+    _run(exe, "200000000")

@@ -137,3 +137,22 @@ def test_simd_triangle_scan_matches_scalar_loop():
         assert p.returncode == 0, p.stderr
         outs.append(json.loads(p.stdout.strip().splitlines()[-1]))
     assert outs[0] == outs[1]
+
+
+def test_oracle_segments_mt19937_window_equals_full_stream():
+    """oracle_render_segments with engine 1 generates only its rows' draws
+    (std::mt19937 discard to the first): the rows equal oracle_render's full
+    frame from draw 0 (the GPU test past 2^32 draws compares against this mode)."""
+    scene, w, h, depth, ao = "simpleSphereScene.json", 40, 30, 2, 4
+    full, _ = helpers.oracle_render(scene, w, h, depth, ao, True, engine=1)
+    calls = []
+    for y in range(h):
+        _, c, _, _ = helpers.oracle_render_segments(scene, w, h, depth, ao, [(y, 0, w)], [0])
+        calls.append(c[0])
+    base = np.concatenate([[0], np.cumsum(calls)[:-1]]).astype(np.uint64)
+    rows = [y for y in range(h) if calls[y]][-6:]
+    px, c2, _, _ = helpers.oracle_render_segments(scene, w, h, depth, ao, [(y, 0, w) for y in rows],
+                                                  [int(base[y]) for y in rows], engine=1)
+    assert c2 == [calls[y] for y in rows]
+    for y, p in zip(rows, px):
+        assert np.array_equal(p, full[y]), y
