@@ -81,6 +81,7 @@ const Knob kKnobs[] = {
     {"RT580_AO_BUDGET", INT_RANGE, 0, 64, nullptr, nullptr},
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
     {"RT580_AO_RESUME", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_AO_BLOCK", INT_RANGE, 0, 20, nullptr, nullptr},
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
     {"RT580_NEAR_WPE", INT_SET, 0, 0, kNearWpe, nullptr},
     {"RT580_LATE_WPE", INT_SET, 0, 0, kLateWpe, nullptr},
@@ -90,7 +91,6 @@ const Knob kKnobs[] = {
     {"RT580_FAR_MODE", INT_SET, 0, 0, kFarMode, nullptr},
     {"RT580_FAR_U", INT_SET, 0, 0, kFarU, nullptr},
     {"RT580_FAR_CLOSEST_U", INT_SET, 0, 0, kFarCU, nullptr},
-    {"RT580_CELL_RAYS", INT_RANGE, 0, 64, nullptr, nullptr},
     {"RT580_SORT_BITS", INT_SET, 0, 0, k01, nullptr},
     {"RT580_DEEP_GRID", INT_RANGE, 64, 65536, nullptr, nullptr},
     {"RT580_AO_GRID", INT_RANGE, 256, 1 << 20, nullptr, nullptr},
