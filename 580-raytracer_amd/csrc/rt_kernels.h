@@ -221,6 +221,8 @@ void kernel_timer_release();
 // in raster order.
 hipError_t launch_deinterleave(const int16_t* tiles, int world, int n_max, int width, int height, int16_t* out,
                                hipStream_t s);
+hipError_t launch_deinterleave_u8(const uint8_t* tiles, int world, int n_max, int width, int height, uint8_t* out,
+                                  hipStream_t s);
 hipError_t launch_copy_rows(const int16_t* src, int width, int row_begin, int row_step, int n_rows,
                             int16_t* dst, hipStream_t s);
 

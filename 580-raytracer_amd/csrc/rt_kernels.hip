@@ -3462,8 +3462,10 @@ __global__ void copy_rows_kernel(const int16_t* __restrict__ src, int width, int
     dst[i] = src[(size_t)(row_begin + k * row_step) * per_row + e];
 }
 
-__global__ void deinterleave_kernel(const int16_t* __restrict__ tiles, int world, int n_max, int width, int height,
-                                    int16_t* __restrict__ out) {
+// (T = int16_t: the Pixel framebuffer; uint8_t: the PPM body)
+template <typename T>
+__global__ void deinterleave_kernel(const T* __restrict__ tiles, int world, int n_max, int width, int height,
+                                    T* __restrict__ out) {
     const size_t per_row = (size_t)width * 3;
     const size_t total = per_row * (size_t)height;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -3477,8 +3479,17 @@ hipError_t launch_deinterleave(const int16_t* tiles, int world, int n_max, int w
                                hipStream_t s) {
     const uint64_t n = (uint64_t)width * 3 * height;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(deinterleave_kernel, dim3(grid_for(n, 16384)), dim3(256), 0, s, tiles, world, n_max, width,
-                       height, out);
+    hipLaunchKernelGGL(deinterleave_kernel<int16_t>, dim3(grid_for(n, 16384)), dim3(256), 0, s, tiles, world, n_max,
+                       width, height, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_deinterleave_u8(const uint8_t* tiles, int world, int n_max, int width, int height, uint8_t* out,
+                                  hipStream_t s) {
+    const uint64_t n = (uint64_t)width * 3 * height;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(deinterleave_kernel<uint8_t>, dim3(grid_for(n, 16384)), dim3(256), 0, s, tiles, world, n_max,
+                       width, height, out);
     return hipGetLastError();
 }
 

@@ -43,7 +43,7 @@ struct Slot {
     hipEvent_t ao_done = nullptr;  // end of the AO kernels of the slot's last frame
     DevBuf nodes, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
         row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream, aofix_items, aofix_count,
-        call_hint, mt_windows;
+        call_hint, mt_windows, fb8;
     uint64_t mt_base = 0;  // absolute index of mt_stream's first draw
     // BVH frames: the far queue, the AO ray records and the split trace's
     // provisional hits -- per slot, so that consecutive BVH frames overlap
@@ -1245,17 +1245,26 @@ uint64_t rt_gpu_scene_id(void) { return g.inited && g.have_scene ? g.scene_gen :
 // The frame of rt_gpu_render_device; with fb_host (a registered range of the
 // selected rows' bytes) also its D2H copy on the frame's slot stream, before
 // the slot's end, so the caller's stream waits for the copy too.
-static int render_device_frame(const rt_render_params* p, int16_t** fb_device, int16_t* fb_host);
+// host: a registered range receiving the selected rows as the int16
+// framebuffer (u8 = false) or as the PPM body (u8 = true: FlushFrameBufferToPPM's
+// pixel mapping on the device first, rt_gpu_gamma_u8, half the bytes).
+static int render_device_frame(const rt_render_params* p, int16_t** fb_device, void* host, bool u8);
 
 int rt_gpu_render_device(const rt_render_params* p, int16_t** fb_device) {
     RT_WORK("rt_gpu_render_device");
-    return render_device_frame(p, fb_device, nullptr);
+    return render_device_frame(p, fb_device, nullptr, false);
 }
 
 int rt_gpu_render_async(const rt_render_params* p, int16_t* fb_host) {
     RT_WORK("rt_gpu_render_async");
     if (!fb_host) return fail("rt_gpu_render_async: NULL framebuffer");
-    return render_device_frame(p, nullptr, fb_host);
+    return render_device_frame(p, nullptr, fb_host, false);
+}
+
+int rt_gpu_render_async_ppm(const rt_render_params* p, uint8_t* ppm_body_host) {
+    RT_WORK("rt_gpu_render_async_ppm");
+    if (!ppm_body_host) return fail("rt_gpu_render_async_ppm: NULL buffer");
+    return render_device_frame(p, nullptr, ppm_body_host, true);
 }
 
 static HostRange* host_range(const void* p, size_t bytes) {
@@ -1265,24 +1274,41 @@ static HostRange* host_range(const void* p, size_t bytes) {
     return nullptr;
 }
 
-static int render_device_frame(const rt_render_params* p, int16_t** fb_device, int16_t* fb_host) {
+// The registered range of `bytes` at `host` with its copy-ordering event on
+// this context's device (created on first use); null when not registered.
+static HostRange* host_range_ready(const void* host, size_t bytes) {
+    HostRange* hr = host_range(host, bytes);
+    if (!hr) return nullptr;
+    if (hr->copied && hr->copied_device != g.device) {
+        (void)hipEventDestroy(hr->copied);
+        hr->copied = nullptr;
+    }
+    if (!hr->copied) {
+        if (hipEventCreateWithFlags(&hr->copied, hipEventDisableTiming) != hipSuccess) return nullptr;
+        hr->copied_device = g.device;
+        if (hipEventRecord(hr->copied, g.stream) != hipSuccess) return nullptr;
+    }
+    return hr;
+}
+
+// src (device) -> host on stream s, after the previous copy into the same range
+static int ordered_d2h(HostRange* hr, void* host, const void* src, size_t bytes, hipStream_t s) {
+    HIP_TRY(hipStreamWaitEvent(s, hr->copied, 0));
+    HIP_TRY(hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(hr->copied, s));
+    return RT_SUCCESS;
+}
+
+static int render_device_frame(const rt_render_params* p, int16_t** fb_device, void* host, bool u8) {
     if (check_params(p)) return RT_FAILURE;
     HIP_TRY(hipSetDevice(g.device));
     HostRange* hr = nullptr;
-    if (fb_host) {
-        hr = host_range(fb_host, (size_t)n_selected_rows(p) * p->width * 6);
+    const size_t host_bytes = (size_t)n_selected_rows(p) * p->width * (u8 ? 3 : 6);
+    if (host) {
+        hr = host_range_ready(host, host_bytes);
         if (!hr)
-            return fail("rt_gpu_render_async: the framebuffer is not a registered range of %zu bytes "
-                        "(rt_gpu_host_register)", (size_t)n_selected_rows(p) * p->width * 6);
-        if (hr->copied && hr->copied_device != g.device) {
-            (void)hipEventDestroy(hr->copied);
-            hr->copied = nullptr;
-        }
-        if (!hr->copied) {
-            HIP_TRY(hipEventCreateWithFlags(&hr->copied, hipEventDisableTiming));
-            hr->copied_device = g.device;
-            HIP_TRY(hipEventRecord(hr->copied, g.stream));
-        }
+            return fail("%s: the buffer is not a registered range of %zu bytes (rt_gpu_host_register)", g_call,
+                        host_bytes);
     }
     const int n_sel = n_selected_rows(p);
     const bool prefix = p->row_begin == 0 && p->row_step == 1;
@@ -1312,10 +1338,12 @@ static int render_device_frame(const rt_render_params* p, int16_t** fb_device, i
         bool retry = false;
         if (check_capacity(p, retry)) return RT_FAILURE;
         if (!retry) {
-            if (hr) {  // the frame to the host, after the previous copy into the same range
-                HIP_TRY(hipStreamWaitEvent(fs(), hr->copied, 0));
-                HIP_TRY(hipMemcpyAsync(fb_host, SL.fb.p, (size_t)n_sel * p->width * 6, hipMemcpyDeviceToHost, fs()));
-                HIP_TRY(hipEventRecord(hr->copied, fs()));
+            if (hr && u8) {  // the PPM body: gamma u8 on the device, then to the host
+                if (ensure(SL.fb8, host_bytes)) return RT_FAILURE;
+                HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, host_bytes, (uint8_t*)SL.fb8.p, fs()));
+                if (ordered_d2h(hr, host, SL.fb8.p, host_bytes, fs())) return RT_FAILURE;
+            } else if (hr) {  // the frame to the host, after the previous copy into the same range
+                if (ordered_d2h(hr, host, SL.fb.p, host_bytes, fs())) return RT_FAILURE;
             }
             if (end_slot()) return RT_FAILURE;
             if (fb_device) *fb_device = (int16_t*)SL.fb.p;
@@ -1813,7 +1841,7 @@ void shutdown_ctx() {
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
                           &sl.row_calls, &sl.row_hits, &sl.row_nodes, &sl.row_base_local, &sl.totals, &sl.call_node,
-                          &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.mt_stream, &sl.mt_windows, &sl.aofix_items, &sl.aofix_count,
+                          &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.fb8, &sl.mt_stream, &sl.mt_windows, &sl.aofix_items, &sl.aofix_count,
                           &sl.call_hint, &sl.ao_rays, &sl.ao_state, &sl.ao_key, &sl.ao_order, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
                           &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.far_count, &sl.far_seg_off,
                           &sl.far_seg_n, &sl.far_wofs, &sl.far_work, &sl.sort_tmp, &sl.hit4, &sl.hit_prim, &sl.shadow,
@@ -1925,6 +1953,17 @@ struct Multi {
     DevBuf row_calls[kMaxCtx], gathered[kMaxCtx], base[kMaxCtx], tile[kMaxCtx];  // on device k
     DevBuf root_tiles, frame;                                                     // on device 0
     hipEvent_t ready[kMaxCtx] = {};                                               // local transport
+    // rt_gpu_render_multi_async: a ring of per-frame buffer sets. Frame f + kRing
+    // reuses frame f's set only after every stream that read it has passed a
+    // wait on frame f + 1's exchange (count gather: each context waits on every
+    // other's event, or RCCL's own group), so any kRing >= 2 is safe; 3 matches
+    // the frames a context keeps in flight
+    static constexpr int kRing = 3;
+    int ring = 0;
+    DevBuf a_rc[kRing][kMaxCtx], a_gat[kRing][kMaxCtx], a_base[kRing][kMaxCtx], a_t16[kRing][kMaxCtx],
+        a_t8[kRing][kMaxCtx];                                                    // on device k
+    DevBuf a_root8[kRing], a_frame8[kRing];                                      // on device 0
+    hipEvent_t a_ready[kRing][kMaxCtx] = {};                                     // local transport
 } g_multi;
 
 void destroy_comms() {
@@ -1947,6 +1986,13 @@ void release_multi_ctx(int k) {
     for (DevBuf* b : {&g_multi.row_calls[k], &g_multi.gathered[k], &g_multi.base[k], &g_multi.tile[k]}) release(*b);
     if (g_multi.ready[k]) (void)hipEventDestroy(g_multi.ready[k]);
     g_multi.ready[k] = nullptr;
+    for (int r = 0; r < Multi::kRing; r++) {
+        for (DevBuf* b : {&g_multi.a_rc[r][k], &g_multi.a_gat[r][k], &g_multi.a_base[r][k], &g_multi.a_t16[r][k],
+                          &g_multi.a_t8[r][k]})
+            release(*b);
+        if (g_multi.a_ready[r][k]) (void)hipEventDestroy(g_multi.a_ready[r][k]);
+        g_multi.a_ready[r][k] = nullptr;
+    }
     g_multi.scene_of[k] = 0;
 }
 
@@ -1957,6 +2003,10 @@ void release_multi() {
         (void)hipSetDevice(g_ctx[0].device);
         release(g_multi.root_tiles);
         release(g_multi.frame);
+        for (int r = 0; r < Multi::kRing; r++) {
+            release(g_multi.a_root8[r]);
+            release(g_multi.a_frame8[r]);
+        }
     }
 }
 
@@ -2055,10 +2105,13 @@ int multi_finish(const rt_render_params* p, int n, int n_max, int16_t* fb_out) {
     return RT_SUCCESS;
 }
 
-int multi_render(const rt_render_params* p, int16_t* fb_out, int n, const int* devices) {
+// Contexts 1..n-1 on their devices with context 0's scene, and the
+// communicator of the device set. false: the caller renders on context 0 alone
+// (n == 1 without a forced RCCL transport).
+int multi_setup(const rt_render_params* p, int n, const int* devices, bool& single) {
+    single = false;
     if (check_params(p)) return RT_FAILURE;  // context 0: inited, scene resident
     if (n < 1 || n > kMaxCtx) return fail("rt_gpu_render_multi: %d devices outside [1, %d]", n, kMaxCtx);
-    if (!fb_out) return fail("rt_gpu_render_multi: fb_out is NULL");
     if (p->row_begin != 0 || p->row_step != 1 || p->row_end != p->height)
         return fail("rt_gpu_render_multi renders whole frames (row_begin 0, row_step 1, row_end height)");
     int devs[kMaxCtx];
@@ -2073,7 +2126,10 @@ int multi_render(const rt_render_params* p, int16_t* fb_out, int n, const int* d
     bool dup = false;
     for (int a = 0; a < n; a++)
         for (int b = a + 1; b < n; b++) dup = dup || devs[a] == devs[b];
-    if (n == 1 && tr != 1) return rt_gpu_render(p, fb_out);
+    if (n == 1 && tr != 1) {
+        single = true;
+        return RT_SUCCESS;
+    }
     const bool use_rccl = tr == 1 || (tr == 0 && !dup);
     if (use_rccl && dup) return fail("rt_gpu_render_multi: RCCL needs distinct devices");
     if (use_rccl && !rccl_load()) return fail("rt_gpu_render_multi: librccl.so.1 could not be loaded");
@@ -2108,6 +2164,14 @@ int multi_render(const rt_render_params* p, int16_t* fb_out, int n, const int* d
         g_multi.rccl = use_rccl;
         for (int k = 0; k < n; k++) g_multi.devs[k] = devs[k];
     }
+    return RT_SUCCESS;
+}
+
+int multi_render(const rt_render_params* p, int16_t* fb_out, int n, const int* devices) {
+    if (!fb_out) return fail("rt_gpu_render_multi: fb_out is NULL");
+    bool single = false;
+    if (multi_setup(p, n, devices, single)) return RT_FAILURE;
+    if (single) return rt_gpu_render(p, fb_out);
     // phase 1 on every device: trace its interleaved rows, count their AO calls
     const int H = p->height, W = p->width;
     const int n_max = (H + n - 1) / n;
@@ -2128,7 +2192,123 @@ int multi_render(const rt_render_params* p, int16_t* fb_out, int n, const int* d
     return multi_finish(p, n, n_max, fb_out);
 }
 
+// One frame of rt_gpu_render_multi_async: the same phases as multi_render on
+// the ring's next buffer set, the tiles mapped to PPM bytes on their devices
+// before the gather (half the bytes), the de-interleaved body copied into the
+// registered host range on context 0's stream -- and no wait anywhere: each
+// context keeps its frame slots in flight, the exchange and the copy of frame
+// f overlap the kernels of frame f + 1.
+int multi_frame_async(const rt_render_params* p, uint8_t* ppm_host, int n, const int* devices) {
+    if (!ppm_host) return fail("rt_gpu_render_multi_async: NULL buffer");
+    bool single = false;
+    if (multi_setup(p, n, devices, single)) return RT_FAILURE;
+    if (single) return rt_gpu_render_async_ppm(p, ppm_host);
+    const int H = p->height, W = p->width;
+    const int n_max = (H + n - 1) / n;
+    const size_t t16 = (size_t)n_max * W * 6, t8 = (size_t)n_max * W * 3, body = (size_t)H * W * 3;
+    g_cur = 0;
+    HostRange* hr = host_range_ready(ppm_host, body);
+    if (!hr) return fail("rt_gpu_render_multi_async: the buffer is not a registered range of %zu bytes", body);
+    const int r = g_multi.ring;
+    g_multi.ring = (r + 1) % Multi::kRing;
+    // phase 1
+    for (int k = 0; k < n; k++) {
+        g_cur = k;
+        HIP_TRY(hipSetDevice(g.device));
+        if (!g_multi.a_ready[r][k]) HIP_TRY(hipEventCreateWithFlags(&g_multi.a_ready[r][k], hipEventDisableTiming));
+        if (ensure(g_multi.a_rc[r][k], (size_t)n_max * 4) || ensure(g_multi.a_gat[r][k], (size_t)n * n_max * 4) ||
+            ensure(g_multi.a_base[r][k], (size_t)n_max * 8) || ensure(g_multi.a_t16[r][k], t16) ||
+            ensure(g_multi.a_t8[r][k], t8))
+            return RT_FAILURE;
+        HIP_TRY(hipMemsetAsync(g_multi.a_rc[r][k].p, 0, (size_t)n_max * 4, g.stream));
+        rt_render_params pk = *p;
+        pk.row_begin = k;
+        pk.row_step = n;
+        pk.row_end = H;
+        if (rt_gpu_count_rows(&pk, (uint32_t*)g_multi.a_rc[r][k].p)) return RT_FAILURE;
+    }
+    // the per-row AO-call counts, all-gathered
+    if (g_multi.rccl) {
+        RCCL_TRY(g_rccl.GroupStart());
+        for (int k = 0; k < n; k++) {
+            g_cur = k;
+            RCCL_TRY(g_rccl.AllGather(g_multi.a_rc[r][k].p, g_multi.a_gat[r][k].p, (size_t)n_max, ncclInt32,
+                                      g_multi.comms[k], g.stream));
+        }
+        RCCL_TRY(g_rccl.GroupEnd());
+    } else {
+        for (int k = 0; k < n; k++) {
+            g_cur = k;
+            HIP_TRY(hipSetDevice(g.device));
+            HIP_TRY(hipEventRecord(g_multi.a_ready[r][k], g.stream));
+        }
+        for (int k = 0; k < n; k++) {
+            g_cur = k;
+            HIP_TRY(hipSetDevice(g.device));
+            for (int j = 0; j < n; j++) {
+                HIP_TRY(hipStreamWaitEvent(g.stream, g_multi.a_ready[r][j], 0));
+                HIP_TRY(hipMemcpyPeerAsync((char*)g_multi.a_gat[r][k].p + (size_t)j * n_max * 4, g.device,
+                                           g_multi.a_rc[r][j].p, g_ctx[j].device, (size_t)n_max * 4, g.stream));
+            }
+        }
+    }
+    // phase 2, then each tile as PPM bytes
+    for (int k = 0; k < n; k++) {
+        g_cur = k;
+        HIP_TRY(hipSetDevice(g.device));
+        rt_render_params pk = *p;
+        pk.row_begin = k;
+        pk.row_step = n;
+        pk.row_end = H;
+        if (rt_gpu_row_bases((const int32_t*)g_multi.a_gat[r][k].p, n, n_max, H, k,
+                             (uint64_t*)g_multi.a_base[r][k].p) ||
+            rt_gpu_shade_rows(&pk, (const uint64_t*)g_multi.a_base[r][k].p, (int16_t*)g_multi.a_t16[r][k].p))
+            return RT_FAILURE;
+        HIP_TRY(launch_gamma_u8((const int16_t*)g_multi.a_t16[r][k].p, t8, (uint8_t*)g_multi.a_t8[r][k].p, g.stream));
+    }
+    // the tiles to device 0, de-interleaved, to the host
+    g_cur = 0;
+    HIP_TRY(hipSetDevice(g.device));
+    if (ensure(g_multi.a_root8[r], t8 * n) || ensure(g_multi.a_frame8[r], body)) return RT_FAILURE;
+    HIP_TRY(hipMemcpyAsync(g_multi.a_root8[r].p, g_multi.a_t8[r][0].p, t8, hipMemcpyDeviceToDevice, g.stream));
+    if (g_multi.rccl) {
+        RCCL_TRY(g_rccl.GroupStart());
+        for (int k = 1; k < n; k++) {
+            RCCL_TRY(g_rccl.Send(g_multi.a_t8[r][k].p, t8, ncclUint8, 0, g_multi.comms[k], g_ctx[k].stream));
+            RCCL_TRY(g_rccl.Recv((char*)g_multi.a_root8[r].p + (size_t)k * t8, t8, ncclUint8, k, g_multi.comms[0],
+                                 g_ctx[0].stream));
+        }
+        RCCL_TRY(g_rccl.GroupEnd());
+    } else {
+        for (int k = 1; k < n; k++) {
+            g_cur = k;
+            HIP_TRY(hipSetDevice(g.device));
+            HIP_TRY(hipEventRecord(g_multi.a_ready[r][k], g.stream));
+        }
+        g_cur = 0;
+        HIP_TRY(hipSetDevice(g.device));
+        for (int k = 1; k < n; k++) {
+            HIP_TRY(hipStreamWaitEvent(g.stream, g_multi.a_ready[r][k], 0));
+            HIP_TRY(hipMemcpyPeerAsync((char*)g_multi.a_root8[r].p + (size_t)k * t8, g.device, g_multi.a_t8[r][k].p,
+                                       g_ctx[k].device, t8, g.stream));
+        }
+    }
+    HIP_TRY(launch_deinterleave_u8((const uint8_t*)g_multi.a_root8[r].p, n, n_max, W, H,
+                                   (uint8_t*)g_multi.a_frame8[r].p, g.stream));
+    return ordered_d2h(hr, ppm_host, g_multi.a_frame8[r].p, body, g.stream);
+}
+
 }  // namespace
+
+extern "C" int rt_gpu_render_multi_async(const rt_render_params* p, uint8_t* ppm_body_host, int n_devices,
+                                         const int* devices) {
+    RT_WORK("rt_gpu_render_multi_async");
+    if (g_cur != 0) return fail("re-entered");
+    const int st = multi_frame_async(p, ppm_body_host, n_devices, devices);
+    g_cur = 0;
+    if (g.inited) (void)hipSetDevice(g.device);
+    return st;
+}
 
 extern "C" int rt_gpu_render_multi(const rt_render_params* p, int16_t* fb_out, int n_devices, const int* devices) {
     RT_WORK("rt_gpu_render_multi");

@@ -62,6 +62,7 @@ SIGNATURES = [
     ("rt_gpu_render", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
     ("rt_gpu_render_device", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.POINTER(ctypes.c_void_p)]),
     ("rt_gpu_render_async", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
+    ("rt_gpu_render_async_ppm", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
     ("rt_gpu_count_rows", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
     ("rt_gpu_shade_rows", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_void_p]),
     ("rt_gpu_last_stats", ctypes.c_int, [ctypes.POINTER(RenderStats)]),
@@ -72,6 +73,8 @@ SIGNATURES = [
     ("rt_gpu_set_accel", ctypes.c_int, [ctypes.c_int]),
     ("rt_gpu_render_multi", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
                                             ctypes.c_void_p]),
+    ("rt_gpu_render_multi_async", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_int,
+                                                  ctypes.c_void_p]),
     ("rt_gpu_device_count", ctypes.c_int, []),
     ("rt_gpu_gamma_u8", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     ("rt_gpu_row_bases", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

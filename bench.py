@@ -7,7 +7,7 @@ depth 4, 64 AO samples; the reference's own scene file) rendered from scratch
 by the reference's Render() loop (Raytracer.cpp:916-935): trace of the
 recursion tree, AO-call count + RNG-offset scan, AO kernel, resolve (+ for
 N > 1 the all-gather of per-row AO counts and the gather of the row tiles),
-and the int16 framebuffer copied into host memory. The scene is resident in
+and the frame copied into host memory. The scene is resident in
 HBM.
 
     python bench.py [--gpus N [--rehearse]] [--steps K] [--warmup W]
@@ -16,14 +16,15 @@ HBM.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Parallel modes (the row split of SURVEY §8e, byte-identical frames for every N):
-  * N = 1: rt_gpu_render_async into page-locked host buffers, up to three frames
-    in flight (each frame's D2H overlaps the next frames' kernels); the blocking
-    Render() latency is reported beside it.
-  * --gpus N without a launcher: rt_gpu_render_multi over devices 0..N-1 in this
-    process (what the drop-in Render() calls: single-process RCCL, framebuffer
-    on the host every step). N above the visible devices is an error;
-    --rehearse runs the same split on device 0 N times (device copies instead
-    of RCCL) to rehearse it on a one-GPU box.
+  * N = 1: rt_gpu_render_async_ppm into page-locked host buffers (the frame's
+    PPM body), up to three frames in flight (each frame's D2H overlaps the next
+    frames' kernels); the blocking Render() latency is reported beside it.
+  * --gpus N without a launcher: rt_gpu_render_multi_async over devices
+    0..N-1 in this process, the same step (single-process RCCL; each device
+    keeps its frame slots in flight, the gather and the D2H of one frame
+    overlap the next frame's kernels). N above the visible devices is an
+    error; --rehearse runs the same split on device 0 N times (device copies
+    instead of RCCL) to rehearse it on a one-GPU box.
   * under torch.distributed.run: one process per GPU (rt580_dist.DistFrame:
     RCCL all-gather of the counts, async gather of the u8 tiles to rank 0).
     --gpus must equal WORLD_SIZE.
@@ -178,7 +179,6 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     n_tri = sum(1 for i in range(sc.n_prims) if sc.prims[i].kind == 0)
     log("%s: scene uploaded (%d primitives, %.1f s incl. acceleration build)" % (name, sc.n_prims, upload_s))
 
-    host = None
     dframe = None
     dist_mod = helpers.rt580_dist() if ctx.dist_on else None
     if ctx.dist_on:
@@ -187,16 +187,17 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
             dframe = dist_mod.DistFrame(backend, ctx.dist, torch, H, W, ctx.rank, ctx.world, ctx.device)
     import numpy as np
     if ctx.multi:
-        host = np.zeros(W * H * 3, dtype=np.int16)
         devs = (ctypes.c_int * ctx.multi)(*ctx.devices)
-    # N = 1: each step's frame lands in host memory (SURVEY 8d's ms/frame ends
-    # with the framebuffer on the host): a ring of page-locked int16 buffers,
-    # one per frame in flight; rt_gpu_render_async queues the frame and its D2H
-    # copy, which overlaps the next frames' kernels
+    # one process (N = 1, or N devices of rt_gpu_render_multi_async): each
+    # step's frame lands in host memory as the PPM body the reference writes
+    # (SURVEY 8d's ms/frame ends with the frame on the host): a ring of
+    # page-locked u8 buffers, one per frame in flight; the call queues the
+    # frame, its gamma/PPM mapping and its D2H copy, which overlaps the next
+    # frames' kernels
     ring = []
-    if not ctx.dist_on and not ctx.multi and ctx.row_sample == 1:
+    if not ctx.dist_on and ctx.row_sample == 1:
         for _ in range(RING):
-            raw, buf, span = registered_int16(W * H * 3)
+            raw, buf, span = registered_buffer(W * H * 3, np.uint8)
             rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "rt_gpu_host_register")
             ring.append((raw, buf))
     step_i = [0]
@@ -211,13 +212,14 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
                 dframe.render()
                 return None
             return dist_mod.render_frame(backend, ctx.dist, torch, H, W, ctx.rank, ctx.world)
-        if ctx.multi:
-            rt580.check(lib.rt_gpu_render_multi(ctypes.byref(params), host.ctypes.data, ctx.multi, devs),
-                        "rt_gpu_render_multi")
-            return None
         buf = ring[step_i[0] % RING][1]
         step_i[0] += 1
-        rt580.check(lib.rt_gpu_render_async(ctypes.byref(params), buf.ctypes.data), "rt_gpu_render_async")
+        if ctx.multi:
+            rt580.check(lib.rt_gpu_render_multi_async(ctypes.byref(params), buf.ctypes.data, ctx.multi, devs),
+                        "rt_gpu_render_multi_async")
+        else:
+            rt580.check(lib.rt_gpu_render_async_ppm(ctypes.byref(params), buf.ctypes.data),
+                        "rt_gpu_render_async_ppm")
         return buf
 
     def finish():
@@ -290,8 +292,6 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     if ctx.rank == 0 and K == 1:
         if ctx.dist_on:
             frame_np = last.cpu().numpy() if last is not None else None
-        elif ctx.multi:
-            frame_np = host.reshape(H, W, 3)
         else:
             rt580.check(lib.rt_gpu_synchronize(), "rt_gpu_synchronize")
             frame_np = last.copy().reshape(H, W, 3)
@@ -337,11 +337,10 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
             "scene_query": "exact BVH + plane tree (rt_bvh.h)" if lib.rt_gpu_accel_active() else
                            "brute force (every primitive per ray, as the reference)",
         },
-        "step": ("one frame into host memory: rt_gpu_render_async, the int16 framebuffer copied into a page-locked "
-                 "host buffer (a ring of %d), up to three frames in flight (each frame's D2H overlaps the next "
-                 "frames' kernels)" % RING if not
-                 (ctx.dist_on or ctx.multi) else
-                 "one frame, whole Render(): framebuffer on device 0's host copy" if ctx.multi else
+        "step": ("one frame into host memory as its PPM body: %s, a ring of %d page-locked host buffers, up to "
+                 "three frames in flight (each frame's gather and D2H overlap the next frames' kernels)"
+                 % ("rt_gpu_render_multi_async (tiles mapped to bytes on their devices, gathered and de-interleaved "
+                    "on device 0)" if ctx.multi else "rt_gpu_render_async_ppm", RING) if not ctx.dist_on else
                  "one frame on every rank; rank 0 holds the gathered u8 frame"),
         "scene_upload_s": round(upload_s, 3),
         "host_enqueue_ms_per_step": round(host_s / steps * 1e3, 4),
@@ -362,7 +361,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     # per-row AO-call counts of the frame from one untimed GPU count pass: the
     # RNG bases of the oracle's frame-check rows and of the CPU baseline's range
     row_counts = None
-    if frame_np is not None and frame_np.dtype == np.int16 and not ctx.multi and not ctx.dist_on and \
+    if frame_np is not None and not ctx.multi and not ctx.dist_on and \
             ((check and ctx.args.check_pixels != 0) or cpu_baseline_on):
         row_counts = helpers.rt580_dist().GpuRows(rt580, params, torch, ctx.device).count(0, 1)[:H].cpu().numpy()
     if frame_np is not None:
@@ -376,7 +375,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     for _, buf in ring:
         rt580.check(lib.rt_gpu_host_unregister(buf.ctypes.data), "rt_gpu_host_unregister")
     if cpu_baseline_on and ctx.n_gpus == 1 and not ctx.dist_on:
-        gpu_px = frame_np.reshape(-1, 3) if frame_np is not None and frame_np.dtype == np.int16 else None
+        gpu_px = frame_np.reshape(-1, 3) if frame_np is not None else None
         out["cpu_baseline"] = cpu_baseline(ctx, name, root, params, gpu_px, row_counts)
     return out
 
@@ -406,7 +405,10 @@ def oracle_rows_check(ctx, name, root, frame_np, row_counts, n_px):
     t0 = time.perf_counter()
     px, calls, cnt, secs = helpers.oracle_render_segments(scene, W, H, depth, ao, segs, [int(base[y]) for y, _, _ in segs],
                                                           root=root)
-    bad_rows = [y for (y, x0, n), p in zip(segs, px) if not np.array_equal(p, frame_np[y, x0:x0 + n])]
+    lut = ctx.rt580.gamma_lut()
+    # the oracle's Pixel values as the frame holds them (u8: the PPM bytes)
+    as_frame = (lambda p: lut[np.asarray(p, dtype=np.int64)]) if frame_np.dtype == np.uint8 else (lambda p: p)
+    bad_rows = [y for (y, x0, n), p in zip(segs, px) if not np.array_equal(as_frame(p), frame_np[y, x0:x0 + n])]
     bad_counts = [y for (y, _, _), c in zip(segs, calls) if c != int(counts[y])]
     log("%s: frame check: %d pixels in %d segments against the oracle in %.1f s: %d rows differ, %d counts differ"
         % (name, sum(n for _, _, n in segs), len(segs), time.perf_counter() - t0, len(bad_rows), len(bad_counts)))
@@ -435,7 +437,8 @@ def frame_check(ctx, name, frame_np, single, W, H, check):
         res["reference_sha256"] = want
         res["matches_reference"] = res["sha256"] == want
     if single is not None and (ctx.multi or ctx.dist_on):
-        res["matches_single_gpu"] = bool(np.array_equal(frame_np.reshape(-1), single))
+        ref = rt580.gamma_lut()[single.astype(np.int64)] if frame_np.dtype == np.uint8 else single
+        res["matches_single_gpu"] = bool(np.array_equal(frame_np.reshape(-1), ref.reshape(-1)))
     return res
 
 
@@ -527,17 +530,18 @@ def roofline(workload, k_ms, k_launches, k_rays, iso=None):
     return res
 
 
-RING = 3  # host framebuffers of the N = 1 step (one per frame slot in flight)
+RING = 3  # host frames of the one-process step (one per frame slot in flight)
 
 
-def registered_int16(n_val):
-    """A page-aligned, page-rounded int16 host buffer of n_val values (a
+def registered_buffer(n_val, dtype):
+    """A page-aligned, page-rounded host buffer of n_val values of dtype (a
     registration must not share pages with other allocations) -> (owner, view, span)."""
     import numpy as np
-    span = (n_val * 2 + 4095) // 4096 * 4096
+    item = np.dtype(dtype).itemsize
+    span = (n_val * item + 4095) // 4096 * 4096
     raw = np.zeros(span + 4096, dtype=np.uint8)
     off = (-raw.ctypes.data) % 4096
-    return raw, raw[off:off + span].view(np.int16)[:n_val], span
+    return raw, raw[off:off + span].view(dtype)[:n_val], span
 
 
 def render_latency(lib, rt580, params, torch, n=5, warm=4):
@@ -550,7 +554,8 @@ def render_latency(lib, rt580, params, torch, n=5, warm=4):
     on each slot's second call, rt_shim.cpp render_split: the steady state of
     repeated renders)."""
     # page-aligned and page-rounded, like the class surface's own framebuffer
-    raw, host, span = registered_int16(params.width * params.height * 3)
+    import numpy as np
+    raw, host, span = registered_buffer(params.width * params.height * 3, np.int16)
     rt580.check(lib.rt_gpu_host_register(host.ctypes.data, span), "rt_gpu_host_register")
     try:
         for _ in range(warm):
@@ -615,7 +620,12 @@ def cpu_baseline(ctx, name, root, params, gpu_px, row_counts=None):
                    "oracle/rt_oracle.cpp in ref-faithful mode (the reference's arithmetic and per-call work)"
                    % (scene, W, H, depth, ao, n, y0, max(y0 - 1, 0))),
     }
-    parity = None if gpu_px is None else bool((fb1 == gpu_px[p0:p0 + n]).all())
+    import numpy as np
+    if gpu_px is not None and gpu_px.dtype == np.uint8:  # the PPM body: the oracle's pixels through the same LUT
+        fb1_frame = ctx.rt580.gamma_lut()[np.asarray(fb1, dtype=np.int64)]
+    else:
+        fb1_frame = fb1
+    parity = None if gpu_px is None else bool((fb1_frame == gpu_px[p0:p0 + n]).all())
     if threads > 1 and n > 1:
         fbn, cntn, secsn = helpers.oracle_time_prefix(scene, W, H, depth, ao, p0, n, threads=threads, root=root,
                                                       faithful=True)

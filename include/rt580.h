@@ -174,6 +174,10 @@ int rt_gpu_render_device(const rt_render_params* params, int16_t** fb_device);
  * reaches the point of this call: rt_gpu_synchronize, or a sync of that
  * stream. Replayed-count checks are reported as for rt_gpu_render_device. */
 int rt_gpu_render_async(const rt_render_params* params, int16_t* fb_host);
+/* The same with the frame delivered as the PPM body (height x width x 3 bytes,
+ * FlushFrameBufferToPPM's pixel mapping applied on the device, Raytracer.cpp:
+ * 812-818, rt_gpu_gamma_u8): half the bytes over PCIe. */
+int rt_gpu_render_async_ppm(const rt_render_params* params, uint8_t* ppm_body_host);
 /* Page-lock a host buffer that will receive frames (rt_gpu_render's fb_out):
  * a frame copied into a registered range lands there with one DMA instead of
  * through the shim's pinned staging buffer. The caller keeps the buffer alive
@@ -212,6 +216,15 @@ int rt_gpu_row_bases(const int32_t* gathered_device, int world, int n_max, int h
  * one GPU; RT580_MULTI_TRANSPORT=rccl|local forces either). n_devices == 1 is
  * rt_gpu_render. Blocking. The image is byte-identical for every G. */
 int rt_gpu_render_multi(const rt_render_params* params, int16_t* fb_out, int n_devices, const int* devices);
+/* Throughput form of rt_gpu_render_multi (rt_gpu_render_async_ppm across
+ * devices): the frame's phases are queued on every device and the call
+ * returns; the tiles are mapped to PPM bytes before the gather, and the
+ * de-interleaved PPM body is copied into ppm_body_host (a registered range of
+ * height x width x 3 bytes) on context 0's stream, in call order. Each device
+ * keeps its frame slots in flight: the gather and the copy of one frame overlap
+ * the next frame's kernels. Complete after rt_gpu_synchronize. */
+int rt_gpu_render_multi_async(const rt_render_params* params, uint8_t* ppm_body_host, int n_devices,
+                              const int* devices);
 /* Visible HIP devices (0 without a GPU). */
 int rt_gpu_device_count(void);
 /* FlushFrameBufferToPPM's pixel mapping on the device (Raytracer.cpp:812-818):

@@ -161,3 +161,71 @@ def test_mt19937_rows_past_two_to_the_32_draws():
     for y, p in zip(ys, px):
         assert np.array_equal(fb[y], p), "row %d" % y
     rt.close()
+
+
+def _registered_u8(n):
+    span = (n + 4095) // 4096 * 4096
+    raw = np.zeros(span + 4096, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    return raw, raw[off:off + span][:n], span
+
+
+@pytest.mark.parametrize("G,transport", [(1, None), (2, None), (3, None), (1, "rccl")])
+def test_render_multi_async_frames_are_the_ppm_bodies(G, transport):
+    """rt_gpu_render_multi_async (bench.py's step for every N): frames of two
+    configurations queued over a ring of three registered u8 buffers with no
+    wait in between -- after a synchronize each buffer holds the PPM body of the
+    last frame queued into it, byte-equal to the single-GPU render mapped by the
+    reference's gamma LUT; G = 1 is rt_gpu_render_async_ppm; an unregistered
+    buffer is refused."""
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    root = helpers.synthetic_root("cornell10k")
+    w, h = 53, 29
+    cfg = [(4, 16), (2, 8)]
+    lut = rt580.gamma_lut()
+    want = []
+    for d, a in cfg:
+        full, _ = render_gpu("cornell10k.json", w, h, d, a, True, root=root)
+        want.append(lut[full.astype(np.int64)].astype(np.uint8).reshape(-1))
+    rts = []
+    for d, a in cfg:
+        rt = rt580.Raytracer(w, h, root)
+        assert rt.LoadSceneJSON("cornell10k.json") == 0
+        rt.set_depth(d)
+        rt.set_ao(a, True)
+        assert rt.InitializeRenderer() == 0
+        rts.append((rt, rt.render_params()))
+    s = rts[0][0].scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    devs = (ctypes.c_int * G)(*([0] * G))
+    bufs = [_registered_u8(w * h * 3) for _ in range(3)]
+    for _, buf, span in bufs:
+        rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "host_register")
+    old = os.environ.get("RT580_MULTI_TRANSPORT")
+    if transport:
+        os.environ["RT580_MULTI_TRANSPORT"] = transport
+    try:
+        for _, buf, _ in bufs:
+            buf[:] = 7
+        last = {}
+        for i in range(10):
+            k, b = i % 2, i % 3
+            rt580.check(lib.rt_gpu_render_multi_async(ctypes.byref(rts[k][1]), bufs[b][1].ctypes.data, G, devs),
+                        "rt_gpu_render_multi_async")
+            last[b] = k
+        rt580.check(lib.rt_gpu_synchronize(), "synchronize")
+        for b, k in last.items():
+            assert np.array_equal(bufs[b][1], want[k]), "buffer %d (config %d, G %d)" % (b, k, G)
+        plain = np.zeros(w * h * 3, dtype=np.uint8)
+        assert lib.rt_gpu_render_multi_async(ctypes.byref(rts[0][1]), plain.ctypes.data, G, devs) != 0
+    finally:
+        if transport:
+            if old is None:
+                del os.environ["RT580_MULTI_TRANSPORT"]
+            else:
+                os.environ["RT580_MULTI_TRANSPORT"] = old
+        for _, buf, _ in bufs:
+            lib.rt_gpu_host_unregister(buf.ctypes.data)
+    for rt, _ in rts:
+        rt.close()

@@ -1,0 +1,8 @@
+set -o pipefail
+export DL=$PWD/580-raytracer_amd/lib580rt_diag.so
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_multi.py -k "async" tests/test_gpu_state.py -k "async or replay" > gpurun_out/t10.log 2>&1; rc=$?; [ $rc -le 1 ] || exit $rc
+tail -3 gpurun_out/t10.log
+timeout -k 10 600 python bench.py > gpurun_out/b1.json 2> gpurun_out/b1.err || exit 1
+timeout -k 10 300 python bench.py --gpus 3 --rehearse --no-cpu-baseline --no-north-star --no-config3 > gpurun_out/b1r.json 2> gpurun_out/b1r.err || exit 1
+timeout -k 10 300 env RT580_LIB=$DL RT580_AO_VERIFY=1 RT580_AO_BLOCK=15 python -u tools/ao_verify.py field100k_1080p 2 > gpurun_out/ablk.json 2> gpurun_out/ablk.err || exit 1
+tools/gpu.sh ab blk "RT580_AO_BLOCK=0" "RT580_AO_BLOCK=13" "RT580_AO_BLOCK=15" "RT580_AO_BLOCK=17" "RT580_AO_BLOCK=0" "RT580_AO_BLOCK=15" -- --workload field100k_1080p --no-cpu-baseline --no-config3 > gpurun_out/blk.txt 2>&1
