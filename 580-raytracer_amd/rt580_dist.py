@@ -130,6 +130,14 @@ class DistFrame:
                       for _ in range(2)] if rank == 0 else None
         self.frame = torch.empty(self.n_max * world, width, 3, dtype=torch.uint8 if u8 else torch.int16,
                                  device=device) if rank == 0 else None
+        # rank 0: each assembled frame is copied into page-locked host memory on
+        # the compute stream (a ring of two, the frames in flight): a step ends
+        # with the frame on the host, as the one-process paths' steps do
+        on_gpu = torch.device(device).type == "cuda"
+        self.host = [torch.empty(height, width, 3, dtype=self.frame.dtype, pin_memory=True)
+                     for _ in range(2)] if rank == 0 and on_gpu else None
+        self.host_i = 0
+        self.last_host = None
         self.work = [None, None]
         self.i = 0
         self.pending = None  # buffer index whose gather is in flight and not yet de-interleaved
@@ -142,6 +150,10 @@ class DistFrame:
             tiles = (self.tiles[k] if self.u8 else self.tiles[k].view(self.t.int16)).view(
                 self.world, self.n_max, self.w, 3)
             self.frame.view(self.n_max, self.world, self.w, 3).copy_(tiles.transpose(0, 1))
+            if self.host is not None:
+                self.last_host = self.host[self.host_i]
+                self.last_host.copy_(self.frame[:self.h], non_blocking=True)
+                self.host_i ^= 1
 
     def render(self):
         k = self.i
@@ -164,8 +176,9 @@ class DistFrame:
         self.i ^= 1
 
     def finish(self):
-        """Complete the last frame; returns the (H, W, 3) frame on rank 0 (uint8
-        PPM pixels with u8=True, else the int16 Pixel framebuffer)."""
+        """Complete the last frame; returns the (H, W, 3) frame in rank 0's
+        page-locked host memory (uint8 PPM pixels with u8=True, else the int16
+        Pixel framebuffer), its copy complete."""
         if self.pending is not None:
             self._assemble(self.pending)
             self.pending = None
@@ -173,4 +186,9 @@ class DistFrame:
             if self.work[k] is not None:
                 self.work[k].wait()
                 self.work[k] = None
-        return self.frame[:self.h] if self.rank == 0 else None
+        if self.rank != 0:
+            return None
+        if self.host is None:  # a CPU backend (gloo tests): the frame is host memory already
+            return self.frame[:self.h]
+        self.t.cuda.current_stream(self.frame.device).synchronize()
+        return self.last_host

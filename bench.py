@@ -341,7 +341,8 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
                  "three frames in flight (each frame's gather and D2H overlap the next frames' kernels)"
                  % ("rt_gpu_render_multi_async (tiles mapped to bytes on their devices, gathered and de-interleaved "
                     "on device 0)" if ctx.multi else "rt_gpu_render_async_ppm", RING) if not ctx.dist_on else
-                 "one frame on every rank; rank 0 holds the gathered u8 frame"),
+                 "one frame on every rank; rank 0 gathers the u8 tiles, de-interleaves them and copies the PPM body "
+                 "into page-locked host memory (rt580_dist.DistFrame)"),
         "scene_upload_s": round(upload_s, 3),
         "host_enqueue_ms_per_step": round(host_s / steps * 1e3, 4),
         "kernel_ms_per_frame" + ("" if not (ctx.dist_on or ctx.multi) else "_rank0"): {
