@@ -206,6 +206,8 @@ hipError_t launch_row_bases(const int32_t* gathered, int world, int n_max, int h
                             hipStream_t s);
 hipError_t upload_gamma_lut(const uint8_t* lut, hipStream_t s);
 hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
+// the same, 16 bytes per lane (out 16-byte aligned; e.g. mapped host memory)
+hipError_t launch_gamma_u8_wide(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
 // mt19937 draws [lo, hi) of the serial stream into out[0, hi - lo): one
 // workgroup per checkpoint block k in [k0, k0 + nblk) (rt_mt.h: windows[j] =
 // W_{(k0 + j) kMtBlock}), each running the twist from its window.

@@ -377,6 +377,15 @@ __device__ __forceinline__ uint32_t far_key(const BvhView& V, rv3 o, rv3 d) {
     if (grid_origin(V, o)) return grid_cell(d, V.grid_log2) << (24 - 2 * V.grid_log2);
     return RT_KEY_TREE | dir_key(d);
 }
+// false: a grid-origin ray whose direction-grid cell lists no candidate (and
+// the scene has no always-tested plane) -- it cannot have a far hit, and the
+// far pass would only find that out after sorting it (routing only: an any-hit
+// ray that skips the far queue stays a miss, as it would there)
+__device__ __forceinline__ bool far_live(const BvhView& V, rv3 o, rv3 d) {
+    if (V.n_always > 0 || !grid_origin(V, o)) return true;
+    const uint32_t cell = grid_cell(d, V.grid_log2);
+    return V.grid_start[cell + 1] != V.grid_start[cell];
+}
 __device__ __forceinline__ uint32_t dir_key(rv3 d) {
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
     float x = d.x / s, y = d.y / s;
@@ -583,7 +592,8 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             if (active) {
                 W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
                 W.hit_prim[node] = nh ? h.prim : -1;
-                q = brute || (!dir_zero(d) && !(nh && h.t < far_T(far_ray(S.bv, o), root.min_dhi)));
+                q = brute || (!dir_zero(d) && !(nh && h.t < far_T(far_ray(S.bv, o), root.min_dhi)) &&
+                              far_live(S.bv, o, d));
             }
             const uint64_t bm = __ballot(brute);
             if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
@@ -648,7 +658,7 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
                 nh = lit && !brute && bvh_any_near(S.bv, so, L2, tmax);
             }
             if (nh) flag = 1;
-            else q = lit && (brute || (!dir_zero(L2) && isinf(tmax)));
+            else q = lit && (brute || (!dir_zero(L2) && isinf(tmax) && far_live(S.bv, so, L2)));
             if (active) W.shadow[(size_t)dl * W.far_cap + (item - i0)] = flag;
             const uint64_t bm = __ballot(brute);
             if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
@@ -952,8 +962,9 @@ template <bool BVH>
 __device__ __forceinline__ void ao_finish(const DevScene& S, const DevWork& W, uint32_t N, bool active, bool ao_brute,
                                           bool hit, uint64_t c, rv3 o, rv3 d) {
     if (BVH) {
-        // rays that miss every near triangle go to the sorted far-hit pass
-        const bool q = active && !hit && S.bv.has_far;
+        // rays that miss every near triangle go to the sorted far-hit pass,
+        // unless their direction-grid cell is empty
+        const bool q = active && !hit && S.bv.has_far && (ao_brute || far_live(S.bv, o, d));
         const uint64_t qm = __ballot(q);
         const uint64_t bm = __ballot(ao_brute);
         if (bm && (threadIdx.x & 63) == 0) atomicAdd(W.far_count + 1, (uint32_t)__popcll(bm));
@@ -1159,7 +1170,7 @@ __device__ void ao_fix_item(const DevScene& S, const DevFrame& F, const DevWork&
     if (S.use_bvh) {
         const bool brute = S.bv.has_far && far_origin(S, o);
         hit = !brute && bvh_any_near(S.bv, o, d);
-        if (!hit && S.bv.has_far) {
+        if (!hit && S.bv.has_far && (brute || far_live(S.bv, o, d))) {
             if (brute) atomicAdd(W.far_count + 1, 1u);
             const uint32_t slot = atomicAdd(W.far_count, 1u);
             W.far_rays[2 * (size_t)slot] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
@@ -1512,7 +1523,7 @@ __global__ void __launch_bounds__(TB) ao_audit_expect_kernel(DevScene S, DevWork
         if (hit) {
             atomicAdd(&exp[c - c_lo], 1u);
             atomicAdd(&out[5], 1ull);
-        } else if (S.bv.has_far) {
+        } else if (S.bv.has_far && (flag == 2u || far_live(S.bv, o, d))) {
             const uint32_t key = flag == 2u ? RT_KEY_BRUTE : far_key(S.bv, o, d);
             atomicAdd(&aud[0], 1ull);
             atomicAdd(&aud[1], audit_mix(make_float4(o.x, o.y, o.z, r0.w), make_float4(d.x, d.y, d.z, INFINITY), key));
@@ -3317,6 +3328,36 @@ hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStrea
     return hipGetLastError();
 }
 
+// 16 pixel bytes per lane, one 16-byte store: the form for an `out` in mapped
+// host memory (the PPM body written over the host link by the kernel itself,
+// no separate copy; whole 16-byte stores keep the link's write combining
+// full). The LUT is staged in LDS (per-lane indices).
+__device__ __forceinline__ uint32_t gamma4(const uint32_t* lut, uint32_t lo, uint32_t hi) {
+    auto one = [&](int v) { return lut[v < 0 ? 0 : (v > 255 ? 255 : v)]; };
+    return one((int16_t)(lo & 0xffffu)) | (one((int16_t)(lo >> 16)) << 8) | (one((int16_t)(hi & 0xffffu)) << 16) |
+           (one((int16_t)(hi >> 16)) << 24);
+}
+__global__ void __launch_bounds__(TB) gamma_u8_wide_kernel(const int16_t* __restrict__ fb, uint64_t n16,
+                                                           uint8_t* __restrict__ out) {
+    __shared__ uint32_t lut[256];
+    for (int k = threadIdx.x; k < 256; k += TB) lut[k] = c_gamma_lut[k];
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(fb);
+    uint4* dst = reinterpret_cast<uint4*>(out);
+    for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * TB) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        dst[i] = make_uint4(gamma4(lut, a.x, a.y), gamma4(lut, a.z, a.w), gamma4(lut, b.x, b.y), gamma4(lut, b.z, b.w));
+    }
+}
+
+hipError_t launch_gamma_u8_wide(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s) {
+    const uint64_t n16 = n / 16;
+    if (n16) hipLaunchKernelGGL(gamma_u8_wide_kernel, dim3(grid_for(n16, 4096)), dim3(TB), 0, s, fb, n16, out);
+    if (n > n16 * 16)
+        hipLaunchKernelGGL(gamma_u8_kernel, dim3(1), dim3(TB), 0, s, fb + n16 * 16, n - n16 * 16, out + n16 * 16);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- math self-test
 // The device-only fast sequences against the plain operations they replace:
 //  [0] rt_sqrt_nr vs sqrtf over EVERY float in [2^-96, +inf] and +0
@@ -3484,12 +3525,28 @@ hipError_t launch_deinterleave(const int16_t* tiles, int world, int n_max, int w
     return hipGetLastError();
 }
 
+// 16 bytes per lane when a row is a whole number of them (1920 x 3 is): the
+// form for an `out` in mapped host memory, like gamma_u8_wide_kernel
+__global__ void deinterleave_u8_wide_kernel(const uint4* __restrict__ tiles, int world, int n_max, int row16,
+                                            int height, uint4* __restrict__ out) {
+    const size_t total = (size_t)row16 * (size_t)height;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t y = i / (size_t)row16, e = i - y * (size_t)row16;
+        const size_t r = y % (size_t)world, j = y / (size_t)world;
+        out[i] = tiles[(r * (size_t)n_max + j) * (size_t)row16 + e];
+    }
+}
+
 hipError_t launch_deinterleave_u8(const uint8_t* tiles, int world, int n_max, int width, int height, uint8_t* out,
                                   hipStream_t s) {
     const uint64_t n = (uint64_t)width * 3 * height;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(deinterleave_kernel<uint8_t>, dim3(grid_for(n, 16384)), dim3(256), 0, s, tiles, world, n_max,
-                       width, height, out);
+    if ((width * 3) % 16 == 0 && ((uintptr_t)tiles | (uintptr_t)out) % 16 == 0)
+        hipLaunchKernelGGL(deinterleave_u8_wide_kernel, dim3(grid_for(n / 16, 8192)), dim3(256), 0, s,
+                           (const uint4*)tiles, world, n_max, width * 3 / 16, height, (uint4*)out);
+    else
+        hipLaunchKernelGGL(deinterleave_kernel<uint8_t>, dim3(grid_for(n, 16384)), dim3(256), 0, s, tiles, world,
+                           n_max, width, height, out);
     return hipGetLastError();
 }
 
@@ -3585,7 +3642,13 @@ static int sort_begin_bit(const DevScene& S) {
     return b > 0 ? b : 0;
 }
 
-static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb) {
+// one_dir: every ray of the queue has the same direction (a directional
+// light's shadow rays): its keys take at most three values (the light's grid
+// cell, RT_KEY_TREE | its direction key, RT_KEY_BRUTE), which differ in bits
+// 24-25 -- one digit pass on those bits groups them as the whole sort would
+// (stable: within a class the keys are equal, so the order is the same).
+static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_t s, uint32_t& nq, uint32_t& nb,
+                                 bool one_dir = false) {
     RT_STEP("far queue count D2H");
     hipError_t e = read_counts(W.far_count, 2, W.far_count_host, s, W.far_cap, W.far_cap);
     if (e != hipSuccess) return e;
@@ -3593,10 +3656,13 @@ static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_
     if (W.far_count_host[1] > nq) return counts_fit(W.far_count_host, 2, W.far_cap, nq);
     nb = W.far_count_host[1];  // far-origin rays: keyed to sort last
     if (nq == 0) return hipSuccess;
+    if (one_dir && nb == nq)  // every key RT_KEY_BRUTE: already grouped; the brute pass reads the sorted values
+        return hipMemcpyAsync(W.far_vals_alt, W.far_vals, (size_t)nq * 4, hipMemcpyDeviceToDevice, s);
     size_t tmp = W.sort_tmp_bytes;
     RT_STEP("far queue radix sort");
     return hipcub::DeviceRadixSort::SortPairs(W.sort_tmp, tmp, W.far_keys, W.far_keys_alt, W.far_vals,
-                                              W.far_vals_alt, (int)nq, sort_begin_bit(S), RT_DIR_KEY_BITS, s);
+                                              W.far_vals_alt, (int)nq, one_dir ? 24 : sort_begin_bit(S),
+                                              RT_DIR_KEY_BITS, s);
 }
 
 // Per-frame counters, one launch: level counts/bases, the node-capacity probe,
@@ -3723,7 +3789,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                                            li, dl, near_wave() ? 1 : 0);
                         if ((e = hipGetLastError()) != hipSuccess) return e;
                         uint32_t sq = 0, sb = 0;
-                        if ((e = sort_far_queue(S, W, s, sq, sb)) != hipSuccess) return e;
+                        if ((e = sort_far_queue(S, W, s, sq, sb, /*one_dir=*/true)) != hipSuccess) return e;
                         uint8_t* flags = W.shadow + (size_t)dl * W.far_cap;
                         if (sb) {
                             RT_STEP("trace shadow brute scan");

@@ -445,6 +445,7 @@ struct HostRange {
     // next one waits for it, so frames land in call order
     hipEvent_t copied = nullptr;
     int copied_device = -1;
+    void* dev = nullptr;  // the range mapped into the devices' address space
 };
 std::vector<HostRange> g_host_ranges;
 
@@ -1291,6 +1292,24 @@ static HostRange* host_range_ready(const void* host, size_t bytes) {
     return hr;
 }
 
+// RT580_D2H_MAPPED (default 1): the PPM body is written into the registered
+// range by the kernel that produces it (the range mapped into the device's
+// address space) instead of a device buffer and a copy (0, A/B)
+static bool d2h_mapped() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("RT580_D2H_MAPPED");
+        v = e ? std::atoi(e) : 1;
+    }
+    return v != 0;
+}
+
+// host's address inside the range as the device sees it (null: not mapped)
+static void* mapped(const HostRange* hr, const void* host) {
+    if (!d2h_mapped() || !hr->dev || ((uintptr_t)host % 16) != 0) return nullptr;
+    return (char*)hr->dev + ((const char*)host - hr->p);
+}
+
 // src (device) -> host on stream s, after the previous copy into the same range
 static int ordered_d2h(HostRange* hr, void* host, const void* src, size_t bytes, hipStream_t s) {
     HIP_TRY(hipStreamWaitEvent(s, hr->copied, 0));
@@ -1338,7 +1357,11 @@ static int render_device_frame(const rt_render_params* p, int16_t** fb_device, v
         bool retry = false;
         if (check_capacity(p, retry)) return RT_FAILURE;
         if (!retry) {
-            if (hr && u8) {  // the PPM body: gamma u8 on the device, then to the host
+            if (hr && u8 && mapped(hr, host)) {  // the PPM body straight into the host range
+                HIP_TRY(hipStreamWaitEvent(fs(), hr->copied, 0));
+                HIP_TRY(launch_gamma_u8_wide((const int16_t*)SL.fb.p, host_bytes, (uint8_t*)mapped(hr, host), fs()));
+                HIP_TRY(hipEventRecord(hr->copied, fs()));
+            } else if (hr && u8) {  // the PPM body: gamma u8 on the device, then to the host
                 if (ensure(SL.fb8, host_bytes)) return RT_FAILURE;
                 HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, host_bytes, (uint8_t*)SL.fb8.p, fs()));
                 if (ordered_d2h(hr, host, SL.fb8.p, host_bytes, fs())) return RT_FAILURE;
@@ -1568,8 +1591,15 @@ int rt_gpu_host_register(void* host_ptr, uint64_t bytes) {
     if (!host_ptr || bytes == 0) return fail("rt_gpu_host_register: empty range");
     if (host_registered(host_ptr, bytes)) return RT_SUCCESS;
     if (!g.inited && rt_gpu_init(-1) != RT_SUCCESS) return RT_FAILURE;
-    HIP_TRY(hipHostRegister(host_ptr, bytes, hipHostRegisterPortable));
-    g_host_ranges.push_back({(const char*)host_ptr, (size_t)bytes});
+    HIP_TRY(hipHostRegister(host_ptr, bytes, hipHostRegisterPortable | hipHostRegisterMapped));
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, host_ptr, 0) != hipSuccess) dev = nullptr;
+    (void)hipGetLastError();
+    HostRange r;
+    r.p = (const char*)host_ptr;
+    r.bytes = (size_t)bytes;
+    r.dev = dev;
+    g_host_ranges.push_back(r);
     return RT_SUCCESS;
 }
 
@@ -2292,6 +2322,12 @@ int multi_frame_async(const rt_render_params* p, uint8_t* ppm_host, int n, const
             HIP_TRY(hipMemcpyPeerAsync((char*)g_multi.a_root8[r].p + (size_t)k * t8, g.device, g_multi.a_t8[r][k].p,
                                        g_ctx[k].device, t8, g.stream));
         }
+    }
+    if (uint8_t* dst = (uint8_t*)mapped(hr, ppm_host)) {  // de-interleaved straight into the host range
+        HIP_TRY(hipStreamWaitEvent(g.stream, hr->copied, 0));
+        HIP_TRY(launch_deinterleave_u8((const uint8_t*)g_multi.a_root8[r].p, n, n_max, W, H, dst, g.stream));
+        HIP_TRY(hipEventRecord(hr->copied, g.stream));
+        return RT_SUCCESS;
     }
     HIP_TRY(launch_deinterleave_u8((const uint8_t*)g_multi.a_root8[r].p, n, n_max, W, H,
                                    (uint8_t*)g_multi.a_frame8[r].p, g.stream));

@@ -195,9 +195,10 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     # frame, its gamma/PPM mapping and its D2H copy, which overlaps the next
     # frames' kernels
     ring = []
-    if not ctx.dist_on and ctx.row_sample == 1:
+    step_kind = ctx.args.step if not ctx.multi else "ppm"
+    if not ctx.dist_on and ctx.row_sample == 1 and step_kind != "device":
         for _ in range(RING):
-            raw, buf, span = registered_buffer(W * H * 3, np.uint8)
+            raw, buf, span = registered_buffer(W * H * 3, np.int16 if step_kind == "host16" else np.uint8)
             rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "rt_gpu_host_register")
             ring.append((raw, buf))
     step_i = [0]
@@ -212,9 +213,15 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
                 dframe.render()
                 return None
             return dist_mod.render_frame(backend, ctx.dist, torch, H, W, ctx.rank, ctx.world)
+        if step_kind == "device":
+            dev = ctypes.c_void_p()
+            rt580.check(lib.rt_gpu_render_device(ctypes.byref(params), ctypes.byref(dev)), "rt_gpu_render_device")
+            return None
         buf = ring[step_i[0] % RING][1]
         step_i[0] += 1
-        if ctx.multi:
+        if step_kind == "host16":
+            rt580.check(lib.rt_gpu_render_async(ctypes.byref(params), buf.ctypes.data), "rt_gpu_render_async")
+        elif ctx.multi:
             rt580.check(lib.rt_gpu_render_multi_async(ctypes.byref(params), buf.ctypes.data, ctx.multi, devs),
                         "rt_gpu_render_multi_async")
         else:
@@ -292,7 +299,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     if ctx.rank == 0 and K == 1:
         if ctx.dist_on:
             frame_np = last.cpu().numpy() if last is not None else None
-        else:
+        elif last is not None:
             rt580.check(lib.rt_gpu_synchronize(), "rt_gpu_synchronize")
             frame_np = last.copy().reshape(H, W, 3)
 
@@ -343,6 +350,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
                     "on device 0)" if ctx.multi else "rt_gpu_render_async_ppm", RING) if not ctx.dist_on else
                  "one frame on every rank; rank 0 gathers the u8 tiles, de-interleaves them and copies the PPM body "
                  "into page-locked host memory (rt580_dist.DistFrame)"),
+        "step_kind": step_kind,
         "scene_upload_s": round(upload_s, 3),
         "host_enqueue_ms_per_step": round(host_s / steps * 1e3, 4),
         "kernel_ms_per_frame" + ("" if not (ctx.dist_on or ctx.multi) else "_rank0"): {
@@ -684,6 +692,10 @@ def main():
                          "interleaved split; RNG bases from an untimed full-frame count), for huge frames and "
                          "the per-rank shares of a split")
     ap.add_argument("--row-rank", type=int, default=0, help="R of --row-sample")
+    ap.add_argument("--step", default="ppm", choices=["ppm", "host16", "device"],
+                    help="one process, N = 1 (A/B of the step's end; the default is the contract's): ppm = the PPM "
+                         "body in host memory (rt_gpu_render_async_ppm), host16 = the int16 framebuffer in host "
+                         "memory (rt_gpu_render_async), device = the framebuffer left in HBM (rt_gpu_render_device)")
     args = ap.parse_args()
     if args.row_sample < 1 or not 0 <= args.row_rank < args.row_sample:
         raise SystemExit("bench.py: need --row-sample K >= 1 and 0 <= --row-rank < K")
