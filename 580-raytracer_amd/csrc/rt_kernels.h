@@ -118,12 +118,6 @@ struct DevWork {
     // split AO pass (ao_trace_kernel): (o.xyz, call), (d.xyz, flag) per item of a chunk
     float4* ao_rays;       // [2 * ao_cap] or null
     uint32_t ao_cap;
-    // RT580_AO_BLOCK (A/B): each ray's 16 x 16 octahedral direction cell
-    // (written by the generation pass) and, per block of the chunk's rays, their
-    // indices in cell order (ao_block_sort_kernel): ao_trace_kernel<.., ORD>
-    // traces in that order instead of sorting 2048 samples in LDS. Null: off.
-    uint8_t* ao_key;         // [ao_cap] or null
-    uint32_t* ao_order;      // [ao_cap] or null
     // AO rays of a chunk whose near traversal ran out of its step budget in
     // ao_trace_kernel (item index in the chunk), finished by ao_late_kernel
     uint32_t* ao_late;       // [ao_cap] or null
@@ -186,8 +180,6 @@ hipError_t launch_row_counts(const DevScene& S, const DevFrame& F, const DevWork
 hipError_t launch_rank(const DevScene& S, const DevFrame& F, const DevWork& W, const uint64_t* row_base_global,
                        hipStream_t s);
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s);
-// RT580_AO_BLOCK: log2 of the blocks sorted by direction before the AO trace (0: off)
-int ao_block_log2();
 // The launcher step that ran last (for error messages).
 const char* launch_where();
 // Temporary storage of the far-queue radix sort / run-length encoding / scan for `cap` rays.

@@ -1119,7 +1119,6 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                 float4* r = W.ao_rays + 2 * (size_t)(item - item_begin);
                 r[0] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
                 r[1] = make_float4(d.x, d.y, d.z, __uint_as_float(flag));
-                if (W.ao_key) W.ao_key[item - item_begin] = (uint8_t)(flag ? grid_cell(d, 4) : 255u);
             }
             continue;
         }
@@ -1255,9 +1254,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
 // BUDGET > 0: a lane gives up after BUDGET leaf visits; its item goes to
 // W.ao_late (ao_late_kernel re-runs the full query), so a wave is not held by
 // its few long traversals (tools/simd_sim.cpp "budget").
-// ORD: rays in the order of W.ao_order (ao_block_sort_kernel: larger blocks
-// sorted by direction cell before the launch) instead of the LDS sort.
-template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0, bool ORD = false>
+template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
@@ -1325,7 +1322,6 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
             }
             i = blk + s_order[round * TB + threadIdx.x];
         }
-        if (ORD && i < n) i = W.ao_order[i];
         float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
         if (i < n) {
             r0 = W.ao_rays[2 * i];
@@ -1369,7 +1365,7 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
             hit = flag == 1u && bvh4_any_near(S.bv, o, d);
         }
         // sorted: a wave's lanes are no longer one call's samples
-        ao_finish<true>(S, W, (SORT > 0 || ORD) ? 1u : N, active && !late, ao_brute, hit,
+        ao_finish<true>(S, W, SORT > 0 ? 1u : N, active && !late, ao_brute, hit,
                         (uint64_t)__float_as_uint(r0.w), o, d);
     }
 }
@@ -1672,50 +1668,6 @@ static int late_wpe() {
     if (v < 0) {
         const char* e = getenv("RT580_LATE_WPE");
         v = e ? atoi(e) : 6;
-    }
-    return v;
-}
-
-// The rays of each block of 2^lg consecutive items of the chunk (2^lg / N
-// AO calls of neighbouring pixels) in the order of their direction cells
-// (W.ao_key): a counting sort per block, indices (chunk-relative) into
-// W.ao_order. Cells keep no order inside (atomics): the trace's any-hit
-// answers and per-call counts do not depend on it.
-__global__ void __launch_bounds__(1024) ao_block_sort_kernel(DevWork W, uint64_t n, int lg) {
-    __shared__ uint32_t bin[257];
-    const uint64_t b0 = (uint64_t)blockIdx.x << lg;
-    if (b0 >= n) return;
-    const uint64_t b1 = b0 + (1ull << lg) < n ? b0 + (1ull << lg) : n;
-    for (int k = threadIdx.x; k < 257; k += blockDim.x) bin[k] = 0;
-    __syncthreads();
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) atomicAdd(&bin[W.ao_key[i]], 1u);
-    __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of 256 bins by one wave, 4 per lane
-        const int l = threadIdx.x;
-        uint32_t v[4], s = 0;
-        for (int q = 0; q < 4; q++) { v[q] = bin[4 * l + q]; s += v[q]; }
-        uint32_t inc = s;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
-            if (l >= o) inc += t;
-        }
-        uint32_t acc = inc - s;
-        for (int q = 0; q < 4; q++) { bin[4 * l + q] = acc; acc += v[q]; }
-    }
-    __syncthreads();
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
-        const uint32_t pos = atomicAdd(&bin[W.ao_key[i]], 1u);
-        W.ao_order[b0 + pos] = (uint32_t)i;
-    }
-}
-
-// RT580_AO_BLOCK=lg (A/B): blocks of 2^lg AO samples sorted by direction cell
-// before the trace (ao_block_sort_kernel); 0: the trace's own sort of 2048.
-int ao_block_log2() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_BLOCK");
-        v = e ? atoi(e) : 0;
     }
     return v;
 }
@@ -3934,13 +3886,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
                     if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
                     const int bu = ao_budget();
-                    if (W.ao_order && bu == 4) {
-                        const int lg = ao_block_log2();
-                        hipLaunchKernelGGL(ao_block_sort_kernel, dim3((unsigned)(((e1 - b) + (1ull << lg) - 1) >> lg)),
-                                           dim3(1024), 0, s, W, e1 - b, lg);
-                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 0, 4, 4, true>), dim3(grid_for(e1 - b, 16384)),
-                                           dim3(TB), 0, s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    } else if (bu <= 2)
+                    if (bu <= 2)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 2>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     else if (bu == 3)

@@ -81,7 +81,6 @@ const Knob kKnobs[] = {
     {"RT580_AO_BUDGET", INT_RANGE, 0, 64, nullptr, nullptr},
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
     {"RT580_AO_RESUME", INT_SET, 0, 0, k01, nullptr},
-    {"RT580_AO_BLOCK", INT_RANGE, 0, 20, nullptr, nullptr},
     {"RT580_D2H_MAPPED", INT_SET, 0, 0, k01, nullptr},
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
     {"RT580_NEAR_WPE", INT_SET, 0, 0, kNearWpe, nullptr},

@@ -49,7 +49,6 @@ struct Slot {
     // provisional hits -- per slot, so that consecutive BVH frames overlap
     // like the others (count schedule replay, see trace_rows)
     DevBuf ao_state;  // saved walks of late AO rays (DevWork::ao_state)
-    DevBuf ao_key, ao_order;  // RT580_AO_BLOCK (DevWork::ao_key / ao_order)
     DevBuf ao_rays, ao_late, ao_late_count, far_rays, far_keys, far_keys_alt, far_vals, far_vals_alt, far_count,
         far_seg_off, far_seg_n, far_wofs, far_work, sort_tmp, hit4, hit_prim, shadow;
     uint32_t far_cap = 0, ao_cap = 0;
@@ -624,8 +623,6 @@ DevWork dev_work() {
     w.ao_rays = w.ao_cap ? (float4*)SL.ao_rays.p : nullptr;
     w.ao_late = w.ao_cap ? (uint32_t*)SL.ao_late.p : nullptr;
     w.ao_late_count = w.ao_cap ? (uint32_t*)SL.ao_late_count.p : nullptr;
-    w.ao_key = w.ao_cap && ao_block_log2() > 0 ? (uint8_t*)SL.ao_key.p : nullptr;
-    w.ao_order = w.ao_key ? (uint32_t*)SL.ao_order.p : nullptr;
     w.ao_state_cap = w.ao_cap && ao_resume() ? w.ao_cap / 16 : 0u;
     w.ao_state = w.ao_state_cap ? (uint32_t*)SL.ao_state.p : nullptr;
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
@@ -674,8 +671,7 @@ void set_chunk_log2(int log2) {
     g.chunk_log2 = log2;
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.far_rays, &sl.far_keys, &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.sort_tmp,
-                          &sl.ao_rays, &sl.far_seg_off, &sl.far_wofs, &sl.far_work, &sl.ao_late, &sl.shadow, &sl.ao_state,
-                          &sl.ao_key, &sl.ao_order})
+                          &sl.ao_rays, &sl.far_seg_off, &sl.far_wofs, &sl.far_work, &sl.ao_late, &sl.shadow, &sl.ao_state})
             release(*b);
         sl.far_cap = sl.ao_cap = 0;
     }
@@ -714,8 +710,7 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     g.frame_ac = g.bvh_ok ? ac : 0;
     g.frame_fc = 0;
     if (g.bvh_ok && SL.ao_cap < ac) {  // ray records of the split AO pass (ao_trace_kernel)
-        if ((ao_block_log2() > 0 && (ensure(SL.ao_key, (size_t)ac) || ensure(SL.ao_order, (size_t)ac * 4))) ||
-            ensure(SL.ao_rays, (size_t)ac * 32) || ensure(SL.ao_late, (size_t)ac * 4) || ensure(SL.ao_late_count, 64) ||
+        if (ensure(SL.ao_rays, (size_t)ac * 32) || ensure(SL.ao_late, (size_t)ac * 4) || ensure(SL.ao_late_count, 64) ||
             (ao_resume() && ensure(SL.ao_state, 2 * (size_t)(ac / 16) * kLateWords * 4)))
             return RT_FAILURE;
         SL.ao_cap = ac;
@@ -1872,7 +1867,7 @@ void shutdown_ctx() {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
                           &sl.row_calls, &sl.row_hits, &sl.row_nodes, &sl.row_base_local, &sl.totals, &sl.call_node,
                           &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.fb8, &sl.mt_stream, &sl.mt_windows, &sl.aofix_items, &sl.aofix_count,
-                          &sl.call_hint, &sl.ao_rays, &sl.ao_state, &sl.ao_key, &sl.ao_order, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
+                          &sl.call_hint, &sl.ao_rays, &sl.ao_state, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
                           &sl.far_keys_alt, &sl.far_vals, &sl.far_vals_alt, &sl.far_count, &sl.far_seg_off,
                           &sl.far_seg_n, &sl.far_wofs, &sl.far_work, &sl.sort_tmp, &sl.hit4, &sl.hit_prim, &sl.shadow,
                           &sl.bad})

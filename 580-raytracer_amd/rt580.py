@@ -123,18 +123,18 @@ def copy_to_host(device_ptr, nbytes, dtype):
 
 
 def _preload_torch_hip_runtime():
-    """PyTorch-ROCm wheels bundle their own libamdhip64.so. A process must hold
-    ONE HIP runtime (device pointers, streams and events are runtime objects),
-    so when torch is installed its copy is loaded first, by path: lib580rt.so's
-    libamdhip64.so.7 then binds to it (same SONAME) and a later `import torch`
-    reuses the same file. Without torch, /opt/rocm's runtime is used."""
+    """PyTorch-ROCm wheels bundle their own libamdhip64.so and librccl.so. A
+    process must hold ONE HIP runtime (device pointers, streams and events are
+    runtime objects) and one RCCL: lib580rt.so loaded first would bind
+    /opt/rocm's copies, and a later `import torch` would add its own (two
+    RCCLs tear each other's state down at exit: "double free or corruption";
+    preloading torch's two libraries by path before torch does not avoid it
+    either). So when torch is installed it is imported first: lib580rt.so's
+    libamdhip64.so.7 and its dlopen("librccl.so.1") then bind to torch's
+    copies (same SONAMEs). Without torch, /opt/rocm's are used."""
     import importlib.util
-    spec = importlib.util.find_spec("torch")
-    if spec is None or not spec.submodule_search_locations:
-        return
-    hip = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
-    if os.path.exists(hip):
-        ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
 
 
 def load(path=None):

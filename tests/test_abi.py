@@ -109,3 +109,36 @@ def test_render_without_gpu_fails_cleanly():
     assert rt.LoadSceneJSON("simpleSphereScene.json") == 0
     assert rt.Render("") == 1  # RT_FAILURE, no abort
     rt.close()
+
+
+_ONE_RUNTIME_CHILD = r"""
+import ctypes, os, sys
+sys.path.insert(0, sys.argv[1])
+import helpers
+helpers.rt580().load()
+ctypes.CDLL("librccl.so.1", mode=ctypes.RTLD_GLOBAL)  # what rt_shim.cpp rccl_load() opens
+import torch
+maps = open("/proc/self/maps").read().splitlines()
+libs = sorted({l.split()[-1] for l in maps if "librccl" in l or "libamdhip64" in l})
+print("LIBS", libs)
+"""
+
+
+def test_one_hip_runtime_and_one_rccl_per_process(tmp_path):
+    """The binding loads lib580rt.so after torch (when installed), so the
+    library's libamdhip64.so.7 and its dlopen("librccl.so.1") bind to torch's
+    bundled copies and a later `import torch` adds none: two RCCL copies in one
+    process (the library's first, torch's after it) ended the GPU suite with
+    "double free or corruption" at exit. Runs without a GPU."""
+    import subprocess
+    import sys
+    script = tmp_path / "child.py"
+    script.write_text(_ONE_RUNTIME_CHILD)
+    r = subprocess.run([sys.executable, str(script), os.path.dirname(os.path.abspath(__file__))],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("LIBS")]
+    assert line, r.stdout
+    import ast
+    libs = ast.literal_eval(line[0][5:])
+    assert sum("librccl" in l for l in libs) <= 1 and sum("libamdhip64" in l for l in libs) == 1, libs
