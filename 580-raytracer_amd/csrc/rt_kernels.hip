@@ -1370,6 +1370,170 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     }
 }
 
+// Persistent-lane form of ao_trace_kernel<WPE, LDS_D, SORT, KL, BUDGET>
+// (RT580_AO_REFILL=1): the block's SORT * TB samples are ordered by direction
+// cell as there; each wave then owns SORT * 64 consecutive sorted samples and
+// gives a lane the next one as soon as its ray is decided (hit, miss, or out
+// of budget: queued for ao_late_kernel), instead of running rounds of 64 rays
+// in lock step, where a round lasts as long as its longest ray
+// (tools/simd_sim.cpp "persistent refill" on the 100k field: node-step
+// efficiency 0.16 -> 0.30, leaf tests 0.10 -> 0.49). One step per loop
+// iteration = a descent to a leaf and its tests (bvh4_descend /
+// bvh4_leaf_hit / bvh4_pop, the visits of bvh4_any_near_budget_state); the
+// answers, queues and counts are the same as the round form's.
+template <int WPE, int LDS_D, int SORT, int KL, int BUDGET>
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
+ao_trace_refill_kernel(DevScene S, DevWork W, uint64_t n) {
+    static_assert(LDS_D > 0 && SORT > 0 && BUDGET > 0, "refill form: LDS stack, block sort, step budget");
+    __shared__ uint32_t lstk[LDS_D][TB];
+    constexpr int SN = SORT * TB;
+    constexpr int NB = 1 << (2 * KL);  // direction cells
+    __shared__ uint32_t s_order[SN];
+    __shared__ uint32_t s_bin[NB + 1];
+    __shared__ uint32_t s_wsum[TB / 64];
+    const BvhView& V = S.bv;
+    const int wave = threadIdx.x >> 6;
+    const uint64_t lt_mask = lanemask_lt();
+    uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
+    const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
+    for (uint64_t blk = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * SN; blk < n; blk += (uint64_t)gridDim.x * SN) {
+        // counting sort of the block's samples by direction cell (as ao_trace_kernel)
+        __syncthreads();
+        for (int k = threadIdx.x; k < NB + 1; k += TB) s_bin[k] = 0;
+        __syncthreads();
+        uint32_t key[SORT];
+#pragma unroll
+        for (int q = 0; q < SORT; q++) {
+            const uint64_t j = blk + (uint64_t)q * TB + threadIdx.x;
+            key[q] = NB;  // past the end: last
+            if (j < n) {
+                const float4 r1 = W.ao_rays[2 * j + 1];
+                key[q] = grid_cell(v3(r1.x, r1.y, r1.z), KL);
+            }
+            atomicAdd(&s_bin[key[q]], 1u);
+        }
+        __syncthreads();
+        {
+            constexpr int PER = (NB + 1 + TB - 1) / TB;
+            const int k0 = threadIdx.x * PER;
+            uint32_t run = 0;
+#pragma unroll
+            for (int q = 0; q < PER; q++)
+                if (k0 + q < NB + 1) run += s_bin[k0 + q];
+            const int ln = threadIdx.x & 63;
+            uint32_t inc = run;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
+                if (ln >= o) inc += v;
+            }
+            if (ln == 63) s_wsum[wave] = inc;
+            __syncthreads();
+            uint32_t acc = inc - run;
+            for (int w2 = 0; w2 < wave; w2++) acc += s_wsum[w2];
+#pragma unroll
+            for (int q = 0; q < PER; q++)
+                if (k0 + q < NB + 1) {
+                    const uint32_t cnt = s_bin[k0 + q];
+                    s_bin[k0 + q] = acc;
+                    acc += cnt;
+                }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < SORT; q++) {
+            const uint32_t pos = atomicAdd(&s_bin[key[q]], 1u);
+            s_order[pos] = (uint32_t)(q * TB + threadIdx.x);
+        }
+        __syncthreads();
+        // this wave's pool of sorted positions
+        const uint32_t p_end = (uint32_t)((wave + 1) * SORT * 64);
+        uint32_t p_next = (uint32_t)(wave * SORT * 64);  // wave-uniform
+        bool busy = false;  // the lane holds an undecided near query
+        uint64_t i = 0;
+        uint32_t call = 0;
+        rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+        SlabRay sr;
+        int sp = 0, visits = 0;
+        int32_t c = 0, nn = 0;
+        for (;;) {
+            bool fin = false, hit = false, brute = false, late = false;
+            // idle lanes take the next samples of the pool
+            const uint64_t want = __ballot(!busy);
+            if (want && p_next < p_end) {
+                const uint32_t pos = p_next + (uint32_t)__popcll(want & lt_mask);
+                p_next += (uint32_t)__popcll(want);
+                if (!busy && pos < p_end) {
+                    i = blk + s_order[pos];
+                    if (i < n) {
+                        const float4 r0 = W.ao_rays[2 * i], r1 = W.ao_rays[2 * i + 1];
+                        const uint32_t flag = __float_as_uint(r1.w);
+                        o = v3(r0.x, r0.y, r0.z);
+                        d = v3(r1.x, r1.y, r1.z);
+                        call = __float_as_uint(r0.w);
+                        if (flag == 2u) {
+                            fin = brute = true;
+                        } else if (flag == 1u) {
+                            // bvh4_any_near_budget_state's start: the brute list, then the tree
+                            for (int k = 0; k < V.n_brute && !hit; k++)
+                                hit = prim_hit_within(V.all[V.brute[k]], o, d, INFINITY);
+                            if (hit || !V.has_tree || dir_zero(d)) {
+                                fin = true;
+                            } else {
+                                sr = slab_ray(V, o, d);
+                                sp = 0;
+                                c = 0;
+                                nn = 0;  // root (internal)
+                                visits = 0;
+                                busy = true;
+                            }
+                        }
+                    }
+                }
+            }
+            // one leaf visit of every undecided ray
+            if (busy) {
+                if (visits == BUDGET) {
+                    late = true;
+                    busy = false;
+                } else {
+                    visits++;
+                    if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, nn)) {
+                        fin = true;
+                    } else if (bvh4_leaf_hit(V, o, d, INFINITY, c, nn)) {
+                        fin = hit = true;
+                    } else if (!bvh4_pop(stk, sp, c, nn)) {
+                        fin = true;
+                    }
+                    if (fin) busy = false;
+                }
+            }
+            // rays out of budget: queued for ao_late_kernel with their walk
+            const uint64_t lm = __ballot(late);
+            if (lm) {
+                const int leader = __ffsll((unsigned long long)lm) - 1;
+                uint32_t base = 0;
+                if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count, (uint32_t)__popcll(lm));
+                base = __shfl(base, leader);
+                if (late) {
+                    const uint32_t slot = base + (uint32_t)__popcll(lm & lt_mask);
+                    W.ao_late[slot] = (uint32_t)i;
+                    if (slot < W.ao_state_cap) {
+                        uint32_t* rec = W.ao_state + (size_t)slot * kLateWords;
+                        rec[0] = (uint32_t)c;
+                        rec[1] = sp <= kLateSaved ? ((uint32_t)nn | ((uint32_t)sp << 8)) : 0xffffffffu;
+                        if (sp <= kLateSaved)
+                            for (int t = 0; t < sp; t++) rec[2 + t] = stk.get(t);
+                    }
+                }
+            }
+            // decided rays: occlusion counts and the far queue
+            if (__ballot(fin)) ao_finish<true>(S, W, 1u, fin && !brute, fin && brute, hit, (uint64_t)call, o, d);
+            if (__ballot(busy) == 0 && p_next >= p_end) break;
+        }
+    }
+}
+
 // The chunk's AO rays that ran out of ao_trace_kernel's step budget: the full
 // near query, then the same bookkeeping (hits counted per call, misses queued
 // for the far pass). Grid-stride over the device-side count.
@@ -1724,6 +1888,16 @@ static int ao_sort() {
 // RT580_AO_BUDGET: leaf visits per AO ray in ao_trace_kernel before the ray is
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
+// RT580_AO_REFILL: the AO trace's persistent-lane form (ao_trace_refill_kernel)
+static int ao_refill() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_REFILL");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
 static int ao_budget() {
     static int v = -1;
     if (v < 0) {
@@ -3302,9 +3476,22 @@ __global__ void __launch_bounds__(TB) gamma_u8_wide_kernel(const int16_t* __rest
     }
 }
 
+// RT580_D2H_BLOCKS: workgroups of the kernels that write mapped host memory.
+// Their waves wait on the host link (~55 GB/s), so a few suffice to keep it
+// busy; a full grid would hold most of the chip's wave slots for the whole
+// transfer, away from the other frames' kernels.
+int d2h_blocks() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_D2H_BLOCKS");
+        v = e ? atoi(e) : 64;
+    }
+    return v;
+}
+
 hipError_t launch_gamma_u8_wide(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s) {
     const uint64_t n16 = n / 16;
-    if (n16) hipLaunchKernelGGL(gamma_u8_wide_kernel, dim3(grid_for(n16, 4096)), dim3(TB), 0, s, fb, n16, out);
+    if (n16) hipLaunchKernelGGL(gamma_u8_wide_kernel, dim3(grid_for(n16, d2h_blocks())), dim3(TB), 0, s, fb, n16, out);
     if (n > n16 * 16)
         hipLaunchKernelGGL(gamma_u8_kernel, dim3(1), dim3(TB), 0, s, fb + n16 * 16, n - n16 * 16, out + n16 * 16);
     return hipGetLastError();
@@ -3494,7 +3681,7 @@ hipError_t launch_deinterleave_u8(const uint8_t* tiles, int world, int n_max, in
     const uint64_t n = (uint64_t)width * 3 * height;
     if (n == 0) return hipSuccess;
     if ((width * 3) % 16 == 0 && ((uintptr_t)tiles | (uintptr_t)out) % 16 == 0)
-        hipLaunchKernelGGL(deinterleave_u8_wide_kernel, dim3(grid_for(n / 16, 8192)), dim3(256), 0, s,
+        hipLaunchKernelGGL(deinterleave_u8_wide_kernel, dim3(grid_for(n / 16, d2h_blocks())), dim3(256), 0, s,
                            (const uint4*)tiles, world, n_max, width * 3 / 16, height, (uint4*)out);
     else
         hipLaunchKernelGGL(deinterleave_kernel<uint8_t>, dim3(grid_for(n, 16384)), dim3(256), 0, s, tiles, world,
@@ -3895,6 +4082,9 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     else if (bu == 5 || bu == 6)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 6>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
+                    else if (bu <= 4 && ao_refill())
+                        hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)),
+                                           dim3(TB), 0, s, S, W, e1 - b);
                     else if (bu <= 4)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
