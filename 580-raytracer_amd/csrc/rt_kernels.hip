@@ -1528,7 +1528,8 @@ ao_trace_refill_kernel(DevScene S, DevWork W, uint64_t n) {
                 }
             }
             // decided rays: occlusion counts and the far queue
-            if (__ballot(fin)) ao_finish<true>(S, W, 1u, fin && !brute, fin && brute, hit, (uint64_t)call, o, d);
+            // (a far-origin ray is active with ao_brute: queued for the brute scan, as in the round form)
+            if (__ballot(fin)) ao_finish<true>(S, W, 1u, fin, fin && brute, hit, (uint64_t)call, o, d);
             if (__ballot(busy) == 0 && p_next >= p_end) break;
         }
     }
@@ -1626,6 +1627,85 @@ ao_late_kernel(DevScene S, DevWork W) {
                             v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z));
         else
             ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w), o, d);
+    }
+}
+
+// Persistent-lane form of ao_late_kernel<WPE, LDS_D> (RT580_AO_REFILL=1, no
+// second budget): each wave owns a contiguous range of the late queue and
+// gives a lane the next ray as soon as its walk is decided -- the late rays
+// are the long, uneven walks, where a lock-step round of 64 lasts as long as
+// its longest. A ray resumes the walk ao_trace_*_kernel saved for it, else
+// starts over (brute list, then the tree), as in ao_late_kernel.
+template <int WPE, int LDS_D>
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
+ao_late_refill_kernel(DevScene S, DevWork W) {
+    __shared__ uint32_t lstk[LDS_D][TB];
+    const BvhView& V = S.bv;
+    const uint32_t cnt = W.ao_late_count[0];
+    const uint32_t nwaves = gridDim.x * (TB / 64);
+    const uint32_t wid = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+    const uint32_t per = (cnt + nwaves - 1) / nwaves;
+    uint32_t p_next = wid * per;  // wave-uniform
+    const uint32_t p_end = p_next + per < cnt ? p_next + per : cnt;
+    if (p_next >= p_end) return;  // whole waves only (no barrier in this kernel)
+    const uint64_t lt_mask = lanemask_lt();
+    uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
+    const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
+    bool busy = false;
+    uint32_t call = 0;
+    rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+    SlabRay sr;
+    int sp = 0;
+    int32_t c = 0, nn = 0;
+    for (;;) {
+        bool fin = false, hit = false;
+        const uint64_t want = __ballot(!busy);
+        if (want && p_next < p_end) {
+            const uint32_t k = p_next + (uint32_t)__popcll(want & lt_mask);
+            p_next += (uint32_t)__popcll(want);
+            if (!busy && k < p_end) {
+                const uint32_t i = W.ao_late[k];
+                const float4 r0 = W.ao_rays[2 * (size_t)i], r1 = W.ao_rays[2 * (size_t)i + 1];
+                o = v3(r0.x, r0.y, r0.z);
+                d = v3(r1.x, r1.y, r1.z);
+                call = __float_as_uint(r0.w);
+                sp = 0;
+                c = 0;
+                nn = 0;  // root (internal)
+                bool saved = false;
+                if (k < W.ao_state_cap) {
+                    const uint32_t* rec = W.ao_state + (size_t)k * kLateWords;
+                    const uint32_t h1 = rec[1];
+                    if (h1 != 0xffffffffu) {
+                        saved = true;
+                        sp = (int)(h1 >> 8);
+                        nn = (int32_t)(h1 & 255u);
+                        c = (int32_t)rec[0];
+                        for (int t = 0; t < sp; t++) stk.put(t, rec[2 + t]);
+                    }
+                }
+                if (!saved)  // start over: bvh4_any_near_s's brute list first
+                    for (int j = 0; j < V.n_brute && !hit; j++) hit = prim_hit_within(V.all[V.brute[j]], o, d, INFINITY);
+                if (hit) {
+                    fin = true;
+                } else {
+                    sr = slab_ray(V, o, d);
+                    busy = true;
+                }
+            }
+        }
+        if (busy) {
+            if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, nn)) {
+                fin = true;
+            } else if (bvh4_leaf_hit(V, o, d, INFINITY, c, nn)) {
+                fin = hit = true;
+            } else if (!bvh4_pop(stk, sp, c, nn)) {
+                fin = true;
+            }
+            if (fin) busy = false;
+        }
+        if (__ballot(fin)) ao_finish<true>(S, W, 1u, fin, false, hit, (uint64_t)call, o, d);
+        if (__ballot(busy) == 0 && p_next >= p_end) break;
     }
 }
 
@@ -3336,6 +3416,46 @@ static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStre
     return e;
 }
 
+// RT580_SMALL_SORT (default 1): queues of <= 4096 rays sorted by one workgroup
+static bool small_sort_on() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_SMALL_SORT");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
+// Queues of at most kSmallSort rays: one workgroup sorts them in LDS (one
+// launch) instead of the device-wide radix sort's chain of ~5-20 launches
+// (per pass a histogram, a scan, a scatter, and their fills), which at a
+// K-way row share's queue sizes is latency, not work. Stable on the same bits,
+// so the same order. Padding keys sort after every real key (all ones).
+constexpr int kSmallSortThreads = 512, kSmallSortItems = 8;
+constexpr uint32_t kSmallSort = kSmallSortThreads * kSmallSortItems;
+__global__ void __launch_bounds__(kSmallSortThreads)
+small_sort_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, uint32_t n, int begin_bit,
+                  int end_bit, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out) {
+    using Sort = hipcub::BlockRadixSort<uint32_t, kSmallSortThreads, kSmallSortItems, uint32_t>;
+    __shared__ typename Sort::TempStorage tmp;
+    uint32_t k[kSmallSortItems], v[kSmallSortItems];
+#pragma unroll
+    for (int q = 0; q < kSmallSortItems; q++) {
+        const uint32_t i = threadIdx.x * kSmallSortItems + q;  // blocked arrangement: input order kept per thread
+        k[q] = i < n ? keys[i] : 0xffffffffu;
+        v[q] = i < n ? vals[i] : 0u;
+    }
+    Sort(tmp).Sort(k, v, begin_bit, end_bit);
+#pragma unroll
+    for (int q = 0; q < kSmallSortItems; q++) {
+        const uint32_t i = threadIdx.x * kSmallSortItems + q;
+        if (i < n) {
+            keys_out[i] = k[q];
+            vals_out[i] = v[q];
+        }
+    }
+}
+
 // Work items of the cell pass: segment k (W.far_vals[k] rays) is cut into
 // ceil(count / 64) chunks; chunk counts first (into far_keys_alt, free after
 // the run-length encoding), then, after their scan into far_wofs, one entry
@@ -3387,6 +3507,65 @@ __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, ui
     }
 }
 
+// launch_far_cells' segments and work items of a queue of n <= kSmallSort
+// sorted rays in one workgroup (one launch instead of the run-length encoding,
+// the segment-count read, two scans and two kernels): a segment starts where
+// the key changes; its chunks of <= 64 rays become work items (sorted rays
+// [r0, r1), the cell list's first entry and length, or ~0 for a plane-tree
+// key), in segment order; far_seg_n = (segments, work items).
+__global__ void __launch_bounds__(kSmallSortThreads) small_cells_kernel(DevScene S, DevWork W, uint32_t n) {
+    using Scan = hipcub::BlockScan<uint32_t, kSmallSortThreads>;
+    __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ uint32_t seg_start[kSmallSort + 1];
+    __shared__ uint32_t s_nseg;
+    const int shift = 24 - 2 * S.bv.grid_log2;
+    uint32_t key[kSmallSortItems], f[kSmallSortItems], idx[kSmallSortItems];
+#pragma unroll
+    for (int q = 0; q < kSmallSortItems; q++) {
+        const uint32_t i = threadIdx.x * kSmallSortItems + q;
+        key[q] = i < n ? W.far_keys_alt[i] : 0u;
+        f[q] = i < n && (i == 0 || W.far_keys_alt[i - 1] != key[q]) ? 1u : 0u;
+    }
+    uint32_t nseg = 0;
+    Scan(scan_tmp).ExclusiveSum(f, idx, nseg);
+#pragma unroll
+    for (int q = 0; q < kSmallSortItems; q++)
+        if (f[q]) seg_start[idx[q]] = threadIdx.x * kSmallSortItems + q;
+    if (threadIdx.x == 0) {
+        seg_start[nseg] = n;
+        s_nseg = nseg;
+    }
+    __syncthreads();
+    uint32_t cnt[kSmallSortItems], wofs[kSmallSortItems];
+#pragma unroll
+    for (int q = 0; q < kSmallSortItems; q++) {
+        const uint32_t i = threadIdx.x * kSmallSortItems + q;
+        cnt[q] = f[q] ? (seg_start[idx[q] + 1] - i + 63u) / 64u : 0u;
+    }
+    uint32_t nwork = 0;
+    __syncthreads();  // scan_tmp reused
+    Scan(scan_tmp).ExclusiveSum(cnt, wofs, nwork);
+#pragma unroll
+    for (int q = 0; q < kSmallSortItems; q++) {
+        if (!f[q]) continue;
+        const uint32_t s0 = threadIdx.x * kSmallSortItems + q, s1 = seg_start[idx[q] + 1];
+        uint32_t lb = 0, lw = 0xffffffffu;
+        if (key[q] < RT_KEY_TREE) {
+            const uint32_t cell = key[q] >> shift;
+            lb = S.bv.grid_start[cell];
+            lw = S.bv.grid_start[cell + 1] - lb;
+        }
+        for (uint32_t j = 0; j < cnt[q]; j++) {
+            const uint32_t r0 = s0 + 64u * j;
+            W.far_work[wofs[q] + j] = make_uint4(r0, s1 - r0 < 64u ? s1 : r0 + 64u, lb, lw);
+        }
+    }
+    if (threadIdx.x == 0) {
+        W.far_seg_n[0] = s_nseg;
+        W.far_seg_n[1] = nwork;
+    }
+}
+
 // The any-hit far pass over the sorted queue [0, n) (far-origin rays
 // excluded): segments of one key (run-length encoding of the sorted keys into
 // far_keys / far_vals -- the sort's inputs, free now -- and the exclusive scan
@@ -3394,6 +3573,17 @@ __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, ui
 // far_cell_any_kernel. One host read (the segment count).
 static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s,
                                    bool closest = false) {
+    if (n <= kSmallSort && small_sort_on()) {  // segments and work items in one workgroup
+        RT_STEP("far queue small segments");
+        hipLaunchKernelGGL(small_cells_kernel, dim3(1), dim3(kSmallSortThreads), 0, s, S, W, n);
+        RT_STEP("far cell pass");
+        const dim3 cg(grid_for((uint64_t)n * 64, 16384));  // work items <= rays
+        if (closest)
+            hipLaunchKernelGGL(far_cell_closest_kernel, cg, dim3(TB), 0, s, S, W);
+        else
+            hipLaunchKernelGGL(far_cell_any_kernel, cg, dim3(TB), 0, s, S, W, n, flag);
+        return hipGetLastError();
+    }
     size_t tmp = W.sort_tmp_bytes;
     RT_STEP("far queue segments");
     hipError_t e = hipcub::DeviceRunLengthEncode::Encode(W.sort_tmp, tmp, W.far_keys_alt, W.far_keys, W.far_vals,
@@ -3797,11 +3987,17 @@ static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_
     if (nq == 0) return hipSuccess;
     if (one_dir && nb == nq)  // every key RT_KEY_BRUTE: already grouped; the brute pass reads the sorted values
         return hipMemcpyAsync(W.far_vals_alt, W.far_vals, (size_t)nq * 4, hipMemcpyDeviceToDevice, s);
+    const int b0 = one_dir ? 24 : sort_begin_bit(S);
+    if (nq <= kSmallSort && small_sort_on()) {
+        RT_STEP("far queue small sort");
+        hipLaunchKernelGGL(small_sort_kernel, dim3(1), dim3(kSmallSortThreads), 0, s, W.far_keys, W.far_vals, nq, b0,
+                           RT_DIR_KEY_BITS, W.far_keys_alt, W.far_vals_alt);
+        return hipGetLastError();
+    }
     size_t tmp = W.sort_tmp_bytes;
     RT_STEP("far queue radix sort");
     return hipcub::DeviceRadixSort::SortPairs(W.sort_tmp, tmp, W.far_keys, W.far_keys_alt, W.far_vals,
-                                              W.far_vals_alt, (int)nq, one_dir ? 24 : sort_begin_bit(S),
-                                              RT_DIR_KEY_BITS, s);
+                                              W.far_vals_alt, (int)nq, b0, RT_DIR_KEY_BITS, s);
 }
 
 // Per-frame counters, one launch: level counts/bases, the node-capacity probe,
@@ -4073,7 +4269,16 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
                     if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
                     const int bu = ao_budget();
-                    if (bu <= 2)
+                    if (ao_refill() && bu >= 3) {  // persistent lanes: budgets 4 (3-5), 8 (6-11), 16 (12+)
+                        const dim3 g(grid_for(e1 - b, 16384));
+                        if (bu <= 5)
+                            hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 4>), g, dim3(TB), 0, s, S, W, e1 - b);
+                        else if (bu <= 11)
+                            hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 8>), g, dim3(TB), 0, s, S, W, e1 - b);
+                        else
+                            hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 16>), g, dim3(TB), 0, s, S, W, e1 - b);
+                    }
+                    else if (bu <= 2)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 2>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
                     else if (bu == 3)
@@ -4082,9 +4287,6 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     else if (bu == 5 || bu == 6)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 6>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    else if (bu <= 4 && ao_refill())
-                        hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)),
-                                           dim3(TB), 0, s, S, W, e1 - b);
                     else if (bu <= 4)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
@@ -4095,6 +4297,8 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     if (ao_budget2() > 0) {
                         hipLaunchKernelGGL((ao_late_kernel<6, 16, 16, 0>), dim3(4096), dim3(TB), 0, s, S, W);
                         hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 1>), dim3(1024), dim3(TB), 0, s, S, W);
+                    } else if (ao_refill() && late_wpe() == 6) {
+                        hipLaunchKernelGGL((ao_late_refill_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
                     } else {
 #ifdef RT580_DIAGNOSTICS
                         if (late_wpe() == 8 && late_reread() == 0)
