@@ -184,6 +184,34 @@ __device__ bool any_hit_scalar(const DevScene& S, bool active, rv3 o, rv3 d) {
     return active && hit;
 }
 
+// any_hit_scalar for two rays per lane: each primitive is loaded once for
+// both; both tests run unconditionally (straight-line code the compiler can
+// interleave; an any-hit answer is the OR over the primitives, so testing a ray
+// already hit changes nothing). Early exit once every lane has both answers.
+template <bool SIGN = false>
+__device__ void any_hit_scalar2(const DevScene& S, bool a0, rv3 o0, rv3 d0, bool a1, rv3 o1, rv3 d1, bool& h0,
+                                bool& h1) {
+    bool x0 = !a0, x1 = !a1;
+    for (int j = 0; j < S.n_prims; j++) {
+        const rt_prim P = load_prim_scalar(S.prims, j);
+        float t0, t1, a, b, g;
+        if (P.kind == RT_PRIM_TRIANGLE) {
+            const bool y0 = tri_test<false, SIGN>(P, o0, d0, t0, a, b, g);
+            const bool y1 = tri_test<false, SIGN>(P, o1, d1, t1, a, b, g);
+            x0 = x0 || y0;
+            x1 = x1 || y1;
+        } else {
+            const bool y0 = sph_test(P, o0, d0, t0);
+            const bool y1 = sph_test(P, o1, d1, t1);
+            x0 = x0 || y0;
+            x1 = x1 || y1;
+        }
+        if (__builtin_amdgcn_read_exec() == __ballot(x0 && x1)) break;  // every lane of the wave done
+    }
+    h0 = a0 && x0;
+    h1 = a1 && x1;
+}
+
 // Small scenes (<= TILE primitives) are staged once per workgroup and stay resident.
 __device__ __forceinline__ bool stage_resident(const DevScene& S, rt_prim* tile) {
     const bool resident = S.n_prims <= TILE;
@@ -1002,6 +1030,89 @@ __device__ __forceinline__ void ao_finish(const DevScene& S, const DevWork& W, u
 // ao_fix_kernel instead of running glibc's sincos inline (keeps the rarely
 // taken fallback's registers out of the hot loop).
 // AO items [item_begin, item_end) (item = call * N + sample).
+// One AO sample of ao_body: item -> its call c and the ray (o, d) of
+// CalculateAmbientOcclusion's hemisphere sample (RandomInHemisphere /
+// RandomUnitVector with the serial RNG's draws); ao_brute: a far-origin ray;
+// fix: the fast sincos's rounding test failed (VARIANT & 4096).
+template <int VARIANT>
+__device__ __forceinline__ void ao_sample(const DevScene& S, const DevFrame& F, const DevWork& W, const double* sct,
+                                          uint32_t N, bool pow2, int log2n, bool wave_per_call, uint64_t item,
+                                          bool active, uint64_t& c, rv3& o, rv3& d, bool& ao_brute, bool& fix) {
+    c = 0;
+    uint32_t s = 0;
+    if (active) {
+        if (pow2) { c = item >> log2n; s = (uint32_t)(item & (N - 1)); }
+        else { c = item / N; s = (uint32_t)(item - c * N); }
+    }
+    o = v3(0, 0, 0);
+    d = v3(0, 0, 0);
+    ao_brute = false;
+    fix = false;  // VARIANT & 4096: this sample goes to ao_fix_kernel
+    if (active) {
+        // With N a multiple of 64 a wave serves one call: keep its data scalar.
+        uint32_t cc = (uint32_t)c;
+        if (wave_per_call) cc = __builtin_amdgcn_readfirstlane(cc);
+        uint32_t node = W.call_node[cc];
+        if (wave_per_call) node = __builtin_amdgcn_readfirstlane(node);
+        const NodeRec& nd = W.nodes[node];
+        rv3 hp = ld3(nd.hp), n = ld3(nd.n);
+        uint64_t rbase = W.call_rng[cc];
+        if (wave_per_call) {
+            hp = v3(__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.x))),
+                    __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.y))),
+                    __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.z))));
+            n = v3(__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.x))),
+                   __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.y))),
+                   __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.z))));
+            rbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rbase >> 32)) << 32) |
+                    __builtin_amdgcn_readfirstlane((uint32_t)rbase);
+        }
+        float u0, u1;
+        ao_draws(F, W, rbase, s, u0, u1);
+        // uniform_real_distribution<float>: canonical * (b - a) + a
+        const float z = u0 * (1.0f - (-1.0f)) + (-1.0f);
+        const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
+        // Ranges for the 2048 sequences (rt_math.h): z is 0 or a multiple of
+        // 2^-30 in [-1, 1), so 1 - z*z (float) is +0 or >= 2^-24 and r is 0 or
+        // >= 2^-12; |cos|, |sin| of a float angle in [0, 2pi) are 0 or > 2^-27,
+        // so v's components are 0 or in [2^-39, 1] and |v| ~ 1 (also after the
+        // first normalize).
+        const float r = (VARIANT & 2048) ? rt_sqrt_nr(1 - z * z) : sqrtf(1 - z * z);
+        rv3 v;
+        if (VARIANT & 4096) {
+            double sa, ca;
+            rt_fast_sincos((double)ang, &sa, &ca);
+            const double X = (double)r * ca, Y = (double)r * sa;
+            const float fx = (float)X, fy = (float)Y;
+            fix = !(rt_f32_round_safe(X, fx) && rt_f32_round_safe(Y, fy));
+            v = v3(fx, fy, z);
+        } else if (VARIANT & 1024) {
+            float vx, vy;
+            rt_ao_dir_xy(rt_dev::rt_sincostab, r, ang, &vx, &vy);
+            v = v3(vx, vy, z);
+        } else {
+            double sa, ca;
+#ifdef RT580_DIAGNOSTICS
+            if (VARIANT & 64) { sa = ang; ca = z; }  // DIAGNOSTIC build only (wrong output)
+            else
+#endif
+            rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
+            v = v3((float)((double)r * ca), (float)((double)r * sa), z);
+        }
+#ifdef RT580_DIAGNOSTICS
+        constexpr bool skip_norm = (VARIANT & 128) != 0;  // DIAGNOSTIC build only (wrong output)
+#else
+        constexpr bool skip_norm = false;
+#endif
+        if (!skip_norm) v = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
+        if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
+        o = v3_add(hp, v3_scale(v, 0.2f));
+        // Ray constructor (Raytracer.h:431-433)
+        d = skip_norm ? v : ((VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v));
+        if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o);
+    }
+}
+
 template <int VARIANT>
 __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, const DevWork& W,
                                         uint64_t item_begin = 0, uint64_t item_end = ~0ull) {
@@ -1021,119 +1132,73 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
     const int log2n = 31 - __clz((int)N);
     const bool wave_per_call = (VARIANT & 2) && (N & 63u) == 0;
     const bool resident = (VARIANT & (8 | 512)) ? true : stage_resident(S, tile);
-    for (uint64_t b0 = item_begin + (uint64_t)blockIdx.x * TB; b0 < items; b0 += (uint64_t)gridDim.x * TB) {
-        const uint64_t item = b0 + threadIdx.x;
-        bool active = item < items;
-        uint64_t c = 0;
-        uint32_t s = 0;
-        if (active) {
-            if (pow2) { c = item >> log2n; s = (uint32_t)(item & (N - 1)); }
-            else { c = item / N; s = (uint32_t)(item - c * N); }
+    // VARIANT & 32768: two samples per lane (items b0 + threadIdx.x and
+    // b0 + TB + threadIdx.x): the scene loop loads each primitive once for both
+    // rays, and the two rays' arithmetic is independent (more work in flight per
+    // wave, half the per-sample scalar loads and loop control)
+    constexpr int SPL = (VARIANT & 32768) ? 2 : 1;
+    for (uint64_t b0 = item_begin + (uint64_t)blockIdx.x * TB * SPL; b0 < items; b0 += (uint64_t)gridDim.x * TB * SPL) {
+        bool active[SPL], ao_brute[SPL], fix[SPL], hit[SPL];
+        uint64_t c[SPL];
+        rv3 o[SPL], d[SPL];
+#pragma unroll
+        for (int k = 0; k < SPL; k++) {
+            const uint64_t item = b0 + (uint64_t)k * TB + threadIdx.x;
+            active[k] = item < items;
+            ao_sample<VARIANT>(S, F, W, sct, N, pow2, log2n, wave_per_call, item, active[k], c[k], o[k], d[k],
+                               ao_brute[k], fix[k]);
         }
-        rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-        bool ao_brute = false;
-        bool fix = false;  // VARIANT & 4096: this sample goes to ao_fix_kernel
-        if (active) {
-            // With N a multiple of 64 a wave serves one call: keep its data scalar.
-            uint32_t cc = (uint32_t)c;
-            if (wave_per_call) cc = __builtin_amdgcn_readfirstlane(cc);
-            uint32_t node = W.call_node[cc];
-            if (wave_per_call) node = __builtin_amdgcn_readfirstlane(node);
-            const NodeRec& nd = W.nodes[node];
-            rv3 hp = ld3(nd.hp), n = ld3(nd.n);
-            uint64_t rbase = W.call_rng[cc];
-            if (wave_per_call) {
-                hp = v3(__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.x))),
-                        __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.y))),
-                        __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, hp.z))));
-                n = v3(__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.x))),
-                       __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.y))),
-                       __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, n.z))));
-                rbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rbase >> 32)) << 32) |
-                        __builtin_amdgcn_readfirstlane((uint32_t)rbase);
-            }
-            float u0, u1;
-            ao_draws(F, W, rbase, s, u0, u1);
-            // uniform_real_distribution<float>: canonical * (b - a) + a
-            const float z = u0 * (1.0f - (-1.0f)) + (-1.0f);
-            const float ang = u1 * (F.ao_angle_max - 0.0f) + 0.0f;
-            // Ranges for the 2048 sequences (rt_math.h): z is 0 or a multiple of
-            // 2^-30 in [-1, 1), so 1 - z*z (float) is +0 or >= 2^-24 and r is 0 or
-            // >= 2^-12; |cos|, |sin| of a float angle in [0, 2pi) are 0 or > 2^-27,
-            // so v's components are 0 or in [2^-39, 1] and |v| ~ 1 (also after the
-            // first normalize).
-            const float r = (VARIANT & 2048) ? rt_sqrt_nr(1 - z * z) : sqrtf(1 - z * z);
-            rv3 v;
+#pragma unroll
+        for (int k = 0; k < SPL; k++) {
+            const uint64_t item = b0 + (uint64_t)k * TB + threadIdx.x;
             if (VARIANT & 4096) {
-                double sa, ca;
-                rt_fast_sincos((double)ang, &sa, &ca);
-                const double X = (double)r * ca, Y = (double)r * sa;
-                const float fx = (float)X, fy = (float)Y;
-                fix = !(rt_f32_round_safe(X, fx) && rt_f32_round_safe(Y, fy));
-                v = v3(fx, fy, z);
-            } else if (VARIANT & 1024) {
-                float vx, vy;
-                rt_ao_dir_xy(rt_dev::rt_sincostab, r, ang, &vx, &vy);
-                v = v3(vx, vy, z);
-            } else {
-                double sa, ca;
-#ifdef RT580_DIAGNOSTICS
-                if (VARIANT & 64) { sa = ang; ca = z; }  // DIAGNOSTIC build only (wrong output)
-                else
-#endif
-                rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
-                v = v3((float)((double)r * ca), (float)((double)r * sa), z);
+                const uint64_t fm = __ballot(fix[k]);
+                if (fm) {
+                    const int leader = __ffsll((unsigned long long)fm) - 1;
+                    uint32_t fb = 0;
+                    if ((threadIdx.x & 63) == leader) fb = atomicAdd(W.aofix_count, (uint32_t)__popcll(fm));
+                    fb = __shfl(fb, leader);
+                    if (fix[k]) {
+                        const uint32_t slot = fb + (uint32_t)__popcll(fm & lanemask_lt());
+                        if (slot < W.aofix_cap) W.aofix_items[slot] = item;
+                        active[k] = false;
+                        ao_brute[k] = false;
+                    }
+                }
             }
-#ifdef RT580_DIAGNOSTICS
-            constexpr bool skip_norm = (VARIANT & 128) != 0;  // DIAGNOSTIC build only (wrong output)
-#else
-            constexpr bool skip_norm = false;
-#endif
-            if (!skip_norm) v = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
-            if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
-            o = v3_add(hp, v3_scale(v, 0.2f));
-            // Ray constructor (Raytracer.h:431-433)
-            d = skip_norm ? v : ((VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v));
-            if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o);
-        }
-        if (VARIANT & 4096) {
-            const uint64_t fm = __ballot(fix);
-            if (fm) {
-                const int leader = __ffsll((unsigned long long)fm) - 1;
-                uint32_t fb = 0;
-                if ((threadIdx.x & 63) == leader) fb = atomicAdd(W.aofix_count, (uint32_t)__popcll(fm));
-                fb = __shfl(fb, leader);
-                if (fix) {
-                    const uint32_t slot = fb + (uint32_t)__popcll(fm & lanemask_lt());
-                    if (slot < W.aofix_cap) W.aofix_items[slot] = item;
-                    active = false;
-                    ao_brute = false;
+            if (VARIANT & 16384) {
+                // generation only: the ray record for ao_trace_kernel (flag 0: no ray,
+                // 1: near query, 2: far origin)
+                if (item < items) {
+                    const uint32_t flag = active[k] ? (ao_brute[k] ? 2u : 1u) : 0u;
+                    float4* r = W.ao_rays + 2 * (size_t)(item - item_begin);
+                    r[0] = make_float4(o[k].x, o[k].y, o[k].z, __uint_as_float((uint32_t)c[k]));
+                    r[1] = make_float4(d[k].x, d[k].y, d[k].z, __uint_as_float(flag));
                 }
             }
         }
-        if (VARIANT & 16384) {
-            // generation only: the ray record for ao_trace_kernel (flag 0: no ray,
-            // 1: near query, 2: far origin)
-            if (item < items) {
-                const uint32_t flag = active ? (ao_brute ? 2u : 1u) : 0u;
-                float4* r = W.ao_rays + 2 * (size_t)(item - item_begin);
-                r[0] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)c));
-                r[1] = make_float4(d.x, d.y, d.z, __uint_as_float(flag));
-            }
-            continue;
-        }
-        const bool hit =
+        if (VARIANT & 16384) continue;
+        if (SPL == 2 && (VARIANT & 8) && !(VARIANT & 512)) {
+            any_hit_scalar2<(VARIANT & 4) != 0>(S, active[0], o[0], d[0], active[SPL - 1], o[SPL - 1], d[SPL - 1],
+                                                hit[0], hit[SPL - 1]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < SPL; k++)
+                hit[k] =
 #ifdef RT580_DIAGNOSTICS
-                         (VARIANT & 32) ? (d.x > 2.0f) :  // DIAGNOSTIC build only (wrong output)
+                    (VARIANT & 32) ? (d[k].x > 2.0f) :  // DIAGNOSTIC build only (wrong output)
 #endif
-                         (VARIANT & 8192) ? bvh_any_near_wave(S.bv, active && !ao_brute, o, d, ao_wstk[threadIdx.x >> 6])
+                    (VARIANT & 8192) ? bvh_any_near_wave(S.bv, active[k] && !ao_brute[k], o[k], d[k], ao_wstk[threadIdx.x >> 6])
 #ifdef RT580_DIAG_NO_NEAR
-                       : (VARIANT & 512) ? (active && !ao_brute)  // DIAGNOSTIC build only: every AO ray occluded, no traversal
+                  : (VARIANT & 512) ? (active[k] && !ao_brute[k])  // DIAGNOSTIC build only: every AO ray occluded, no traversal
 #endif
-                       : (VARIANT & 512) ? (active && !ao_brute && bvh_any_near(S.bv, o, d))
-                       : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active, o, d)
-                                       : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active, o, d);
-        ao_finish<(VARIANT & 512) != 0>(S, W, N, active, ao_brute, hit, c, o, d);
+                  : (VARIANT & 512) ? (active[k] && !ao_brute[k] && bvh_any_near(S.bv, o[k], d[k]))
+                  : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active[k], o[k], d[k])
+                                  : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active[k], o[k], d[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < SPL; k++)
+            ao_finish<(VARIANT & 512) != 0>(S, W, N, active[k], ao_brute[k], hit[k], c[k], o[k], d[k]);
     }
 }
 
@@ -1968,7 +2033,8 @@ static int ao_sort() {
 // RT580_AO_BUDGET: leaf visits per AO ray in ao_trace_kernel before the ray is
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
-// RT580_AO_REFILL: the AO trace's persistent-lane form (ao_trace_refill_kernel)
+// RT580_AO_REFILL: persistent-lane forms, bit 0 the AO trace (ao_trace_refill_kernel),
+// bit 1 the late pass (ao_late_refill_kernel)
 static int ao_refill() {
     static int v = -1;
     if (v < 0) {
@@ -4269,7 +4335,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
                     if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
                     const int bu = ao_budget();
-                    if (ao_refill() && bu >= 3) {  // persistent lanes: budgets 4 (3-5), 8 (6-11), 16 (12+)
+                    if ((ao_refill() & 1) && bu >= 3) {  // persistent lanes: budgets 4 (3-5), 8 (6-11), 16 (12+)
                         const dim3 g(grid_for(e1 - b, 16384));
                         if (bu <= 5)
                             hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 4>), g, dim3(TB), 0, s, S, W, e1 - b);
@@ -4297,7 +4363,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     if (ao_budget2() > 0) {
                         hipLaunchKernelGGL((ao_late_kernel<6, 16, 16, 0>), dim3(4096), dim3(TB), 0, s, S, W);
                         hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 1>), dim3(1024), dim3(TB), 0, s, S, W);
-                    } else if (ao_refill() && late_wpe() == 6) {
+                    } else if ((ao_refill() & 2) && late_wpe() == 6) {
                         hipLaunchKernelGGL((ao_late_refill_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
                     } else {
 #ifdef RT580_DIAGNOSTICS
@@ -4446,6 +4512,7 @@ hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& 
 #define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(ao_grid()), dim3(TB), 0, s, S, F, W, call_lo, call_hi); break;
             RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8) RT_AO_CASE(1032) RT_AO_CASE(2056) RT_AO_CASE(3080)
             RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128) RT_AO_CASE(7180) RT_AO_CASE(7182)
+            RT_AO_CASE(32768 | 7180)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;
         }
@@ -4458,6 +4525,7 @@ hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& 
             RT_AO_CASE(41) RT_AO_CASE(73) RT_AO_CASE(105) RT_AO_CASE(137) RT_AO_CASE(233)
 #endif
             RT_AO_CASE(1032) RT_AO_CASE(3080) RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(7180) RT_AO_CASE(7182)
+            RT_AO_CASE(32768 | 7180)
 #undef RT_AO_CASE
             default: return hipErrorInvalidValue;
         }

@@ -47,6 +47,7 @@ const long kAoVariant[] = {
     1032, 3080, 3084, 7176, 7180, 7182,                                               // ao_kernel<v>, v >= 32
     16 | 1, 16 | 9, 16 | 8, 16 | 1032, 16 | 2056, 16 | 3080, 16 | 3084, 16 | 7176,   // ao_kernel_occ8<v>
     16 | 5128, 16 | 7180, 16 | 7182,
+    32768 | 7180, 32768 | 16 | 7180,                                                  // two samples per lane
 #ifdef RT580_DIAGNOSTICS
     41, 73, 105, 137, 233,
 #endif
@@ -82,7 +83,7 @@ const Knob kKnobs[] = {
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
     {"RT580_AO_RESUME", INT_SET, 0, 0, k01, nullptr},
     {"RT580_D2H_MAPPED", INT_SET, 0, 0, k01, nullptr},
-    {"RT580_AO_REFILL", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_AO_REFILL", INT_RANGE, 0, 3, nullptr, nullptr},
     {"RT580_SMALL_SORT", INT_SET, 0, 0, k01, nullptr},
     {"RT580_D2H_BLOCKS", INT_RANGE, 1, 65536, nullptr, nullptr},
     {"RT580_TRACE_WPE", INT_SET, 0, 0, kTraceWpe, nullptr},
