@@ -4255,7 +4255,9 @@ static int ao_variant() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_AO_VARIANT");
-        v = e ? atoi(e) : (4 | 8 | 16 | 1024 | 2048 | 4096);  // scalar scene, 8 waves/SIMD, fast sincos/normalize, sign rejects
+        // scalar scene, 8 waves/SIMD, fast sincos/normalize, sign rejects, two samples per lane
+        // (config 2: 1.519 / 1.539 vs 1.586 / 1.582 ms per frame, profiles/r05/ab/spl_*.json)
+        v = e ? atoi(e) : (4 | 8 | 16 | 1024 | 2048 | 4096 | 32768);
     }
     return v;
 }

@@ -52,7 +52,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 # every 2 cycles, 2.4 GHz; HBM3E 8.0 TB/s.
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0   # 1228.8 G wave-instructions/s
 HBM_PEAK_GBS = 8000.0
-PROFILE_ROUNDS = ("r04", "r03", "r02")         # newest committed counter profiles first
+PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")  # newest committed counter profiles first
 
 # name -> (scene, synthetic?, width, height, depth, AO samples, label)
 WORKLOADS = {
