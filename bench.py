@@ -453,16 +453,19 @@ def frame_check(ctx, name, frame_np, single, W, H, check):
 
 def isolated_ao_launch(lib, rt580, step, torch, rays_ao_frame, frames=3):
     """Mean AO-kernel launch (ms) and AO rays per launch over `frames` frames
-    rendered with AO phases in frame order (rt580_set_ao_order(1)): the AO
-    kernel then shares the chip with the next frame's trace at most, never with
-    another frame's AO kernels. Untimed; restores the default order."""
+    rendered one at a time (each step's frame complete before the next is
+    queued, AO phases in frame order): the AO kernel runs with no other frame's
+    kernels beside it -- its own rate, comparable with the rocprofv3 mean of the
+    committed profile. Untimed; restores the default order."""
     rt580.check(lib.rt580_set_ao_order(1), "rt580_set_ao_order")
     try:
         step()
+        rt580.check(lib.rt_gpu_synchronize(), "rt_gpu_synchronize")
         torch.cuda.synchronize()
         rt580.check(lib.rt_gpu_profile(1), "rt_gpu_profile")
         for _ in range(frames):
             step()
+            rt580.check(lib.rt_gpu_synchronize(), "rt_gpu_synchronize")
         torch.cuda.synchronize()
         ms = [ctypes.c_double() for _ in range(4)]
         nf = ctypes.c_int()
@@ -529,9 +532,9 @@ def roofline(workload, k_ms, k_launches, k_rays, iso=None):
         a_iso = prof["valu_per_ao_ray"] * iso["rays_per_launch"] / (iso["launch_ms"] * 1e-3) / 1e9
         res["isolated"] = {"launch_ms": round(iso["launch_ms"], 4), "ao_rays_per_launch": int(iso["rays_per_launch"]),
                            "achieved": round(a_iso, 2), "frac": round(a_iso / VALU_PEAK_GINST, 4),
-                           "note": "the same kernel timed over %d further frames with AO phases in frame order "
-                                   "(rt580_set_ao_order(1), untimed): no other frame's AO kernels beside the launch"
-                                   % iso["frames"]}
+                           "note": "the same kernel timed over %d further frames rendered one at a time (untimed; "
+                                   "each frame complete before the next is queued): no other frame's kernels beside "
+                                   "the launch" % iso["frames"]}
     res["note"] = ("VALU-issue roofline: counter-measured VALU wave-instructions per AO ray x AO rays per launch "
                    "/ live launch time (frames overlap: AO phases of consecutive frames may run together, which "
                    "stretches each launch; `isolated` times it without that); traffic = FETCH_SIZE+WRITE_SIZE "
