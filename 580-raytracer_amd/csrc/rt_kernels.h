@@ -92,7 +92,8 @@ struct DevWork {
     uint64_t* call_rng;    // [call_cap] minstd state at the call's first draw / mt19937 global call index
     uint32_t* occ;         // [call_cap] occluded samples
     const uint32_t* mt_stream;  // mt19937 draws [mt_base, ...) of the serial stream, else null
-    uint64_t mt_base;           // absolute index of mt_stream[0]
+    uint64_t mt_base;
+    uint32_t refill_min;   // RT580_AO_REFILL_MIN: idle lanes a persistent-lane wave refills at once           // absolute index of mt_stream[0]
     uint32_t node_cap;
     uint32_t call_cap;
     // BVH scenes: AO rays that miss every near triangle, queued for the sorted

@@ -1523,9 +1523,13 @@ ao_trace_refill_kernel(DevScene S, DevWork W, uint64_t n) {
         int32_t c = 0, nn = 0;
         for (;;) {
             bool fin = false, hit = false, brute = false, late = false;
-            // idle lanes take the next samples of the pool
+            // idle lanes take the next samples of the pool, in batches of at
+            // least W.refill_min lanes (or when the wave is empty): refilled
+            // lanes start at the root together, so their first node loads
+            // coalesce as in the round form
             const uint64_t want = __ballot(!busy);
-            if (want && p_next < p_end) {
+            if (want && p_next < p_end &&
+                ((uint32_t)__popcll(want) >= W.refill_min || want == __builtin_amdgcn_read_exec())) {
                 const uint32_t pos = p_next + (uint32_t)__popcll(want & lt_mask);
                 p_next += (uint32_t)__popcll(want);
                 if (!busy && pos < p_end) {
@@ -1725,7 +1729,8 @@ ao_late_refill_kernel(DevScene S, DevWork W) {
     for (;;) {
         bool fin = false, hit = false;
         const uint64_t want = __ballot(!busy);
-        if (want && p_next < p_end) {
+        if (want && p_next < p_end &&
+            ((uint32_t)__popcll(want) >= W.refill_min || want == __builtin_amdgcn_read_exec())) {
             const uint32_t k = p_next + (uint32_t)__popcll(want & lt_mask);
             p_next += (uint32_t)__popcll(want);
             if (!busy && k < p_end) {

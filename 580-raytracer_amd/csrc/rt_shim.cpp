@@ -603,6 +603,11 @@ DevWork dev_work() {
     w.occ = (uint32_t*)SL.occ.p;
     w.mt_stream = (const uint32_t*)SL.mt_stream.p;
     w.mt_base = SL.mt_base;
+    static const uint32_t refill_min = [] {
+        const char* e = std::getenv("RT580_AO_REFILL_MIN");
+        return e ? (uint32_t)std::atoi(e) : 32u;
+    }();
+    w.refill_min = refill_min;
     w.node_cap = g.node_cap;
     w.call_cap = g.call_cap;
     w.far_rays = (float4*)SL.far_rays.p;
