@@ -70,6 +70,7 @@ struct SchedKey {
 
 struct State {
     bool inited = false;
+    DevBuf ppm_stage;  // rt_gpu_deinterleave_ppm without the host mapping (RT580_D2H_MAPPED=0)
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -1685,6 +1686,29 @@ int rt_gpu_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out) {
     return RT_SUCCESS;
 }
 
+int rt_gpu_deinterleave_ppm(const uint8_t* tiles, int world, int n_max, int width, int height,
+                            uint8_t* ppm_body_host) {
+    RT_WORK("rt_gpu_deinterleave_ppm");
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (!tiles || !ppm_body_host || world < 1 || width < 1 || height < 1 || (int64_t)n_max * world < height)
+        return fail("rt_gpu_deinterleave_ppm: bad arguments");
+    HIP_TRY(hipSetDevice(g.device));
+    const size_t body = (size_t)width * height * 3;
+    HostRange* hr = host_range_ready(ppm_body_host, body);
+    if (!hr) return fail("rt_gpu_deinterleave_ppm: the buffer is not a registered range of %zu bytes", body);
+    HIP_TRY(hipStreamWaitEvent(g.stream, hr->copied, 0));
+    if (uint8_t* dst = (uint8_t*)mapped(hr, ppm_body_host)) {
+        HIP_TRY(launch_deinterleave_u8(tiles, world, n_max, width, height, dst, g.stream));
+    } else {
+        DevBuf& f8 = g.ppm_stage;
+        if (ensure(f8, body)) return RT_FAILURE;
+        HIP_TRY(launch_deinterleave_u8(tiles, world, n_max, width, height, (uint8_t*)f8.p, g.stream));
+        HIP_TRY(hipMemcpyAsync(ppm_body_host, f8.p, body, hipMemcpyDeviceToHost, g.stream));
+    }
+    HIP_TRY(hipEventRecord(hr->copied, g.stream));
+    return RT_SUCCESS;
+}
+
 int rt580_selftest_math(uint64_t seed, uint64_t n, uint64_t* mismatches) {
     RT_WORK("rt580_selftest_math");
     if (!g.inited) return fail("rt_gpu_init not called");
@@ -1866,7 +1890,7 @@ void shutdown_ctx() {
     for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always, &g.grid2_start, &g.grid2_items})
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute,
-                      &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims})
+                      &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.ppm_stage})
         release(*b);
     for (Slot& sl : g.slot) {
         for (DevBuf* b : {&sl.nodes, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,

@@ -45,9 +45,20 @@ class GpuRows:
         p.row_begin, p.row_end, p.row_step = rank, self.height, world
         return p
 
-    def count(self, rank, world):
+    def count(self, rank, world, persistent=False):
+        """The per-row AO calls of this rank's rows (int32[n_max], padding rows
+        0). persistent=True reuses one buffer per (rank, world) (DistFrame: the
+        padding rows stay zero, the rows are rewritten every frame; its reader,
+        the all-gather, is ordered before the next frame's count on the stream)."""
         t = self.torch
-        out = t.zeros(n_max_rows(self.height, world), dtype=t.int32, device=self.device)
+        if persistent:
+            key = (rank, world)
+            if getattr(self, "_cnt_key", None) != key:
+                self._cnt = t.zeros(n_max_rows(self.height, world), dtype=t.int32, device=self.device)
+                self._cnt_key = key
+            out = self._cnt
+        else:
+            out = t.zeros(n_max_rows(self.height, world), dtype=t.int32, device=self.device)
         self._pc = self._p(rank, world)
         self.rt580.check(self.lib.rt_gpu_count_rows(ctypes.byref(self._pc), out.data_ptr()), "rt_gpu_count_rows")
         return out
@@ -114,7 +125,10 @@ class DistFrame:
     """Steady-state multi-rank frames on the GPU backend over RCCL (see module doc).
     u8=True: each rank applies FlushFrameBufferToPPM's gamma mapping to its rows
     before the gather (3 B/px on the wire instead of 6), and rank 0
-    assembles the PPM body; u8=False gathers the int16 Pixel framebuffer."""
+    writes the PPM body into registered host memory (rt_gpu_deinterleave_ppm);
+    u8=False gathers the int16 Pixel framebuffer. The library's stream must be
+    torch's current stream (rt_gpu_set_stream), which the collectives' waits
+    order against."""
 
     def __init__(self, backend, dist, torch, height, width, rank, world, device, u8=True):
         self.b, self.dist, self.t = backend, dist, torch
@@ -130,12 +144,29 @@ class DistFrame:
                       for _ in range(2)] if rank == 0 else None
         self.frame = torch.empty(self.n_max * world, width, 3, dtype=torch.uint8 if u8 else torch.int16,
                                  device=device) if rank == 0 else None
-        # rank 0: each assembled frame is copied into page-locked host memory on
-        # the compute stream (a ring of two, the frames in flight): a step ends
-        # with the frame on the host, as the one-process paths' steps do
+        # rank 0: each assembled frame lands in page-locked host memory (a ring
+        # of two, the frames in flight): a step ends with the frame on the
+        # host, as the one-process paths' steps do. The u8 frame is
+        # de-interleaved by the library straight into registered host buffers
+        # (rt_gpu_deinterleave_ppm: one kernel writing through the host
+        # mapping); the int16 frame is assembled by torch and copied.
         on_gpu = torch.device(device).type == "cuda"
-        self.host = [torch.empty(height, width, 3, dtype=self.frame.dtype, pin_memory=True)
-                     for _ in range(2)] if rank == 0 and on_gpu else None
+        self.lib = getattr(backend, "lib", None) if (on_gpu and u8 and rank == 0) else None
+        self.host = None
+        self._reg = []
+        if rank == 0 and on_gpu and self.lib is not None:
+            import numpy as np
+            span = (height * width * 3 + 4095) // 4096 * 4096
+            for _ in range(2):
+                raw = np.zeros(span + 4096, dtype=np.uint8)
+                off = (-raw.ctypes.data) % 4096
+                buf = raw[off:off + span]
+                backend.rt580.check(self.lib.rt_gpu_host_register(buf.ctypes.data, span), "rt_gpu_host_register")
+                self._reg.append((raw, buf))
+            self.host = [torch.from_numpy(buf[:height * width * 3]).view(height, width, 3) for _, buf in self._reg]
+            self.frame = None  # not used: the tiles go straight to the host buffers
+        elif rank == 0 and on_gpu:
+            self.host = [torch.empty(height, width, 3, dtype=self.frame.dtype, pin_memory=True) for _ in range(2)]
         self.host_i = 0
         self.last_host = None
         self.work = [None, None]
@@ -147,6 +178,13 @@ class DistFrame:
             self.work[k].wait()  # stream-level: the compute stream waits for the collective
             self.work[k] = None
         if self.rank == 0:
+            if self.lib is not None:  # u8 tiles -> the PPM body in registered host memory, one kernel
+                self.last_host = self.host[self.host_i]
+                self.b.rt580.check(self.lib.rt_gpu_deinterleave_ppm(
+                    self.tiles[k].data_ptr(), self.world, self.n_max, self.w, self.h,
+                    self._reg[self.host_i][1].ctypes.data), "rt_gpu_deinterleave_ppm")
+                self.host_i ^= 1
+                return
             tiles = (self.tiles[k] if self.u8 else self.tiles[k].view(self.t.int16)).view(
                 self.world, self.n_max, self.w, 3)
             self.frame.view(self.n_max, self.world, self.w, 3).copy_(tiles.transpose(0, 1))
@@ -160,7 +198,8 @@ class DistFrame:
         if self.work[k] is not None:  # buffer k's gather (two frames ago) must be done before reuse
             self._assemble(k)
             self.pending = None
-        counts = self.b.count(self.rank, self.world)
+        counts = self.b.count(self.rank, self.world, persistent=True) if isinstance(self.b, GpuRows) else \
+            self.b.count(self.rank, self.world)
         self.dist.all_gather_into_tensor(self.gathered, counts)
         self.b.row_bases(self.gathered, self.rank, self.world, self.base)
         fb = self.b.shade(self.rank, self.world, self.base, out=self.fb[k])
@@ -190,5 +229,13 @@ class DistFrame:
             return None
         if self.host is None:  # a CPU backend (gloo tests): the frame is host memory already
             return self.frame[:self.h]
-        self.t.cuda.current_stream(self.frame.device).synchronize()
+        if self.lib is not None:
+            self.b.rt580.check(self.lib.rt_gpu_synchronize(), "rt_gpu_synchronize")
+        self.t.cuda.current_stream(self.tiles[0].device).synchronize()
         return self.last_host
+
+    def close(self):
+        """Unregister rank 0's host buffers (after finish())."""
+        for _, buf in self._reg:
+            self.lib.rt_gpu_host_unregister(buf.ctypes.data)
+        self._reg = []

@@ -386,6 +386,8 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     if cpu_baseline_on and ctx.n_gpus == 1 and not ctx.dist_on:
         gpu_px = frame_np.reshape(-1, 3) if frame_np is not None else None
         out["cpu_baseline"] = cpu_baseline(ctx, name, root, params, gpu_px, row_counts)
+    if dframe is not None:
+        dframe.close()
     return out
 
 

@@ -225,6 +225,14 @@ int rt_gpu_render_multi(const rt_render_params* params, int16_t* fb_out, int n_d
  * the next frame's kernels. Complete after rt_gpu_synchronize. */
 int rt_gpu_render_multi_async(const rt_render_params* params, uint8_t* ppm_body_host, int n_devices,
                               const int* devices);
+/* The PPM body of a frame from the u8 row tiles of its `world` interleaved
+ * shares (tile r = rows r, r + world, ... of n_max rows each, contiguous on
+ * this device: what rank 0 gathers in the one-process-per-GPU path), written
+ * into ppm_body_host (a registered range of height x width x 3 bytes) on the
+ * library's stream, after any earlier write into the same range. The
+ * per-process driver's last step (rt580_dist.DistFrame). */
+int rt_gpu_deinterleave_ppm(const uint8_t* tiles, int world, int n_max, int width, int height,
+                            uint8_t* ppm_body_host);
 /* Visible HIP devices (0 without a GPU). */
 int rt_gpu_device_count(void);
 /* FlushFrameBufferToPPM's pixel mapping on the device (Raytracer.cpp:812-818):

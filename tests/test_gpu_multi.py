@@ -229,3 +229,35 @@ def test_render_multi_async_frames_are_the_ppm_bodies(G, transport):
             lib.rt_gpu_host_unregister(buf.ctypes.data)
     for rt, _ in rts:
         rt.close()
+
+
+@pytest.mark.parametrize("world,w,h", [(1, 64, 48), (3, 53, 29), (8, 1920, 1080)])
+def test_deinterleave_ppm_into_registered_memory(world, w, h):
+    """rt_gpu_deinterleave_ppm (rank 0's last step in rt580_dist.DistFrame): the
+    u8 tiles of `world` interleaved row shares (tile r = rows r, r + world, ...,
+    n_max rows, the last rows padding) land de-interleaved in a registered host
+    range -- against numpy's de-interleave of the same random tiles; twice into
+    the same range in call order; an unregistered buffer is refused."""
+    import torch
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    rt580.check(lib.rt_gpu_init(0), "init")
+    n_max = (h + world - 1) // world
+    g = torch.Generator().manual_seed(world * 1000 + w)
+    tiles = [torch.randint(0, 256, (world, n_max, w, 3), dtype=torch.uint8, generator=g) for _ in range(2)]
+    want = [t.transpose(0, 1).reshape(n_max * world, w, 3)[:h].numpy().reshape(-1) for t in tiles]
+    dev = [t.cuda() for t in tiles]
+    torch.cuda.synchronize()  # the tiles are on the device before the library's stream reads them
+    raw, buf, span = _registered_u8(w * h * 3)
+    rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "host_register")
+    try:
+        for k in (0, 1):
+            rt580.check(lib.rt_gpu_deinterleave_ppm(dev[k].data_ptr(), world, n_max, w, h, buf.ctypes.data),
+                        "rt_gpu_deinterleave_ppm")
+        rt580.check(lib.rt_gpu_synchronize(), "synchronize")
+        torch.cuda.synchronize()
+        assert np.array_equal(buf, want[1])
+        plain = np.zeros(w * h * 3, dtype=np.uint8)
+        assert lib.rt_gpu_deinterleave_ppm(dev[0].data_ptr(), world, n_max, w, h, plain.ctypes.data) != 0
+    finally:
+        lib.rt_gpu_host_unregister(buf.ctypes.data)
