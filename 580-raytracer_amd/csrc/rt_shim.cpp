@@ -71,6 +71,7 @@ struct SchedKey {
 struct State {
     bool inited = false;
     DevBuf ppm_stage;  // rt_gpu_deinterleave_ppm without the host mapping (RT580_D2H_MAPPED=0)
+    hipEvent_t ppm_done = nullptr;  // rt_gpu_shade_rows_ppm's frame-done event when frames are not pipelined
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -1677,6 +1678,32 @@ int rt_gpu_shade_rows(const rt_render_params* p, const uint64_t* row_base_device
     return end_slot();
 }
 
+int rt_gpu_shade_rows_ppm(const rt_render_params* p, const uint64_t* row_base_device, uint8_t* tile_u8_device,
+                          void* done_stream) {
+    RT_WORK("rt_gpu_shade_rows_ppm");
+    if (check_params(p)) return RT_FAILURE;
+    if (!row_base_device || !tile_u8_device) return fail("row_base_device / tile_u8_device is NULL");
+    if (!g.split_ready || std::memcmp(&g.split_params, p, sizeof *p) != 0)
+        return fail("rt_gpu_shade_rows_ppm must follow rt_gpu_count_rows with the same params");
+    HIP_TRY(hipSetDevice(g.device));
+    g.split_ready = false;
+    if (slot_wait_user()) return RT_FAILURE;  // the row bases were produced on the caller's stream
+    const size_t n = (size_t)n_selected_rows(p) * p->width * 3;
+    if (ensure(SL.fb, n * 2)) return RT_FAILURE;  // the slot's own int16 rows
+    if (shade_rows(p, p->row_begin, p->row_step, n_selected_rows(p), row_base_device, (int16_t*)SL.fb.p))
+        return RT_FAILURE;
+    HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, n, tile_u8_device, fs()));
+    if (!done_stream) return end_slot();
+    // end_slot with the wait on done_stream: the caller's stream goes on with
+    // the next frame while this one's AO phase runs
+    if (post_replay_check()) return RT_FAILURE;
+    if (!g.ppm_done) HIP_TRY(hipEventCreateWithFlags(&g.ppm_done, hipEventDisableTiming));
+    hipEvent_t ev = g.pipeline ? SL.done : g.ppm_done;
+    HIP_TRY(hipEventRecord(ev, fs()));
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)done_stream, ev, 0));
+    return RT_SUCCESS;
+}
+
 int rt_gpu_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out) {
     RT_WORK("rt_gpu_gamma_u8");
     if (!g.inited) return fail("rt_gpu_init not called");
@@ -1687,8 +1714,9 @@ int rt_gpu_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out) {
 }
 
 int rt_gpu_deinterleave_ppm(const uint8_t* tiles, int world, int n_max, int width, int height,
-                            uint8_t* ppm_body_host) {
+                            uint8_t* ppm_body_host, void* stream) {
     RT_WORK("rt_gpu_deinterleave_ppm");
+    const hipStream_t cs = stream ? (hipStream_t)stream : g.stream;
     if (!g.inited) return fail("rt_gpu_init not called");
     if (!tiles || !ppm_body_host || world < 1 || width < 1 || height < 1 || (int64_t)n_max * world < height)
         return fail("rt_gpu_deinterleave_ppm: bad arguments");
@@ -1696,16 +1724,16 @@ int rt_gpu_deinterleave_ppm(const uint8_t* tiles, int world, int n_max, int widt
     const size_t body = (size_t)width * height * 3;
     HostRange* hr = host_range_ready(ppm_body_host, body);
     if (!hr) return fail("rt_gpu_deinterleave_ppm: the buffer is not a registered range of %zu bytes", body);
-    HIP_TRY(hipStreamWaitEvent(g.stream, hr->copied, 0));
+    HIP_TRY(hipStreamWaitEvent(cs, hr->copied, 0));
     if (uint8_t* dst = (uint8_t*)mapped(hr, ppm_body_host)) {
-        HIP_TRY(launch_deinterleave_u8(tiles, world, n_max, width, height, dst, g.stream));
+        HIP_TRY(launch_deinterleave_u8(tiles, world, n_max, width, height, dst, cs));
     } else {
         DevBuf& f8 = g.ppm_stage;
         if (ensure(f8, body)) return RT_FAILURE;
-        HIP_TRY(launch_deinterleave_u8(tiles, world, n_max, width, height, (uint8_t*)f8.p, g.stream));
-        HIP_TRY(hipMemcpyAsync(ppm_body_host, f8.p, body, hipMemcpyDeviceToHost, g.stream));
+        HIP_TRY(launch_deinterleave_u8(tiles, world, n_max, width, height, (uint8_t*)f8.p, cs));
+        HIP_TRY(hipMemcpyAsync(ppm_body_host, f8.p, body, hipMemcpyDeviceToHost, cs));
     }
-    HIP_TRY(hipEventRecord(hr->copied, g.stream));
+    HIP_TRY(hipEventRecord(hr->copied, cs));
     return RT_SUCCESS;
 }
 
@@ -1913,6 +1941,7 @@ void shutdown_ctx() {
         if (fg.exec) (void)hipGraphExecDestroy(fg.exec);
     if (g.aux_go) (void)hipEventDestroy(g.aux_go);
     if (g.aux_done) (void)hipEventDestroy(g.aux_done);
+    if (g.ppm_done) (void)hipEventDestroy(g.ppm_done);
     for (auto& ev : g.ev_default)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& q : g.prof_pool)

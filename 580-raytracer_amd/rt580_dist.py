@@ -182,7 +182,7 @@ class DistFrame:
                 self.last_host = self.host[self.host_i]
                 self.b.rt580.check(self.lib.rt_gpu_deinterleave_ppm(
                     self.tiles[k].data_ptr(), self.world, self.n_max, self.w, self.h,
-                    self._reg[self.host_i][1].ctypes.data), "rt_gpu_deinterleave_ppm")
+                    self._reg[self.host_i][1].ctypes.data, None), "rt_gpu_deinterleave_ppm")
                 self.host_i ^= 1
                 return
             tiles = (self.tiles[k] if self.u8 else self.tiles[k].view(self.t.int16)).view(
@@ -236,6 +236,94 @@ class DistFrame:
 
     def close(self):
         """Unregister rank 0's host buffers (after finish())."""
+        for _, buf in self._reg:
+            self.lib.rt_gpu_host_unregister(buf.ctypes.data)
+        self._reg = []
+
+
+class PipelinedDistFrame:
+    """DistFrame's u8 steady state with each frame's AO phase left running (the
+    GPU backend over RCCL; bench.py's multi-rank step). In DistFrame the compute
+    stream waits for frame N's AO phase before frame N+1's count exchange, so
+    consecutive AO phases cannot overlap; here rt_gpu_shade_rows_ppm puts that
+    wait on an exchange stream instead: the tiles' gather (on a process group of
+    its own -- a second communicator, whose collectives never queue behind the
+    next frame's count exchange) and rank 0's write of the PPM body into
+    registered host memory (rt_gpu_deinterleave_ppm) run there, while the
+    compute stream goes on with the next frame. A ring of R buffer sets; a set
+    is reused once its frame's gather (and write) is done. The library's stream
+    must be torch's current stream (rt_gpu_set_stream)."""
+
+    R = 3
+
+    def __init__(self, backend, dist, torch, height, width, rank, world, device):
+        import numpy as np
+        self.b, self.dist, self.t = backend, dist, torch
+        self.lib, self.rt580 = backend.lib, backend.rt580
+        self.h, self.w, self.rank, self.world, self.device = height, width, rank, world, device
+        self.n_max = n_max_rows(height, world)
+        tile = self.n_max * width * 3
+        R = self.R
+        self.cnt = [torch.zeros(self.n_max, dtype=torch.int32, device=device) for _ in range(R)]
+        self.gathered = [torch.empty(world * self.n_max, dtype=torch.int32, device=device) for _ in range(R)]
+        self.base = [torch.empty(self.n_max, dtype=torch.int64, device=device) for _ in range(R)]
+        self.fb8 = [torch.empty(tile, dtype=torch.uint8, device=device) for _ in range(R)]
+        self.tiles = [torch.empty(world * tile, dtype=torch.uint8, device=device) for _ in range(R)] \
+            if rank == 0 else None
+        self.x = torch.cuda.Stream(device)
+        self.pg = dist.new_group(list(range(world)))
+        self.done = [None] * R  # event on the exchange stream: set k free again
+        self._reg = []
+        if rank == 0:
+            span = (height * width * 3 + 4095) // 4096 * 4096
+            for _ in range(R):
+                raw = np.zeros(span + 4096, dtype=np.uint8)
+                off = (-raw.ctypes.data) % 4096
+                buf = raw[off:off + span]
+                self.rt580.check(self.lib.rt_gpu_host_register(buf.ctypes.data, span), "rt_gpu_host_register")
+                self._reg.append((raw, buf))
+        self.i = 0
+        self.last_host = None
+
+    def render(self):
+        t, k = self.t, self.i
+        ctypes_ = ctypes
+        cur = t.cuda.current_stream(self.device)
+        if self.done[k] is not None:  # set k's previous frame: gathered (and written) before its buffers are reused
+            cur.wait_event(self.done[k])
+        pc = self.b._p(self.rank, self.world)
+        self.rt580.check(self.lib.rt_gpu_count_rows(ctypes_.byref(pc), self.cnt[k].data_ptr()), "rt_gpu_count_rows")
+        self.dist.all_gather_into_tensor(self.gathered[k], self.cnt[k])
+        self.b.row_bases(self.gathered[k], self.rank, self.world, self.base[k])
+        self.rt580.check(self.lib.rt_gpu_shade_rows_ppm(ctypes_.byref(pc), self.base[k].data_ptr(),
+                                                        self.fb8[k].data_ptr(), ctypes_.c_void_p(self.x.cuda_stream)),
+                         "rt_gpu_shade_rows_ppm")
+        with t.cuda.stream(self.x):
+            if self.rank == 0:
+                work = self.dist.gather(self.fb8[k], gather_list=list(self.tiles[k].chunk(self.world)), dst=0,
+                                        group=self.pg, async_op=True)
+                work.wait()  # the exchange stream waits for the gather
+                buf = self._reg[k][1]
+                self.rt580.check(self.lib.rt_gpu_deinterleave_ppm(
+                    self.tiles[k].data_ptr(), self.world, self.n_max, self.w, self.h, buf.ctypes.data,
+                    ctypes_.c_void_p(self.x.cuda_stream)), "rt_gpu_deinterleave_ppm")
+                self.last_host = t.from_numpy(buf[:self.h * self.w * 3]).view(self.h, self.w, 3)
+            else:
+                work = self.dist.gather(self.fb8[k], dst=0, group=self.pg, async_op=True)
+                work.wait()
+            ev = t.cuda.Event()
+            ev.record(self.x)
+            self.done[k] = ev
+        self.i = (k + 1) % self.R
+
+    def finish(self):
+        """Complete every frame in flight; rank 0: the last frame's PPM body
+        (H, W, 3) uint8 in page-locked host memory."""
+        self.rt580.check(self.lib.rt_gpu_synchronize(), "rt_gpu_synchronize")
+        self.t.cuda.synchronize(self.device)
+        return self.last_host if self.rank == 0 else None
+
+    def close(self):
         for _, buf in self._reg:
             self.lib.rt_gpu_host_unregister(buf.ctypes.data)
         self._reg = []

@@ -184,7 +184,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     if ctx.dist_on:
         backend = dist_mod.GpuRows(rt580, params, torch, ctx.device)
         if ctx.args.backend == "nccl":
-            dframe = dist_mod.DistFrame(backend, ctx.dist, torch, H, W, ctx.rank, ctx.world, ctx.device)
+            dframe = dist_mod.PipelinedDistFrame(backend, ctx.dist, torch, H, W, ctx.rank, ctx.world, ctx.device)
     import numpy as np
     if ctx.multi:
         devs = (ctypes.c_int * ctx.multi)(*ctx.devices)
@@ -348,8 +348,9 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
                  "three frames in flight (each frame's gather and D2H overlap the next frames' kernels)"
                  % ("rt_gpu_render_multi_async (tiles mapped to bytes on their devices, gathered and de-interleaved "
                     "on device 0)" if ctx.multi else "rt_gpu_render_async_ppm", RING) if not ctx.dist_on else
-                 "one frame on every rank; rank 0 gathers the u8 tiles, de-interleaves them and copies the PPM body "
-                 "into page-locked host memory (rt580_dist.DistFrame)"),
+                 "one frame on every rank; rank 0 gathers the u8 tiles and writes the PPM body into page-locked host "
+                 "memory (rt580_dist.PipelinedDistFrame: each frame's gather and write on an exchange stream, the "
+                 "next frame's count exchange and AO phase going ahead)"),
         "step_kind": step_kind,
         "scene_upload_s": round(upload_s, 3),
         "host_enqueue_ms_per_step": round(host_s / steps * 1e3, 4),

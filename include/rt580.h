@@ -232,7 +232,15 @@ int rt_gpu_render_multi_async(const rt_render_params* params, uint8_t* ppm_body_
  * library's stream, after any earlier write into the same range. The
  * per-process driver's last step (rt580_dist.DistFrame). */
 int rt_gpu_deinterleave_ppm(const uint8_t* tiles, int world, int n_max, int width, int height,
-                            uint8_t* ppm_body_host);
+                            uint8_t* ppm_body_host, void* stream /* hipStream_t; NULL: the library's stream */);
+/* rt_gpu_shade_rows with the rows' PPM bytes (FlushFrameBufferToPPM's gamma
+ * mapping) written to tile_u8_device, and the wait for the frame placed on
+ * done_stream (a hipStream_t) instead of the caller's stream: the caller's
+ * stream goes on with the next frame's count and exchange while this frame's
+ * AO phase runs, and the consumers of the tile (the gather, on done_stream)
+ * wait for it. NULL done_stream: the caller's stream waits, as rt_gpu_shade_rows. */
+int rt_gpu_shade_rows_ppm(const rt_render_params* params, const uint64_t* row_base_device, uint8_t* tile_u8_device,
+                          void* done_stream);
 /* Visible HIP devices (0 without a GPU). */
 int rt_gpu_device_count(void);
 /* FlushFrameBufferToPPM's pixel mapping on the device (Raytracer.cpp:812-818):

@@ -70,3 +70,31 @@ def test_dist_frame_rccl_one_rank_matches_reference(rccl_one_rank, u8):
         df.render()
     assert sha(df.finish()) == want
     rt.close()
+
+
+def test_pipelined_dist_frame_rccl_one_rank_matches_reference(rccl_one_rank):
+    """PipelinedDistFrame (bench.py's multi-rank step): each frame's gather and
+    rank 0's host write on the exchange stream and a second communicator, the
+    next frame's count exchange and AO phase going ahead -- frames one at a
+    time, then six queued back to back (two turns of the buffer ring): the PPM
+    body equals the reference's 1080p render."""
+    torch, dist, device, rt580, lib = rccl_one_rank
+    w, h = 1920, 1080
+    want = next(e for e in helpers.golden_entries(False) if e["name"] == "config2_1080p_d4_ao64")["sha256"]
+    rt, params = _setup(rt580, lib, w, h)
+    dm = helpers.rt580_dist()
+    df = dm.PipelinedDistFrame(dm.GpuRows(rt580, params, torch, device), dist, torch, h, w, 0, 1, device)
+
+    def sha(frame):
+        return helpers.sha256(b"P6\n%d %d\n255\n" % (w, h) + frame.numpy().tobytes())
+
+    try:
+        for _ in range(2):
+            df.render()
+            assert sha(df.finish()) == want
+        for _ in range(6):
+            df.render()
+        assert sha(df.finish()) == want
+    finally:
+        df.close()
+    rt.close()

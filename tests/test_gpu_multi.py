@@ -252,12 +252,12 @@ def test_deinterleave_ppm_into_registered_memory(world, w, h):
     rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "host_register")
     try:
         for k in (0, 1):
-            rt580.check(lib.rt_gpu_deinterleave_ppm(dev[k].data_ptr(), world, n_max, w, h, buf.ctypes.data),
+            rt580.check(lib.rt_gpu_deinterleave_ppm(dev[k].data_ptr(), world, n_max, w, h, buf.ctypes.data, None),
                         "rt_gpu_deinterleave_ppm")
         rt580.check(lib.rt_gpu_synchronize(), "synchronize")
         torch.cuda.synchronize()
         assert np.array_equal(buf, want[1])
         plain = np.zeros(w * h * 3, dtype=np.uint8)
-        assert lib.rt_gpu_deinterleave_ppm(dev[0].data_ptr(), world, n_max, w, h, plain.ctypes.data) != 0
+        assert lib.rt_gpu_deinterleave_ppm(dev[0].data_ptr(), world, n_max, w, h, plain.ctypes.data, None) != 0
     finally:
         lib.rt_gpu_host_unregister(buf.ctypes.data)
