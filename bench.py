@@ -263,7 +263,8 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
             torch.cuda.synchronize()
             log("%s: warmup step %d done" % (name, i))
     torch.cuda.synchronize()
-    rt580.check(lib.rt_gpu_profile(1), "rt_gpu_profile")
+    if not ctx.args.no_live_timing:
+        rt580.check(lib.rt_gpu_profile(1), "rt_gpu_profile")
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -698,6 +699,9 @@ def main():
                          "interleaved split; RNG bases from an untimed full-frame count), for huge frames and "
                          "the per-rank shares of a split")
     ap.add_argument("--row-rank", type=int, default=0, help="R of --row-sample")
+    ap.add_argument("--no-live-timing", action="store_true",
+                    help="no HIP-event timing of the frames' phases and AO launches inside the timed region (A/B of "
+                         "its cost; the roofline then has only the isolated timing)")
     ap.add_argument("--step", default="ppm", choices=["ppm", "host16", "device"],
                     help="one process, N = 1 (A/B of the step's end; the default is the contract's): ppm = the PPM "
                          "body in host memory (rt_gpu_render_async_ppm), host16 = the int16 framebuffer in host "
