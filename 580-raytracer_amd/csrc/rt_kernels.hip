@@ -1294,6 +1294,105 @@ ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
     ao_body<V>(S, F, W, b, e);
 }
 
+// bvh4_any_near_budget_state in speculative while-while form (Aila & Laine's
+// postponed leaves): the wave descends until every lane holds a leaf; a lane
+// that reaches one first keeps it and goes on descending from its stack in the
+// node iterations the wave spends on the others, so its next leaf is found in
+// steps that would otherwise idle; the leaf phase then tests the held leaf and,
+// when the lane's current entry is a leaf too, that one. The same nodes and
+// leaves as the ordinary walk, visited in another order and stopped at the
+// first hit: the same boolean. tools/simd_sim.cpp (100k field, budget 4): wave
+// node iterations 45.5 -> 32.8, leaf tests 7.8 -> 8.8. Needs the whole wave
+// (a vote ends the node phase): inactive lanes pass live = false.
+// 1 hit, 0 no hit, -1 undecided after `budget` leaf tests: the stack [0, sp) and
+// the entry (c, n) next (n > 0 a leaf) are the walk's state for ao_late_kernel.
+// bvh4_any_spec_walk: the walk from the state (stack [0, sp), entry (c, n)),
+// as bvh4_any_near_resume_budget; bvh4_any_spec_budget_state: from the root,
+// after the brute list, as bvh4_any_near_budget_state.
+template <class STK>
+__device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, bool live, int& sp,
+                                  int32_t& c, int32_t& n) {
+    if (!live) return 0;
+    int r = 0;
+    const SlabRay sr = slab_ray(V, o, d);
+    int32_t pc = 0, pn = 0;  // the held leaf (pn > 0)
+    int visits = 0;
+    while (live) {
+        for (;;) {  // node phase
+            if (pn == 0 && n > 0) {
+                pc = c;
+                pn = n;
+                if (!bvh4_pop(stk, sp, c, n)) n = -1;
+            }
+            if (!__any(pn == 0 && n == 0)) break;  // every lane holds a leaf or has none left
+            if (n == 0) {  // one node iteration (speculative when the lane holds a leaf)
+                Node4 nd;
+                float t[4];
+                bool ok[4];
+                node4_slab(V.nodes4 + c, sr, t, ok, nd.link);
+#pragma unroll
+                for (int j = 0; j < 4; j++) ok[j] = (nd.link[j] != 0xffffffffu) & ok[j];
+                int best = -1;
+                float bt = INFINITY;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (ok[j] & ((best < 0) | (t[j] < bt))) {
+                        best = j;
+                        bt = t[j];
+                    }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    stk.put(sp, nd.link[j]);
+                    sp += (ok[j] & (j != best)) ? 1 : 0;
+                }
+                if (best >= 0) {
+                    const uint32_t e = best == 0 ? nd.link[0] : best == 1 ? nd.link[1] : best == 2 ? nd.link[2] : nd.link[3];
+                    c = (int32_t)(e & 0x7ffffffu);
+                    n = (int32_t)(e >> 27);
+                } else if (!bvh4_pop(stk, sp, c, n)) {
+                    n = -1;
+                }
+            }
+        }
+        // leaf phase
+        bool h = false;
+        if (pn > 0) {
+            h = bvh4_leaf_hit(V, o, d, INFINITY, pc, pn);
+            visits++;
+            pn = 0;
+            if (!h && n > 0 && visits < budget) {  // the current entry is a leaf too
+                h = bvh4_leaf_hit(V, o, d, INFINITY, c, n);
+                visits++;
+                if (!bvh4_pop(stk, sp, c, n)) n = -1;
+            }
+        }
+        if (h) {
+            r = 1;
+            live = false;
+        } else if (n < 0) {
+            r = 0;
+            live = false;
+        } else if (visits >= budget) {
+            r = -1;
+            live = false;
+        }
+    }
+    return r;
+}
+
+template <class STK>
+__device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, bool live,
+                                          int& sp, int32_t& c, int32_t& n) {
+    sp = 0;
+    c = 0;
+    n = 0;  // root (internal); n < 0: nothing left on this lane
+    if (live)
+        for (int k = 0; k < V.n_brute; k++)
+            if (prim_hit_within(V.all[V.brute[k]], o, d, INFINITY)) return 1;
+    if (live && (!V.has_tree || dir_zero(d))) live = false;
+    return bvh4_any_spec_walk(V, o, d, stk, budget, live, sp, c, n);
+}
+
 // XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs
 // (MI355X_MICROARCH.md, workgroup dispatch: b and b + 8 share an XCD and its
 // 4 MiB L2), so consecutive blocks of work land on 8 different L2s. With
@@ -1319,7 +1418,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
 // BUDGET > 0: a lane gives up after BUDGET leaf visits; its item goes to
 // W.ao_late (ao_late_kernel re-runs the full query), so a wave is not held by
 // its few long traversals (tools/simd_sim.cpp "budget").
-template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0>
+// SPEC: the budgeted walk in speculative while-while form (bvh4_any_spec_budget_state).
+template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0, int SPEC = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
     __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
@@ -1401,7 +1501,8 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
             const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
             int sp = 0;
             int32_t wc = 0, wn = 0;
-            const int r = flag == 1u ? bvh4_any_near_budget_state(S.bv, o, d, stk, BUDGET, sp, wc, wn) : 0;
+            const int r = SPEC ? bvh4_any_spec_budget_state(S.bv, o, d, stk, BUDGET, flag == 1u, sp, wc, wn)
+                          : flag == 1u ? bvh4_any_near_budget_state(S.bv, o, d, stk, BUDGET, sp, wc, wn) : 0;
             hit = r > 0;
             late = r < 0;
             const uint64_t lm = __ballot(late);
@@ -1613,7 +1714,8 @@ ao_trace_refill_kernel(DevScene S, DevWork W, uint64_t n) {
 // (RT580_AO_BUDGET2, A/B); skipped when queue 0 fills more than half the buffer.
 // REREAD = 0 (diagnostic builds only, RT580_LATE_REREAD=0): the round-4 form
 // that queues the ray from the registers of the traversal (see below).
-template <int WPE, int LDS_D, int BUDGET2 = 0, int SRC = 0, int REREAD = 1>
+// SPEC (no second budget): the walks in speculative while-while form.
+template <int WPE, int LDS_D, int BUDGET2 = 0, int SRC = 0, int REREAD = 1, int SPEC = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_late_kernel(DevScene S, DevWork W) {
     __shared__ uint32_t lstk[LDS_D][TB];
@@ -1675,6 +1777,13 @@ ao_late_kernel(DevScene S, DevWork W) {
                     }
                 }
             }
+        } else if (SPEC) {  // one walk for the saved and the restarted rays (the wave votes together)
+            bool go = live, pre = false;
+            if (live && !saved) {  // from the root, after the brute list
+                for (int t = 0; t < S.bv.n_brute && !pre; t++) pre = prim_hit_within(S.bv.all[S.bv.brute[t]], o, d, INFINITY);
+                go = !pre && S.bv.has_tree && !dir_zero(d);
+            }
+            hit = pre || bvh4_any_spec_walk(S.bv, o, d, stk, 1 << 30, go, sp, wc, wn) > 0;
         } else if (saved) {  // the saved walk, continued (same boolean)
             hit = bvh4_any_near_resume(S.bv, o, d, stk, sp, wc, wn);
         } else {
@@ -2038,6 +2147,17 @@ static int ao_sort() {
 // RT580_AO_BUDGET: leaf visits per AO ray in ao_trace_kernel before the ray is
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
+// RT580_AO_SPEC: the AO walks in speculative while-while form, bit 0 the
+// budgeted trace pass (budget 4), bit 1 the late pass
+static int ao_spec() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_AO_SPEC");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
 // RT580_AO_REFILL: persistent-lane forms, bit 0 the AO trace (ao_trace_refill_kernel),
 // bit 1 the late pass (ao_late_refill_kernel)
 static int ao_refill() {
@@ -4351,6 +4471,18 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                         else
                             hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 16>), g, dim3(TB), 0, s, S, W, e1 - b);
                     }
+                    else if ((ao_spec() & 1) && bu >= 3) {  // budgets 3, 4, 6 (5-6), 8 (7+)
+                        const dim3 g(grid_for(e1 - b, 16384));
+                        const uint32_t ns = (uint32_t)F.ao_samples;
+                        if (bu == 3)
+                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 3, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
+                        else if (bu <= 4)
+                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
+                        else if (bu <= 6)
+                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 6, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
+                        else
+                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 8, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
+                    }
                     else if (bu <= 2)
                         hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 2>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
                                            s, S, W, (uint32_t)F.ao_samples, e1 - b);
@@ -4380,6 +4512,8 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
 #endif
                         if (late_wpe() == 8)
                             hipLaunchKernelGGL((ao_late_kernel<8, 16>), dim3(4096), dim3(TB), 0, s, S, W);
+                        else if (ao_spec() & 2)
+                            hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 0, 1, 1>), dim3(4096), dim3(TB), 0, s, S, W);
                         else
                             hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
                     }

@@ -276,6 +276,118 @@ int main(int argc, char** argv) {
                     (c1n + c1t + cSn + cSt) / (base_n + base_t), c1n + c1t + cRn + cRt,
                     (c1n + c1t + cRn + cRt) / (base_n + base_t));
     }
+    // Speculative while-while (postponed leaves): a lane that reaches a leaf
+    // while others still descend keeps it and goes on descending from its stack,
+    // so the wave's idle node iterations advance its next leaf; the leaf phase
+    // then tests the postponed leaf (and the current entry, if it is a leaf too).
+    // Lane op sequences: 0 = a node iteration, k > 0 = a leaf of k tests (the
+    // last op when it hits). Lock-step cost = node iterations + test iterations
+    // (per iteration, the slowest lane), with and without a leaf budget K.
+    {
+        std::mt19937 r5(argc > 4 ? std::atoi(argv[4]) : 580);
+        std::vector<std::vector<int>> ops;
+        ops.reserve(waves * 64);
+        for (long w = 0; w < waves; w++) {
+            const rt_prim& T = P[tris[r5() % tris.size()]];
+            float u = U(r5), v = U(r5);
+            if (u + v > 1) { u = 1 - u; v = 1 - v; }
+            const rv3 p0 = ld3(T.p0), p1 = ld3(T.p1), p2 = ld3(T.p2), N = v3_normalize(ld3(T.nrm));
+            const rv3 hp = v3_add(p0, v3_add(v3_scale(v3_sub(p1, p0), u), v3_scale(v3_sub(p2, p0), v)));
+            for (int l = 0; l < 64; l++) {
+                const float z = U(r5) * 2 - 1, a = U(r5) * 6.2831853f, r = std::sqrt(1 - z * z);
+                rv3 d = v3_normalize(v3(r * std::cos(a), r * std::sin(a), z));
+                if (!(v3_dot(d, N) > 0.0f)) d = v3_neg(d);
+                const rv3 o = v3_add(hp, v3_scale(d, 0.2f));
+                std::vector<Step> st;
+                trace(V, o, d, st);
+                std::vector<int> q;
+                for (const Step& x : st) {
+                    for (int k = 0; k < x.nodes; k++) q.push_back(0);
+                    if (x.tris) q.push_back(x.tris);
+                }
+                ops.push_back(q);
+            }
+        }
+        for (int K : {1 << 30, 4}) {
+            double an = 0, at = 0, bn = 0, bt = 0, spec_nodes = 0;
+            for (size_t w0 = 0; w0 < ops.size(); w0 += 64) {
+                // (A) while-while
+                {
+                    std::vector<size_t> pos(64, 0);
+                    std::vector<int> leaves(64, 0);
+                    for (;;) {
+                        bool any = false;
+                        for (int l = 0; l < 64; l++) any |= pos[l] < ops[w0 + l].size() && leaves[l] < K;
+                        if (!any) break;
+                        int mn = 0, mt = 0;
+                        for (int l = 0; l < 64; l++) {
+                            const std::vector<int>& q = ops[w0 + l];
+                            if (leaves[l] >= K) continue;
+                            int c = 0;
+                            while (pos[l] < q.size() && q[pos[l]] == 0) { pos[l]++; c++; }
+                            mn = std::max(mn, c);
+                        }
+                        for (int l = 0; l < 64; l++) {
+                            const std::vector<int>& q = ops[w0 + l];
+                            if (leaves[l] >= K || pos[l] >= q.size()) continue;
+                            mt = std::max(mt, q[pos[l]]);
+                            pos[l]++;
+                            leaves[l]++;
+                        }
+                        an += mn;
+                        at += mt;
+                    }
+                }
+                // (B) speculative
+                {
+                    std::vector<size_t> pos(64, 0);
+                    std::vector<int> post(64, 0), leaves(64, 0);
+                    auto live = [&](int l) { return leaves[l] < K && (post[l] > 0 || pos[l] < ops[w0 + l].size()); };
+                    for (;;) {
+                        bool any = false;
+                        for (int l = 0; l < 64; l++) any |= live(l);
+                        if (!any) break;
+                        // postpone leading leaves
+                        for (int l = 0; l < 64; l++) {
+                            const std::vector<int>& q = ops[w0 + l];
+                            if (live(l) && !post[l] && pos[l] < q.size() && q[pos[l]] > 0) post[l] = q[pos[l]++];
+                        }
+                        for (;;) {  // node iterations until every live lane holds a leaf
+                            bool need = false;
+                            for (int l = 0; l < 64; l++) need |= live(l) && !post[l];
+                            if (!need) break;
+                            for (int l = 0; l < 64; l++) {
+                                const std::vector<int>& q = ops[w0 + l];
+                                if (!live(l) || pos[l] >= q.size() || q[pos[l]] > 0) continue;
+                                pos[l]++;
+                                if (post[l]) spec_nodes++;
+                                if (!post[l] && pos[l] < q.size() && q[pos[l]] > 0) post[l] = q[pos[l]++];
+                            }
+                            bn++;
+                        }
+                        int mt = 0;
+                        for (int l = 0; l < 64; l++) {
+                            if (!live(l) || !post[l]) continue;
+                            const std::vector<int>& q = ops[w0 + l];
+                            int t = post[l];
+                            post[l] = 0;
+                            leaves[l]++;
+                            if (leaves[l] < K && pos[l] < q.size() && q[pos[l]] > 0) {  // the current entry is a leaf too
+                                t += q[pos[l]++];
+                                leaves[l]++;
+                            }
+                            mt = std::max(mt, t);
+                        }
+                        bt += mt;
+                    }
+                }
+            }
+            const double nw = ops.size() / 64.0;
+            std::printf("while-while%s: nodes %.1f tests %.1f per wave | speculative: nodes %.1f tests %.1f "
+                        "(speculative node steps per lane %.2f)\n", K < (1 << 30) ? " budget 4" : "", an / nw,
+                        at / nw, bn / nw, bt / nw, spec_nodes / ops.size());
+        }
+    }
     const double R = waves * 64.0;
     std::printf("rays=%.0f hit=%.3f per ray: nodes=%.2f tris=%.2f steps=%.2f | per wave (lock-step): nodes=%.1f tris=%.1f "
                 "steps=%.1f | node eff=%.3f tri eff=%.3f\n", R, hits / R, lane_nodes / R, lane_tris / R, lane_steps / R,
