@@ -2148,12 +2148,13 @@ static int ao_sort() {
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
 // RT580_AO_SPEC: the AO walks in speculative while-while form, bit 0 the
-// budgeted trace pass (budget 4), bit 1 the late pass
+// budgeted trace pass, bit 1 the late pass (default both: north-star frame
+// 37.5 -> 34.3 ms, Cornell 59.6 -> 54.7 ms; profiles/r05/ab/spec*)
 static int ao_spec() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_AO_SPEC");
-        v = e ? atoi(e) : 0;
+        v = e ? atoi(e) : 3;
     }
     return v;
 }
