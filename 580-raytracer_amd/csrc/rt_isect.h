@@ -615,6 +615,14 @@ struct ArrStack {
     uint32_t* a;
     RTM_HDM void put(int i, uint32_t v) const { a[i] = v; }
     RTM_HDM uint32_t get(int i) const { return a[i]; }
+    RTM_HDM uint32_t get_lds_first(int i) const { return a[i]; }
+    RTM_HDM void push4(int& sp, const uint32_t v[4], const bool take[4]) const {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            a[sp] = v[j];
+            sp += take[j] ? 1 : 0;
+        }
+    }
 };
 // ... or (device) its first D entries in LDS, one column per lane (stride
 // TB: lanes hit consecutive banks), the rest in a per-lane array.
@@ -627,6 +635,37 @@ struct LdsStack {
         else a[i - D] = v;
     }
     RTM_HDM uint32_t get(int i) const { return i < D ? l[i * STRIDE] : a[i - D]; }
+    // get() as an LDS read that always issues plus a private-memory read only
+    // for entries past D (the compiler otherwise selects the address space per
+    // lane and emits a flat load, which waits on both memory counters)
+    RTM_HDM uint32_t get_lds_first(int i) const {
+        uint32_t e = l[(i < D ? i : D - 1) * STRIDE];
+#ifdef __HIP_DEVICE_COMPILE__
+        asm volatile("" : "+v"(e));  // keeps the two loads apart (no address select)
+#endif
+        if (i >= D) e = a[i - D];
+        return e;
+    }
+    // the node step's four pushes (v[j] written at the top, the top raised when
+    // take[j]): one test of the depth instead of one per entry
+    RTM_HDM void push4(int& sp, const uint32_t v[4], const bool take[4]) const {
+        if (sp + 4 <= D) {
+            uint32_t* p = l + sp * STRIDE;
+            int k = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                p[k * STRIDE] = v[j];
+                k += take[j] ? 1 : 0;
+            }
+            sp += k;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                put(sp, v[j]);
+                sp += take[j] ? 1 : 0;
+            }
+        }
+    }
 };
 
 template <class STK>

@@ -1306,6 +1306,16 @@ ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
 // (a vote ends the node phase): inactive lanes pass live = false.
 // 1 hit, 0 no hit, -1 undecided after `budget` leaf tests: the stack [0, sp) and
 // the entry (c, n) next (n > 0 a leaf) are the walk's state for ao_late_kernel.
+template <class STK>
+__device__ __forceinline__ bool spec_pop(const STK& stk, int& sp, int32_t& c, int32_t& n) {
+    if (sp == 0) return false;
+    sp--;
+    const uint32_t e = stk.get_lds_first(sp);
+    c = (int32_t)(e & 0x7ffffffu);
+    n = (int32_t)(e >> 27);
+    return true;
+}
+
 // bvh4_any_spec_walk: the walk from the state (stack [0, sp), entry (c, n)),
 // as bvh4_any_near_resume_budget; bvh4_any_spec_budget_state: from the root,
 // after the brute list, as bvh4_any_near_budget_state.
@@ -1322,7 +1332,7 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
             if (pn == 0 && n > 0) {
                 pc = c;
                 pn = n;
-                if (!bvh4_pop(stk, sp, c, n)) n = -1;
+                if (!spec_pop(stk, sp, c, n)) n = -1;
             }
             if (!__any(pn == 0 && n == 0)) break;  // every lane holds a leaf or has none left
             if (n == 0) {  // one node iteration (speculative when the lane holds a leaf)
@@ -1340,16 +1350,15 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
                         best = j;
                         bt = t[j];
                     }
+                bool take[4];
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    stk.put(sp, nd.link[j]);
-                    sp += (ok[j] & (j != best)) ? 1 : 0;
-                }
+                for (int j = 0; j < 4; j++) take[j] = ok[j] & (j != best);
+                stk.push4(sp, nd.link, take);
                 if (best >= 0) {
                     const uint32_t e = best == 0 ? nd.link[0] : best == 1 ? nd.link[1] : best == 2 ? nd.link[2] : nd.link[3];
                     c = (int32_t)(e & 0x7ffffffu);
                     n = (int32_t)(e >> 27);
-                } else if (!bvh4_pop(stk, sp, c, n)) {
+                } else if (!spec_pop(stk, sp, c, n)) {
                     n = -1;
                 }
             }
@@ -1363,7 +1372,7 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
             if (!h && n > 0 && visits < budget) {  // the current entry is a leaf too
                 h = bvh4_leaf_hit(V, o, d, INFINITY, c, n);
                 visits++;
-                if (!bvh4_pop(stk, sp, c, n)) n = -1;
+                if (!spec_pop(stk, sp, c, n)) n = -1;
             }
         }
         if (h) {
