@@ -672,7 +672,7 @@ template <class STK>
 RTM_HD bool bvh4_pop(const STK& stk, int& sp, int32_t& c, int32_t& n) {
     if (sp == 0) return false;
     sp--;
-    const uint32_t e = stk.get(sp);
+    const uint32_t e = stk.get_lds_first(sp);
     c = (int32_t)(e & 0x7ffffffu);
     n = (int32_t)(e >> 27);
     return true;
@@ -698,11 +698,10 @@ RTM_HD bool bvh4_descend(const BvhView& V, const SlabRay& sr, float tmax, const 
                 best = j;
                 bt = t[j];
             }
+        bool take[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            stk.put(sp, nd.link[j]);
-            sp += (ok[j] & (j != best)) ? 1 : 0;
-        }
+        for (int j = 0; j < 4; j++) take[j] = ok[j] & (j != best);
+        stk.push4(sp, nd.link, take);
         if (best >= 0) {
             const uint32_t e = best == 0 ? nd.link[0] : best == 1 ? nd.link[1] : best == 2 ? nd.link[2] : nd.link[3];
             c = (int32_t)(e & 0x7ffffffu);
@@ -860,12 +859,16 @@ RTM_HD bool bvh4_closest_near_s(const BvhView& V, rv3 o, rv3 d, Hit& h, const ST
                     best = j;
                     bt = t[j];
                 }
+            bool take[4];
+            uint32_t tb[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                stk.put(sp, nd.link[j]);
-                tstk.put(sp, rt_f32_bits(t[j]));
-                sp += (ok[j] & (j != best)) ? 1 : 0;
+                take[j] = ok[j] & (j != best);
+                tb[j] = rt_f32_bits(t[j]);
             }
+            int sp2 = sp;
+            stk.push4(sp2, nd.link, take);
+            tstk.push4(sp, tb, take);
             if (best >= 0) {
                 const uint32_t e = best == 0 ? nd.link[0] : best == 1 ? nd.link[1] : best == 2 ? nd.link[2] : nd.link[3];
                 c = (int32_t)(e & 0x7ffffffu);
@@ -875,8 +878,8 @@ RTM_HD bool bvh4_closest_near_s(const BvhView& V, rv3 o, rv3 d, Hit& h, const ST
             have = false;
             while (sp > 0) {
                 sp--;
-                if (found && rt_bits_f32(tstk.get(sp)) > h.t) continue;
-                const uint32_t e = stk.get(sp);
+                if (found && rt_bits_f32(tstk.get_lds_first(sp)) > h.t) continue;
+                const uint32_t e = stk.get_lds_first(sp);
                 c = (int32_t)(e & 0x7ffffffu);
                 n = (int32_t)(e >> 27);
                 have = true;
