@@ -1319,13 +1319,18 @@ __device__ __forceinline__ bool spec_pop(const STK& stk, int& sp, int32_t& c, in
 // bvh4_any_spec_walk: the walk from the state (stack [0, sp), entry (c, n)),
 // as bvh4_any_near_resume_budget; bvh4_any_spec_budget_state: from the root,
 // after the brute list, as bvh4_any_near_budget_state.
-template <class STK>
+// HOLD2: a lane holds up to two leaves (the second taken while it goes on
+// descending with one held); the leaf phase tests them in order, then the
+// current entry if it is a leaf. tools/simd_sim.cpp, 100k field, budget 4: wave
+// node iterations 32.6 -> 29.2, leaf tests 8.8 -> 9.1.
+template <int HOLD2 = 0, class STK>
 __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, bool live, int& sp,
                                   int32_t& c, int32_t& n) {
     if (!live) return 0;
     int r = 0;
     const SlabRay sr = slab_ray(V, o, d);
     int32_t pc = 0, pn = 0;  // the held leaf (pn > 0)
+    int32_t qc = 0, qn = 0;  // the second held leaf (HOLD2)
     int visits = 0;
     while (live) {
         for (;;) {  // node phase
@@ -1334,8 +1339,13 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
                 pn = n;
                 if (!spec_pop(stk, sp, c, n)) n = -1;
             }
+            if (HOLD2 && qn == 0 && pn > 0 && n > 0) {
+                qc = c;
+                qn = n;
+                if (!spec_pop(stk, sp, c, n)) n = -1;
+            }
             if (!__any(pn == 0 && n == 0)) break;  // every lane holds a leaf or has none left
-            if (n == 0) {  // one node iteration (speculative when the lane holds a leaf)
+            if (n == 0 && (!HOLD2 || qn == 0)) {  // one node iteration (speculative when the lane holds a leaf)
                 Node4 nd;
                 float t[4];
                 bool ok[4];
@@ -1369,7 +1379,12 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
             h = bvh4_leaf_hit(V, o, d, INFINITY, pc, pn);
             visits++;
             pn = 0;
-            if (!h && n > 0 && visits < budget) {  // the current entry is a leaf too
+            if (HOLD2 && !h && qn > 0 && visits < budget) {
+                h = bvh4_leaf_hit(V, o, d, INFINITY, qc, qn);
+                visits++;
+                qn = 0;
+            }
+            if (!h && n > 0 && (!HOLD2 || qn == 0) && visits < budget) {  // the current entry is a leaf too
                 h = bvh4_leaf_hit(V, o, d, INFINITY, c, n);
                 visits++;
                 if (!spec_pop(stk, sp, c, n)) n = -1;
@@ -1378,10 +1393,20 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
         if (h) {
             r = 1;
             live = false;
-        } else if (n < 0) {
+        } else if (n < 0 && (!HOLD2 || qn == 0)) {
             r = 0;
             live = false;
         } else if (visits >= budget) {
+            if (HOLD2 && qn > 0) {  // the untested held leaf back into the walk's state
+                if (n < 0) {
+                    c = qc;
+                    n = qn;
+                } else {
+                    stk.put(sp, ((uint32_t)qn << 27) | (uint32_t)qc);
+                    sp++;
+                }
+                qn = 0;
+            }
             r = -1;
             live = false;
         }
@@ -1389,7 +1414,7 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
     return r;
 }
 
-template <class STK>
+template <int HOLD2 = 0, class STK>
 __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, bool live,
                                           int& sp, int32_t& c, int32_t& n) {
     sp = 0;
@@ -1399,7 +1424,7 @@ __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const 
         for (int k = 0; k < V.n_brute; k++)
             if (prim_hit_within(V.all[V.brute[k]], o, d, INFINITY)) return 1;
     if (live && (!V.has_tree || dir_zero(d))) live = false;
-    return bvh4_any_spec_walk(V, o, d, stk, budget, live, sp, c, n);
+    return bvh4_any_spec_walk<HOLD2>(V, o, d, stk, budget, live, sp, c, n);
 }
 
 // XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs
@@ -1427,7 +1452,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
 // BUDGET > 0: a lane gives up after BUDGET leaf visits; its item goes to
 // W.ao_late (ao_late_kernel re-runs the full query), so a wave is not held by
 // its few long traversals (tools/simd_sim.cpp "budget").
-// SPEC: the budgeted walk in speculative while-while form (bvh4_any_spec_budget_state).
+// SPEC: the budgeted walk in speculative while-while form (bvh4_any_spec_budget_state);
+// 2: holding up to two leaves.
 template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0, int SPEC = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
@@ -1510,7 +1536,7 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
             const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
             int sp = 0;
             int32_t wc = 0, wn = 0;
-            const int r = SPEC ? bvh4_any_spec_budget_state(S.bv, o, d, stk, BUDGET, flag == 1u, sp, wc, wn)
+            const int r = SPEC ? bvh4_any_spec_budget_state<SPEC == 2>(S.bv, o, d, stk, BUDGET, flag == 1u, sp, wc, wn)
                           : flag == 1u ? bvh4_any_near_budget_state(S.bv, o, d, stk, BUDGET, sp, wc, wn) : 0;
             hit = r > 0;
             late = r < 0;
@@ -1792,7 +1818,7 @@ ao_late_kernel(DevScene S, DevWork W) {
                 for (int t = 0; t < S.bv.n_brute && !pre; t++) pre = prim_hit_within(S.bv.all[S.bv.brute[t]], o, d, INFINITY);
                 go = !pre && S.bv.has_tree && !dir_zero(d);
             }
-            hit = pre || bvh4_any_spec_walk(S.bv, o, d, stk, 1 << 30, go, sp, wc, wn) > 0;
+            hit = pre || bvh4_any_spec_walk<SPEC == 2>(S.bv, o, d, stk, 1 << 30, go, sp, wc, wn) > 0;
         } else if (saved) {  // the saved walk, continued (same boolean)
             hit = bvh4_any_near_resume(S.bv, o, d, stk, sp, wc, wn);
         } else {
@@ -2157,7 +2183,7 @@ static int ao_sort() {
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
 // RT580_AO_SPEC: the AO walks in speculative while-while form, bit 0 the
-// budgeted trace pass, bit 1 the late pass (default both: north-star frame
+// budgeted trace pass, bit 1 the late pass, bit 2 two held leaves (default the first two: north-star frame
 // 37.5 -> 34.3 ms, Cornell 59.6 -> 54.7 ms; profiles/r05/ab/spec*)
 static int ao_spec() {
     static int v = -1;
@@ -4484,7 +4510,9 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     else if ((ao_spec() & 1) && bu >= 3) {  // budgets 3, 4, 6 (5-6), 8 (7+)
                         const dim3 g(grid_for(e1 - b, 16384));
                         const uint32_t ns = (uint32_t)F.ao_samples;
-                        if (bu == 3)
+                        if (bu == 4 && (ao_spec() & 4))
+                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4, 2>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
+                        else if (bu == 3)
                             hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 3, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
                         else if (bu <= 4)
                             hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
@@ -4522,6 +4550,8 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
 #endif
                         if (late_wpe() == 8)
                             hipLaunchKernelGGL((ao_late_kernel<8, 16>), dim3(4096), dim3(TB), 0, s, S, W);
+                        else if ((ao_spec() & 6) == 6)
+                            hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 0, 1, 2>), dim3(4096), dim3(TB), 0, s, S, W);
                         else if (ao_spec() & 2)
                             hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 0, 1, 1>), dim3(4096), dim3(TB), 0, s, S, W);
                         else

@@ -360,7 +360,7 @@ def test_render_async_frames_land_in_registered_buffers():
 
 
 
-@pytest.mark.parametrize("late_wpe,refill,spec", [("6", "0", "0"), ("8", "0", "0"), ("6", "3", "0"), ("6", "0", "3")])
+@pytest.mark.parametrize("late_wpe,refill,spec", [("6", "0", "0"), ("8", "0", "0"), ("6", "3", "0"), ("6", "0", "3"), ("6", "0", "7")])
 def test_ao_audit_of_the_product_trace_and_late_passes(tmp_path, late_wpe, refill, spec):
     """Diagnostic build, RT580_AO_VERIFY=1 (rt_kernels.hip ao_audit_*): on the
     north-star frame, every near-query AO ray is answered again by the

@@ -382,10 +382,58 @@ int main(int argc, char** argv) {
                     }
                 }
             }
+            // (C) speculative with up to two held leaves: the node phase ends
+            // when every live lane holds at least one; the leaf phase tests the
+            // held ones in order (stopping at a hit) and the current entry if a leaf
+            double cn2 = 0, ct2 = 0;
+            for (size_t w0 = 0; w0 < ops.size(); w0 += 64) {
+                std::vector<size_t> pos(64, 0);
+                std::vector<std::vector<int>> held(64);
+                std::vector<int> leaves(64, 0);
+                std::vector<bool> done(64, false);
+                auto live = [&](int l) { return !done[l] && leaves[l] < K && (!held[l].empty() || pos[l] < ops[w0 + l].size()); };
+                for (;;) {
+                    bool any = false;
+                    for (int l = 0; l < 64; l++) any |= live(l);
+                    if (!any) break;
+                    for (int l = 0; l < 64; l++) {
+                        const std::vector<int>& q = ops[w0 + l];
+                        while (live(l) && held[l].size() < 2 && pos[l] < q.size() && q[pos[l]] > 0) held[l].push_back(q[pos[l]++]);
+                    }
+                    for (;;) {
+                        bool need = false;
+                        for (int l = 0; l < 64; l++) need |= live(l) && held[l].empty();
+                        if (!need) break;
+                        for (int l = 0; l < 64; l++) {
+                            const std::vector<int>& q = ops[w0 + l];
+                            if (!live(l) || pos[l] >= q.size() || q[pos[l]] > 0) continue;
+                            pos[l]++;
+                            while (held[l].size() < 2 && pos[l] < q.size() && q[pos[l]] > 0) held[l].push_back(q[pos[l]++]);
+                        }
+                        cn2++;
+                    }
+                    int mt = 0;
+                    for (int l = 0; l < 64; l++) {
+                        if (!live(l)) continue;
+                        const std::vector<int>& q = ops[w0 + l];
+                        int t = 0;
+                        for (size_t h = 0; h < held[l].size() && leaves[l] < K; h++) {
+                            t += held[l][h];
+                            leaves[l]++;
+                        }
+                        held[l].clear();
+                        // a hit ends the lane's sequence: its ops are exhausted once the held leaves were the last
+                        if (pos[l] >= q.size()) done[l] = true;
+                        mt = std::max(mt, t);
+                    }
+                    ct2 += mt;
+                }
+            }
             const double nw = ops.size() / 64.0;
             std::printf("while-while%s: nodes %.1f tests %.1f per wave | speculative: nodes %.1f tests %.1f "
-                        "(speculative node steps per lane %.2f)\n", K < (1 << 30) ? " budget 4" : "", an / nw,
-                        at / nw, bn / nw, bt / nw, spec_nodes / ops.size());
+                        "(speculative node steps per lane %.2f) | two held: nodes %.1f tests %.1f\n",
+                        K < (1 << 30) ? " budget 4" : "", an / nw, at / nw, bn / nw, bt / nw, spec_nodes / ops.size(),
+                        cn2 / nw, ct2 / nw);
         }
     }
     const double R = waves * 64.0;
