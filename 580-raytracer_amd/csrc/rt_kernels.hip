@@ -4495,6 +4495,20 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                 else if (twpe == 6 && trace_lds() && so == 2)  // 2048 samples, 8 x 8 cells
                     hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                        (uint32_t)F.ao_samples, e1 - b);
+                else if ((twpe == 7 || twpe == 8) && trace_lds() && so == 3 && ao_budget() == 4 && (ao_spec() & 1)) {
+                    // (A/B) the speculative budget-4 trace at 7 / 8 waves per SIMD (LDS stacks of
+                    // 12 / 8 entries so that the workgroups fit the LDS); the late pass as below
+                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
+                    const dim3 g(grid_for(e1 - b, 16384));
+                    if (twpe == 7)
+                        hipLaunchKernelGGL((ao_trace_kernel<7, 12, 8, 4, 4, 1>), g, dim3(TB), 0, s, S, W,
+                                           (uint32_t)F.ao_samples, e1 - b);
+                    else
+                        hipLaunchKernelGGL((ao_trace_kernel<8, 8, 8, 4, 4, 1>), g, dim3(TB), 0, s, S, W,
+                                           (uint32_t)F.ao_samples, e1 - b);
+                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                    hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 0, 1, 1>), dim3(4096), dim3(TB), 0, s, S, W);
+                }
                 else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
                     if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
                     const int bu = ao_budget();

@@ -33,7 +33,7 @@ const long k01[] = {0, 1, -1};
 const long k23[] = {2, 3, -1};
 const long k234[] = {2, 3, 4, -1};
 const long kSort[] = {0, 1, 2, 3, -1};
-const long kTraceWpe[] = {4, 6, 8, -1};
+const long kTraceWpe[] = {4, 6, 7, 8, -1};
 const long kNearWpe[] = {0, 5, 6, 8, -1};
 const long kLateWpe[] = {6, 8, -1};
 const long kFarMode[] = {0, 1, 2, 3, 4, -1};
