@@ -559,7 +559,11 @@ __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { retu
 // [i0, i1) of the level.
 // SCALAR (small brute-force scenes): wave-uniform scalar scene loads and the
 // division-free sign rejections (tri_test<SIGN>) instead of the LDS tile.
-template <bool BVH, int PHASE, bool SCALAR = false>
+template <class STK, class TSTK>
+__device__ bool bvh4_closest_spec(const BvhView& V, bool live, rv3 o, rv3 d, Hit& h, const STK& stk, const TSTK& tstk);
+
+// TSPEC (PHASE 1, BVH): the near closest-hit walk in speculative form (bvh4_closest_spec).
+template <bool BVH, int PHASE, bool SCALAR = false, bool TSPEC = false>
 __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
                                                    uint32_t i1, int light = 0, int dl = 0, int wave_near = 0) {
     __shared__ rt_prim tile[TILE];
@@ -607,7 +611,11 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             const FarNode root = load_far_node(S.bv.far_nodes, 0);
             const bool brute = active && far_origin(S, o);
             bool nh = false;
-            if (active && !brute) {
+            if (TSPEC && S.bv.nodes4) {  // the whole wave walks (speculative form)
+                uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS], ta[RT_BVH_STACK + 4 - NEAR_LDS];
+                nh = bvh4_closest_spec(S.bv, active && !brute, o, d, h, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa},
+                                       LdsStack<NEAR_LDS, TB>{&ntstk[0][threadIdx.x], ta});
+            } else if (active && !brute) {
                 if (S.bv.nodes4) {
                     uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS], ta[RT_BVH_STACK + 4 - NEAR_LDS];
                     nh = bvh4_closest_near_s(S.bv, o, d, h, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa},
@@ -1427,6 +1435,126 @@ __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const 
     return bvh4_any_spec_walk<HOLD2>(V, o, d, stk, budget, live, sp, c, n);
 }
 
+// bvh4_closest_near_s in speculative while-while form (the closest-hit walk
+// of the trace levels' near phase; see bvh4_any_spec_walk): a lane that holds
+// a leaf goes on descending while the wave's other lanes look for theirs, with
+// the culling bound it has (h.t only shrinks, so a stale bound visits more,
+// never less); the leaf phase tests the held leaf and the current entry if it
+// is a leaf, each skipped when its entry t is already beyond h.t. The result is
+// the lexicographic minimum of (t, primitive) over the same candidates: the
+// order of the tests does not change it (lex_better).
+template <class STK, class TSTK>
+__device__ __forceinline__ bool spec_pop_closest(const STK& stk, const TSTK& tstk, int& sp, int32_t& c, int32_t& n,
+                                                 float& ct, bool found, float ht) {
+    while (sp > 0) {
+        sp--;
+        const float te = rt_bits_f32(tstk.get_lds_first(sp));
+        if (found && te > ht) continue;
+        const uint32_t e = stk.get_lds_first(sp);
+        c = (int32_t)(e & 0x7ffffffu);
+        n = (int32_t)(e >> 27);
+        ct = te;
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ void spec_leaf_closest(const BvhView& V, rv3 o, rv3 d, int32_t c, int32_t n, Hit& h,
+                                                  bool& found) {
+    for (int k = c; k < c + n; k++) {
+        rt_prim P;
+        load_prim(V.prims + k, P);
+        float t, a, b, g;
+        if (tri_test<true, true>(P, o, d, t, a, b, g, found ? h.t : INFINITY)) {
+            const int id = (int)V.ids[k];
+            if (lex_better(t, id, found, h)) {
+                found = true;
+                h.t = t; h.a = a; h.b = b; h.g = g; h.prim = id;
+            }
+        }
+    }
+}
+
+// Whole wave; inactive lanes pass live = false.
+template <class STK, class TSTK>
+__device__ bool bvh4_closest_spec(const BvhView& V, bool live, rv3 o, rv3 d, Hit& h, const STK& stk,
+                                  const TSTK& tstk) {
+    bool found = false;
+    h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
+    if (!live) return false;
+    for (int k = 0; k < V.n_brute; k++) {
+        const int j = (int)V.brute[k];
+        float t, a, b, g;
+        if (prim_test_closest(V.all[j], o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, j, found, h)) {
+            found = true;
+            h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
+        }
+    }
+    if (!V.has_tree || dir_zero(d)) return found;
+    const SlabRay sr = slab_ray(V, o, d);
+    int sp = 0;
+    int32_t c = 0, n = 0;  // root (internal); n < 0: nothing left
+    float ct = 0.0f;       // the current entry's t
+    int32_t pc = 0, pn = 0;
+    float pt = 0.0f;       // the held leaf and its entry t
+    while (live) {
+        for (;;) {  // node phase
+            if (pn == 0 && n > 0) {
+                pc = c;
+                pn = n;
+                pt = ct;
+                if (!spec_pop_closest(stk, tstk, sp, c, n, ct, found, h.t)) n = -1;
+            }
+            if (!__any(pn == 0 && n == 0)) break;
+            if (n == 0) {
+                Node4 nd;
+                float t[4];
+                bool ok[4];
+                node4_slab(V.nodes4 + c, sr, t, ok, nd.link);
+#pragma unroll
+                for (int j = 0; j < 4; j++) ok[j] = (nd.link[j] != 0xffffffffu) & ok[j] & (!found || t[j] <= h.t);
+                int best = -1;
+                float bt = INFINITY;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (ok[j] & ((best < 0) | (t[j] < bt))) {
+                        best = j;
+                        bt = t[j];
+                    }
+                bool take[4];
+                uint32_t tb[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    take[j] = ok[j] & (j != best);
+                    tb[j] = rt_f32_bits(t[j]);
+                }
+                int sp2 = sp;
+                stk.push4(sp2, nd.link, take);
+                tstk.push4(sp, tb, take);
+                if (best >= 0) {
+                    const uint32_t e = best == 0 ? nd.link[0] : best == 1 ? nd.link[1] : best == 2 ? nd.link[2] : nd.link[3];
+                    c = (int32_t)(e & 0x7ffffffu);
+                    n = (int32_t)(e >> 27);
+                    ct = bt;
+                } else if (!spec_pop_closest(stk, tstk, sp, c, n, ct, found, h.t)) {
+                    n = -1;
+                }
+            }
+        }
+        // leaf phase
+        if (pn > 0) {
+            if (!(found && pt > h.t)) spec_leaf_closest(V, o, d, pc, pn, h, found);
+            pn = 0;
+            if (n > 0) {
+                if (!(found && ct > h.t)) spec_leaf_closest(V, o, d, c, n, h, found);
+                if (!spec_pop_closest(stk, tstk, sp, c, n, ct, found, h.t)) n = -1;
+            }
+        }
+        if (n < 0) live = false;
+    }
+    return found;
+}
+
 // XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs
 // (MI355X_MICROARCH.md, workgroup dispatch: b and b + 8 share an XCD and its
 // 4 MiB L2), so consecutive blocks of work land on 8 different L2s. With
@@ -2182,6 +2310,16 @@ static int ao_sort() {
 // RT580_AO_BUDGET: leaf visits per AO ray in ao_trace_kernel before the ray is
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
+// RT580_TRACE_SPEC: the trace levels' near closest-hit walk in speculative form
+static int trace_spec() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_TRACE_SPEC");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
 // RT580_AO_SPEC: the AO walks in speculative while-while form, bit 0 the
 // budgeted trace pass, bit 1 the late pass, bit 2 two held leaves (default the first two: north-star frame
 // 37.5 -> 34.3 ms, Cornell 59.6 -> 54.7 ms; profiles/r05/ab/spec*)
@@ -4275,7 +4413,10 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 const int grid = grid_for(c1 - c0, 1 << 20);
                 if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
                 RT_STEP("trace near phase");
-                hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
+                if (trace_spec())
+                    hipLaunchKernelGGL((trace_kernel<true, 1, false, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
+                else
+                    hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 uint32_t nq = 0, nb = 0;
                 if ((e = sort_far_queue(S, W, s, nq, nb)) != hipSuccess) return e;
