@@ -562,7 +562,12 @@ __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { retu
 template <class STK, class TSTK>
 __device__ bool bvh4_closest_spec(const BvhView& V, bool live, rv3 o, rv3 d, Hit& h, const STK& stk, const TSTK& tstk);
 
-// TSPEC (PHASE 1, BVH): the near closest-hit walk in speculative form (bvh4_closest_spec).
+template <int HOLD2, bool BOUND, class STK>
+__device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, bool live,
+                                          int& sp, int32_t& c, int32_t& n, float tmax = INFINITY);
+
+// TSPEC (BVH): the near walks in speculative form -- PHASE 1 the closest-hit
+// walk (bvh4_closest_spec), PHASE 3 the shadow rays' bounded any-hit walk.
 template <bool BVH, int PHASE, bool SCALAR = false, bool TSPEC = false>
 __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
                                                    uint32_t i1, int light = 0, int dl = 0, int wave_near = 0) {
@@ -687,6 +692,12 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             bool nh;
             if (wave_near && isinf(tmax)) {
                 nh = bvh_any_near_wave(S.bv, lit && !brute, so, L2, wstk[threadIdx.x >> 6]);
+            } else if (TSPEC && S.bv.nodes4) {  // the whole wave walks (speculative form)
+                uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS];
+                int ssp = 0;
+                int32_t sc = 0, sn = 0;
+                nh = bvh4_any_spec_budget_state<0, true>(S.bv, so, L2, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa},
+                                                         1 << 30, lit && !brute, ssp, sc, sn, tmax) > 0;
             } else if (S.bv.nodes4) {
                 uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS];
                 nh = lit && !brute && bvh4_any_near_s(S.bv, so, L2, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa}, tmax);
@@ -1331,9 +1342,9 @@ __device__ __forceinline__ bool spec_pop(const STK& stk, int& sp, int32_t& c, in
 // descending with one held); the leaf phase tests them in order, then the
 // current entry if it is a leaf. tools/simd_sim.cpp, 100k field, budget 4: wave
 // node iterations 32.6 -> 29.2, leaf tests 8.8 -> 9.1.
-template <int HOLD2 = 0, class STK>
+template <int HOLD2 = 0, bool BOUND = false, class STK>
 __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, bool live, int& sp,
-                                  int32_t& c, int32_t& n) {
+                                  int32_t& c, int32_t& n, float tmax = INFINITY) {
     if (!live) return 0;
     int r = 0;
     const SlabRay sr = slab_ray(V, o, d);
@@ -1359,7 +1370,7 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
                 bool ok[4];
                 node4_slab(V.nodes4 + c, sr, t, ok, nd.link);
 #pragma unroll
-                for (int j = 0; j < 4; j++) ok[j] = (nd.link[j] != 0xffffffffu) & ok[j];
+                for (int j = 0; j < 4; j++) ok[j] = (nd.link[j] != 0xffffffffu) & ok[j] & (!BOUND || !(t[j] > tmax));
                 int best = -1;
                 float bt = INFINITY;
 #pragma unroll
@@ -1384,16 +1395,16 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
         // leaf phase
         bool h = false;
         if (pn > 0) {
-            h = bvh4_leaf_hit(V, o, d, INFINITY, pc, pn);
+            h = bvh4_leaf_hit(V, o, d, BOUND ? tmax : INFINITY, pc, pn);
             visits++;
             pn = 0;
             if (HOLD2 && !h && qn > 0 && visits < budget) {
-                h = bvh4_leaf_hit(V, o, d, INFINITY, qc, qn);
+                h = bvh4_leaf_hit(V, o, d, BOUND ? tmax : INFINITY, qc, qn);
                 visits++;
                 qn = 0;
             }
             if (!h && n > 0 && (!HOLD2 || qn == 0) && visits < budget) {  // the current entry is a leaf too
-                h = bvh4_leaf_hit(V, o, d, INFINITY, c, n);
+                h = bvh4_leaf_hit(V, o, d, BOUND ? tmax : INFINITY, c, n);
                 visits++;
                 if (!spec_pop(stk, sp, c, n)) n = -1;
             }
@@ -1422,17 +1433,17 @@ __device__ int bvh4_any_spec_walk(const BvhView& V, rv3 o, rv3 d, const STK& stk
     return r;
 }
 
-template <int HOLD2 = 0, class STK>
+template <int HOLD2 = 0, bool BOUND = false, class STK>
 __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, bool live,
-                                          int& sp, int32_t& c, int32_t& n) {
+                                          int& sp, int32_t& c, int32_t& n, float tmax) {
     sp = 0;
     c = 0;
     n = 0;  // root (internal); n < 0: nothing left on this lane
     if (live)
         for (int k = 0; k < V.n_brute; k++)
-            if (prim_hit_within(V.all[V.brute[k]], o, d, INFINITY)) return 1;
+            if (prim_hit_within(V.all[V.brute[k]], o, d, BOUND ? tmax : INFINITY)) return 1;
     if (live && (!V.has_tree || dir_zero(d))) live = false;
-    return bvh4_any_spec_walk<HOLD2>(V, o, d, stk, budget, live, sp, c, n);
+    return bvh4_any_spec_walk<HOLD2, BOUND>(V, o, d, stk, budget, live, sp, c, n, tmax);
 }
 
 // bvh4_closest_near_s in speculative while-while form (the closest-hit walk
@@ -2310,7 +2321,8 @@ static int ao_sort() {
 // RT580_AO_BUDGET: leaf visits per AO ray in ao_trace_kernel before the ray is
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
-// RT580_TRACE_SPEC: the trace levels' near closest-hit walk in speculative form
+// RT580_TRACE_SPEC: the trace levels' near walks in speculative form, bit 0
+// the closest-hit phase, bit 1 the shadow rays
 static int trace_spec() {
     static int v = -1;
     if (v < 0) {
@@ -4413,7 +4425,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 const int grid = grid_for(c1 - c0, 1 << 20);
                 if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
                 RT_STEP("trace near phase");
-                if (trace_spec())
+                if (trace_spec() & 1)
                     hipLaunchKernelGGL((trace_kernel<true, 1, false, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
                 else
                     hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
@@ -4488,8 +4500,12 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         const int li = S.shadow_light[dl];
                         if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
                         RT_STEP("trace shadow near pass");
-                        hipLaunchKernelGGL((trace_kernel<true, 3>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1,
-                                           li, dl, near_wave() ? 1 : 0);
+                        if (trace_spec() & 2)
+                            hipLaunchKernelGGL((trace_kernel<true, 3, false, true>), dim3(grid), dim3(TB), 0, s, S, F, W,
+                                               level, c0, c1, li, dl, near_wave() ? 1 : 0);
+                        else
+                            hipLaunchKernelGGL((trace_kernel<true, 3>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1,
+                                               li, dl, near_wave() ? 1 : 0);
                         if ((e = hipGetLastError()) != hipSuccess) return e;
                         uint32_t sq = 0, sb = 0;
                         if ((e = sort_far_queue(S, W, s, sq, sb, /*one_dir=*/true)) != hipSuccess) return e;
