@@ -2322,12 +2322,16 @@ static int ao_sort() {
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
 // RT580_TRACE_SPEC: the trace levels' near walks in speculative form, bit 0
-// the closest-hit phase, bit 1 the shadow rays
+// the closest-hit phase, bit 1 the shadow rays. Default 2 (kernel trace,
+// profiles/r05/ab/trace_spec.txt: the shadow pass 283.5 -> 271.9 us per launch
+// on the north-star frame, 451 -> 404 us on Cornell; the closest-hit form is
+// slower, 392 -> 526 / 480 -> 617 us -- its speculative descents run with the
+// bound of before the held leaf's test, which is what prunes most of the tree)
 static int trace_spec() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("RT580_TRACE_SPEC");
-        v = e ? atoi(e) : 0;
+        v = e ? atoi(e) : 2;
     }
     return v;
 }
