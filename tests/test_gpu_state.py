@@ -281,6 +281,46 @@ def test_graph_replayed_small_frames_match_oracle():
             lib.rt_gpu_host_unregister(buf.ctypes.data)
 
 
+def test_last_stats_follow_graph_replayed_frames():
+    """rt_gpu_last_stats after graph-replayed frames: frame A
+    rendered into a registered buffer (plain, captured, replayed), then a
+    different frame B left in HBM (rt_gpu_render_device), then A replayed
+    again -- the counters always describe the frame just rendered."""
+    rt580 = helpers.rt580()
+    lib = rt580.load()
+    scene, w, h = "simpleSphereSceneAO.json", 64, 48
+    ra, pa = _params(scene, w, h, 4, 8, helpers.ASSETS_ROOT)
+    rb, pb = _params(scene, 40, 24, 3, 4, helpers.ASSETS_ROOT)
+    s = ra.scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(s)), "upload")
+    keys = ("rays_total", "rays_primary", "rays_secondary", "rays_shadow", "rays_ao", "ao_calls")
+
+    def stats():
+        st = rt580.RenderStats()
+        rt580.check(lib.rt_gpu_last_stats(ctypes.byref(st)), "last_stats")
+        return tuple(getattr(st, k) for k in keys)
+
+    raw, buf, span = _registered(w * h * 3)
+    rt580.check(lib.rt_gpu_host_register(buf.ctypes.data, span), "host_register")
+    try:
+        rt580.check(lib.rt_gpu_render(ctypes.byref(pa), buf.ctypes.data), "render A")
+        want_a = stats()
+        assert want_a[1] == w * h and want_a[5] > 0
+        for i in range(3):  # the slot's second identical call captures, later ones replay
+            rt580.check(lib.rt_gpu_render(ctypes.byref(pa), buf.ctypes.data), "render A")
+            assert stats() == want_a, "call %d" % i
+        fb = ctypes.c_void_p()
+        rt580.check(lib.rt_gpu_render_device(ctypes.byref(pb), ctypes.byref(fb)), "render_device B")
+        rt580.check(lib.rt_gpu_synchronize(), "synchronize")
+        want_b = stats()
+        assert want_b[1] == 40 * 24 and want_b != want_a
+        for i in range(2):
+            rt580.check(lib.rt_gpu_render(ctypes.byref(pa), buf.ctypes.data), "render A again")
+            assert stats() == want_a, "after B, call %d" % i
+    finally:
+        lib.rt_gpu_host_unregister(buf.ctypes.data)
+
+
 _GRID_CHILD = r"""
 import sys
 sys.path.insert(0, sys.argv[1])
