@@ -2337,7 +2337,8 @@ static int trace_spec() {
 }
 
 // RT580_AO_SPEC: the AO walks in speculative while-while form, bit 0 the
-// budgeted trace pass, bit 1 the late pass, bit 2 two held leaves (default the first two: north-star frame
+// budgeted trace pass, bit 1 the late pass, bit 2 two held leaves, bits 3-4 the
+// trace's block shape (A/B: 8 x 8 cells, 1024-sample blocks) (default the first two: north-star frame
 // 37.5 -> 34.3 ms, Cornell 59.6 -> 54.7 ms; profiles/r05/ab/spec*)
 static int ao_spec() {
     static int v = -1;
@@ -4687,6 +4688,10 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                         const uint32_t ns = (uint32_t)F.ao_samples;
                         if (bu == 4 && (ao_spec() & 4))
                             hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4, 2>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
+                        else if (bu == 4 && (ao_spec() & 8))  // (A/B) 8 x 8 direction cells
+                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 3, 4, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
+                        else if (bu == 4 && (ao_spec() & 16))  // (A/B) blocks of 1024 samples
+                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 4, 4, 4, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
                         else if (bu == 3)
                             hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 3, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
                         else if (bu <= 4)

@@ -84,7 +84,7 @@ const Knob kKnobs[] = {
     {"RT580_AO_RESUME", INT_SET, 0, 0, k01, nullptr},
     {"RT580_D2H_MAPPED", INT_SET, 0, 0, k01, nullptr},
     {"RT580_TRACE_SPEC", INT_SET, 0, 0, k0123, nullptr},
-    {"RT580_AO_SPEC", INT_RANGE, 0, 7, nullptr, nullptr},
+    {"RT580_AO_SPEC", INT_RANGE, 0, 31, nullptr, nullptr},
     {"RT580_AO_REFILL", INT_RANGE, 0, 3, nullptr, nullptr},
     {"RT580_AO_REFILL_MIN", INT_RANGE, 1, 64, nullptr, nullptr},
     {"RT580_SMALL_SORT", INT_SET, 0, 0, k01, nullptr},
