@@ -381,7 +381,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
             n_px = ctx.args.check_pixels if ctx.args.check_pixels > 0 else CHECK_PIXELS[name]
             if n_px:
                 out["frame_check"].update(oracle_rows_check(ctx, name, root, frame_np, row_counts, n_px))
-    if not ctx.dist_on and not ctx.multi and K == 1:
+    if not ctx.dist_on and not ctx.multi and K == 1 and not ctx.args.no_render_call:
         out["render_call_ms"] = render_latency(lib, rt580, params, torch)
     for _, buf in ring:
         rt580.check(lib.rt_gpu_host_unregister(buf.ctypes.data), "rt_gpu_host_unregister")
@@ -699,6 +699,9 @@ def main():
                          "interleaved split; RNG bases from an untimed full-frame count), for huge frames and "
                          "the per-rank shares of a split")
     ap.add_argument("--row-rank", type=int, default=0, help="R of --row-sample")
+    ap.add_argument("--no-render-call", action="store_true",
+                    help="skip the blocking Render() latency frames (render_call_ms): counter profiles of the step's "
+                         "kernels only (small-scene Render() frames run their AO in two launches)")
     ap.add_argument("--no-live-timing", action="store_true",
                     help="no HIP-event timing of the frames' phases and AO launches inside the timed region (A/B of "
                          "its cost; the roofline then has only the isolated timing)")

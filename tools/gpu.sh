@@ -94,7 +94,9 @@ profile)
   TAG=$1; shift
   OUT=gpurun_out/prof_$TAG
   mkdir -p $OUT
-  BENCH="python3 bench.py --no-cpu-baseline --no-north-star --no-config3 --no-check $*"
+  # the step's frames only: no Render() latency frames (their AO runs in two launches,
+  # which would mix half launches into the per-dispatch averages)
+  BENCH="python3 bench.py --no-cpu-baseline --no-north-star --no-config3 --no-check --no-render-call $*"
   case "$*" in *--steps*) ;; *) BENCH="$BENCH --steps 3 --warmup 1";; esac
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o trace -- $BENCH > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 1; }
   i=0
