@@ -57,7 +57,7 @@ struct NodeRec {
     int32_t local_b_flags;// b | flags << 16
     float kr, kt;         // ComputeFresnel
     int32_t shape;        // material index
-    uint32_t call0;       // first AO call (local index) of this node
+    uint32_t spare;       // unused (a hit node's first AO call is in DevWork::node_call0)
     int32_t pad[2];
 };
 #define RT_NODE_HIT 1
@@ -77,6 +77,8 @@ constexpr int kLateWords = 2 + kLateSaved;  // words per saved walk
 
 struct DevWork {
     NodeRec* nodes;        // [node_cap]
+    int4* topo;            // [node_cap] child[0], child[1], flags (rank_kernel's walk reads these 16 bytes, not the record)
+    uint32_t* node_call0;  // [node_cap] first AO call of a hit node (rank_kernel -> resolve)
     RayItem* rays;         // [node_cap] (indexed by node id; level 0 is implicit)
     uint32_t* lvl;         // [2 * (RT_MAX_DEPTH + 2)]: counts then bases
     uint32_t* needed;      // [1] highest node id requested + 1 (overflow check)

@@ -844,9 +844,10 @@ __global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWo
             rec.kr = kr;
             rec.kt = kt;
             rec.shape = shape;
-            rec.call0 = 0;
+            rec.spare = 0;
             rec.pad[0] = rec.pad[1] = 0;
             W.nodes[node] = rec;
+            W.topo[node] = make_int4(child0, child1, flags, 0);
             if (level == 0) {
                 W.pix_hits[pixel] = hit ? 1u : 0u;
                 W.pix_nodes[pixel] = 1u;
@@ -967,10 +968,9 @@ __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWor
     uint32_t call = (uint32_t)lbase;
     while (sp > 0) {
         const int n = stack[--sp];
-        const NodeRec& nd = W.nodes[n];
-        const int flags = nd.local_b_flags >> 16;
-        if (!(flags & RT_NODE_HIT)) continue;
-        W.nodes[n].call0 = call;
+        const int4 tp = W.topo[n];  // child[0], child[1], flags
+        if (!(tp.z & RT_NODE_HIT)) continue;
+        W.node_call0[n] = call;
         for (int a = 0; a < S.n_ambient; a++) {
             W.call_node[call] = (uint32_t)n;
             W.call_rng[call] = rng;
@@ -979,8 +979,8 @@ __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWor
             if (F.rng_engine == RT_RNG_MINSTD_RAND0) rng = mersenne31_mul((uint32_t)rng, step);
             else rng++;
         }
-        if (nd.child[1] >= 0) stack[sp++] = nd.child[1];  // refraction after
-        if (nd.child[0] >= 0) stack[sp++] = nd.child[0];  // reflection first
+        if (tp.y >= 0) stack[sp++] = tp.y;  // refraction after
+        if (tp.x >= 0) stack[sp++] = tp.x;  // reflection first
     }
 }
 
@@ -3517,7 +3517,7 @@ struct RFrame {
 };
 
 __device__ __forceinline__ rpix node_local(const DevScene& S, const DevFrame& F, const DevWork& W, const NodeRec& nd,
-                                           const rt_material& m) {
+                                           const rt_material& m, uint32_t node) {
     rpix local = px((int16_t)(nd.local_rg & 0xffff), (int16_t)(nd.local_rg >> 16), (int16_t)(nd.local_b_flags & 0xffff));
     int a = 0;
     for (int li = 0; li < S.n_lights; li++) {
@@ -3525,7 +3525,7 @@ __device__ __forceinline__ rpix node_local(const DevScene& S, const DevFrame& F,
         if (l.kind != RT_LIGHT_AMBIENT) continue;
         rv3 amb = v3_scale(v3_mul(v3_scale(ld3(m.cs), m.ka), ld3(l.color)), l.intensity);
         float ao = 1.0f;
-        if (F.ao_enabled) ao = 1.0f - ((float)W.occ[nd.call0 + a] / (float)F.ao_samples);
+        if (F.ao_enabled) ao = 1.0f - ((float)W.occ[W.node_call0[node] + a] / (float)F.ao_samples);
         amb = v3_scale(amb, ao);
         local = px_add(local, px_from(amb));
         a++;
@@ -3549,7 +3549,7 @@ __global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, Dev
             ret = px(254, 64, 205);  // BG_COLOR (Raytracer.h:597)
         } else {
             const rt_material m = S.mats[nd.shape];
-            const rpix local = node_local(S, F, W, nd, m);
+            const rpix local = node_local(S, F, W, nd, m, (uint32_t)cur);
             if (flags & RT_NODE_LEAF) {
                 ret = px_clamp(local);
             } else {
@@ -3623,7 +3623,7 @@ __global__ void __launch_bounds__(TB) resolve_level_kernel(DevScene S, DevFrame 
             v = px(254, 64, 205);  // BG_COLOR (Raytracer.h:597)
         } else {
             const rt_material m = S.mats[nd.shape];
-            const rpix local = node_local(S, F, W, nd, m);
+            const rpix local = node_local(S, F, W, nd, m, node);
             v = (flags & RT_NODE_LEAF) ? px_clamp(local)
                                        : combine(local, node_val_load(W, nd.child[0]), node_val_load(W, nd.child[1]),
                                                  nd.kr, nd.kt, m.ks, m.kt);
