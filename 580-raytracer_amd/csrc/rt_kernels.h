@@ -79,6 +79,7 @@ struct DevWork {
     NodeRec* nodes;        // [node_cap]
     int4* topo;            // [node_cap] child[0], child[1], flags (rank_kernel's walk reads these 16 bytes, not the record)
     uint32_t* node_call0;  // [node_cap] first AO call of a hit node (rank_kernel -> resolve)
+    int2* node_val;        // [node_cap] a node's value (Raycast's return, r | g << 16, b) for its parent's resolve
     RayItem* rays;         // [node_cap] (indexed by node id; level 0 is implicit)
     uint32_t* lvl;         // [2 * (RT_MAX_DEPTH + 2)]: counts then bases
     uint32_t* needed;      // [1] highest node id requested + 1 (overflow check)

@@ -3590,12 +3590,12 @@ __global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, Dev
 
 // Level-by-level form of the same blend: one launch per recursion level, from
 // the deepest up. A node's value (Raycast's return) is combined from its own
-// local colour and its children's values, stored by the previous launch in the
-// children's NodeRec.pad; level 0 writes the framebuffer. Coalesced over each
+// local colour and its children's values, stored by the previous launch in
+// W.node_val (8 bytes per node, not the 64-byte records); level 0 writes the framebuffer. Coalesced over each
 // level's contiguous node ids, no per-thread stack.
 __device__ __forceinline__ rpix node_val_load(const DevWork& W, int32_t id) {
     if (id < 0) return px(0, 0, 0);
-    const int2 v = *reinterpret_cast<const int2*>(W.nodes[id].pad);
+    const int2 v = W.node_val[id];
     return px((int16_t)(v.x & 0xffff), (int16_t)(v.x >> 16), (int16_t)(v.y & 0xffff));
 }
 
@@ -3633,7 +3633,7 @@ __global__ void __launch_bounds__(TB) resolve_level_kernel(DevScene S, DevFrame 
             fb[(size_t)node * 3 + 1] = (int16_t)v.g;
             fb[(size_t)node * 3 + 2] = (int16_t)v.b;
         } else {
-            *reinterpret_cast<int2*>(W.nodes[node].pad) =
+            W.node_val[node] =
                 make_int2((int32_t)(((uint32_t)v.r & 0xffffu) | ((uint32_t)v.g << 16)), (int32_t)((uint32_t)v.b & 0xffffu));
         }
     }

@@ -41,7 +41,7 @@ struct Slot {
     hipStream_t stream = nullptr;  // frame stream (non-blocking)
     hipEvent_t done = nullptr;     // end of the slot's last enqueued phase
     hipEvent_t ao_done = nullptr;  // end of the AO kernels of the slot's last frame
-    DevBuf nodes, topo, node_call0, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
+    DevBuf nodes, topo, node_call0, node_val, rays, lvl, needed, pix_hits, pix_nodes, pix_prefix, row_calls, row_hits, row_nodes,
         row_base_local, totals, call_node, call_rng, occ, fb, fb_full, mt_stream, aofix_items, aofix_count,
         call_hint, mt_windows, fb8;
     uint64_t mt_base = 0;  // absolute index of mt_stream's first draw
@@ -591,6 +591,7 @@ DevWork dev_work() {
     w.nodes = (NodeRec*)SL.nodes.p;
     w.topo = (int4*)SL.topo.p;
     w.node_call0 = (uint32_t*)SL.node_call0.p;
+    w.node_val = (int2*)SL.node_val.p;
     w.rays = (RayItem*)SL.rays.p;
     w.lvl = (uint32_t*)SL.lvl.p;
     w.needed = (uint32_t*)SL.needed.p;
@@ -697,6 +698,7 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     const uint64_t ccap = cap * (uint64_t)(g.n_ambient > 0 ? g.n_ambient : 1);
     if (ccap > 0xffffff00ull) return fail("AO-call capacity exceeds 2^32");
     if (ensure(SL.nodes, cap * sizeof(NodeRec)) || ensure(SL.topo, cap * 16) || ensure(SL.node_call0, cap * 4) ||
+        ensure(SL.node_val, cap * 8) ||
         ensure(SL.rays, cap * sizeof(RayItem)) ||
         ensure(SL.lvl, 4 * (RT_MAX_DEPTH + 2) * sizeof(uint32_t)) || ensure(SL.needed, 64) ||
         ensure(SL.pix_hits, npix * 4) || ensure(SL.pix_nodes, npix * 4) || ensure(SL.pix_prefix, npix * 4) ||
@@ -1924,7 +1926,7 @@ void shutdown_ctx() {
                       &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.ppm_stage})
         release(*b);
     for (Slot& sl : g.slot) {
-        for (DevBuf* b : {&sl.nodes, &sl.topo, &sl.node_call0, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
+        for (DevBuf* b : {&sl.nodes, &sl.topo, &sl.node_call0, &sl.node_val, &sl.rays, &sl.lvl, &sl.needed, &sl.pix_hits, &sl.pix_nodes, &sl.pix_prefix,
                           &sl.row_calls, &sl.row_hits, &sl.row_nodes, &sl.row_base_local, &sl.totals, &sl.call_node,
                           &sl.call_rng, &sl.occ, &sl.fb, &sl.fb_full, &sl.fb8, &sl.mt_stream, &sl.mt_windows, &sl.aofix_items, &sl.aofix_count,
                           &sl.call_hint, &sl.ao_rays, &sl.ao_state, &sl.ao_late, &sl.ao_late_count, &sl.far_rays, &sl.far_keys,
