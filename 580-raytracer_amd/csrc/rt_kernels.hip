@@ -568,8 +568,9 @@ __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const 
 
 // TSPEC (BVH): the near walks in speculative form -- PHASE 1 the closest-hit
 // walk (bvh4_closest_spec), PHASE 3 the shadow rays' bounded any-hit walk.
-template <bool BVH, int PHASE, bool SCALAR = false, bool TSPEC = false>
-__global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
+// WPE > 0: an occupancy target (small-scene A/B, RT580_SMALL_TRACE_WPE).
+template <bool BVH, int PHASE, bool SCALAR = false, bool TSPEC = false, int WPE = 0>
+__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
                                                    uint32_t i1, int light = 0, int dl = 0, int wave_near = 0) {
     __shared__ rt_prim tile[TILE];
     __shared__ WaveEntry wstk[PHASE == 3 ? TB / 64 : 1][RT_WAVE_STACK];
@@ -2321,6 +2322,16 @@ static int ao_sort() {
 // RT580_AO_BUDGET: leaf visits per AO ray in ao_trace_kernel before the ray is
 // left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
 // 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
+// RT580_SMALL_TRACE_WPE: occupancy target of the small-scene trace kernel (0: none, A/B 5, 6)
+static int small_trace_wpe() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RT580_SMALL_TRACE_WPE");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
 // RT580_TRACE_SPEC: the trace levels' near walks in speculative form, bit 0
 // the closest-hit phase, bit 1 the shadow rays. Default 2 (kernel trace,
 // profiles/r05/ab/trace_spec.txt: the shadow pass 283.5 -> 271.9 us per launch
@@ -4542,7 +4553,15 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
         const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, deep_grid());
         if (S.use_bvh) hipLaunchKernelGGL((trace_kernel<true, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
         else if (S.n_prims <= TILE && trace_scalar())
-            hipLaunchKernelGGL((trace_kernel<false, 0, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
+        {
+            const int sw = small_trace_wpe();
+            if (sw == 5)
+                hipLaunchKernelGGL((trace_kernel<false, 0, true, false, 5>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
+            else if (sw == 6)
+                hipLaunchKernelGGL((trace_kernel<false, 0, true, false, 6>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
+            else
+                hipLaunchKernelGGL((trace_kernel<false, 0, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
+        }
         else hipLaunchKernelGGL((trace_kernel<false, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }

@@ -41,6 +41,7 @@ const long kFarU[] = {1, 2, 4, -1};
 const long kFarCU[] = {0, 1, 2, 4, -1};
 const long k0123[] = {0, 1, 2, 3, -1};
 const long k148[] = {1, 4, 8, -1};
+const long kSmallWpe[] = {0, 5, 6, -1};
 // the AO kernel flavours launch_ao_small instantiates (rt_kernels.hip)
 const long kAoVariant[] = {
     0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,                            // ao_kernel<v>
@@ -83,6 +84,7 @@ const Knob kKnobs[] = {
     {"RT580_AO_BUDGET2", INT_SET, 0, 0, k01, nullptr},
     {"RT580_AO_RESUME", INT_SET, 0, 0, k01, nullptr},
     {"RT580_D2H_MAPPED", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_SMALL_TRACE_WPE", INT_SET, 0, 0, kSmallWpe, nullptr},
     {"RT580_TRACE_SPEC", INT_SET, 0, 0, k0123, nullptr},
     {"RT580_AO_SPEC", INT_RANGE, 0, 31, nullptr, nullptr},
     {"RT580_AO_REFILL", INT_RANGE, 0, 3, nullptr, nullptr},
