@@ -49,17 +49,16 @@ struct DevFrame {
 };
 
 // One node of the reflect/refract recursion tree (a Raycast call). 64 bytes.
-struct NodeRec {
+struct alignas(16) NodeRec {
     float hp[3];          // hit point (hitInfo.hitPoint)
     float n[3];           // geometric normal (hitInfo.normal)
-    int32_t child[2];     // reflection / refraction child node ids, -1: none
     int32_t local_rg;     // non-ambient local colour: r | g << 16 (int16 each)
     int32_t local_b_flags;// b | flags << 16
     float kr, kt;         // ComputeFresnel
     int32_t shape;        // material index
-    uint32_t spare;       // unused (a hit node's first AO call is in DevWork::node_call0)
-    int32_t pad[2];
-};
+    int32_t spare;
+};  // 48 bytes; the children and flags are also in DevWork::topo, a hit node's first AO call in node_call0
+static_assert(sizeof(NodeRec) == 48, "NodeRec is three 16-byte words");
 #define RT_NODE_HIT 1
 #define RT_NODE_LEAF 2  // bounces == 0: no combine
 

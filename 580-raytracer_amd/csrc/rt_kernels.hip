@@ -837,8 +837,6 @@ __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE > 0
             NodeRec rec;
             rec.hp[0] = hi.p.x; rec.hp[1] = hi.p.y; rec.hp[2] = hi.p.z;
             rec.n[0] = hi.n.x; rec.n[1] = hi.n.y; rec.n[2] = hi.n.z;
-            rec.child[0] = child0;
-            rec.child[1] = child1;
             const int flags = (hit ? RT_NODE_HIT : 0) | (bounces == 0 ? RT_NODE_LEAF : 0);
             rec.local_rg = (int32_t)(((uint32_t)local.r & 0xffffu) | ((uint32_t)local.g << 16));
             rec.local_b_flags = (int32_t)(((uint32_t)local.b & 0xffffu) | ((uint32_t)flags << 16));
@@ -846,7 +844,6 @@ __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE > 0
             rec.kt = kt;
             rec.shape = shape;
             rec.spare = 0;
-            rec.pad[0] = rec.pad[1] = 0;
             W.nodes[node] = rec;
             W.topo[node] = make_int4(child0, child1, flags, 0);
             if (level == 0) {
@@ -3569,10 +3566,11 @@ __global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, Dev
                 f.refl = px(0, 0, 0);
                 f.kr = nd.kr; f.kt = nd.kt; f.ks = m.ks; f.ktm = m.kt;
                 f.node = cur;
-                if (nd.child[0] >= 0) {
-                    f.stage = 1; cur = nd.child[0]; lvl++; descended = true;
-                } else if (nd.child[1] >= 0) {
-                    f.stage = 2; cur = nd.child[1]; lvl++; descended = true;
+                const int4 tp = W.topo[cur];
+                if (tp.x >= 0) {
+                    f.stage = 1; cur = tp.x; lvl++; descended = true;
+                } else if (tp.y >= 0) {
+                    f.stage = 2; cur = tp.y; lvl++; descended = true;
                 } else {
                     ret = combine(local, px(0, 0, 0), px(0, 0, 0), f.kr, f.kt, f.ks, f.ktm);
                 }
@@ -3584,7 +3582,7 @@ __global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, Dev
             RFrame& pf = st[lvl - 1];
             if (pf.stage == 1) {
                 pf.refl = ret;
-                const int c1 = W.nodes[pf.node].child[1];
+                const int c1 = W.topo[pf.node].y;
                 if (c1 >= 0) { pf.stage = 2; cur = c1; resumed = true; break; }
                 ret = combine(pf.local, pf.refl, px(0, 0, 0), pf.kr, pf.kt, pf.ks, pf.ktm);
             } else {
@@ -3635,9 +3633,12 @@ __global__ void __launch_bounds__(TB) resolve_level_kernel(DevScene S, DevFrame 
         } else {
             const rt_material m = S.mats[nd.shape];
             const rpix local = node_local(S, F, W, nd, m, node);
-            v = (flags & RT_NODE_LEAF) ? px_clamp(local)
-                                       : combine(local, node_val_load(W, nd.child[0]), node_val_load(W, nd.child[1]),
-                                                 nd.kr, nd.kt, m.ks, m.kt);
+            if (flags & RT_NODE_LEAF) {
+                v = px_clamp(local);
+            } else {
+                const int4 tp = W.topo[node];
+                v = combine(local, node_val_load(W, tp.x), node_val_load(W, tp.y), nd.kr, nd.kt, m.ks, m.kt);
+            }
         }
         if (level == 0) {
             fb[(size_t)node * 3 + 0] = (int16_t)v.r;
