@@ -61,14 +61,17 @@ def test_dist_frame_rccl_one_rank_matches_reference(rccl_one_rank, u8):
         ppm = (b"P6\n%d %d\n255\n" % (w, h) + arr.tobytes()) if u8 else rt580.ppm_bytes(arr)
         return helpers.sha256(ppm)
 
-    # one frame at a time
-    for _ in range(2):
-        df.render()
+    try:
+        # one frame at a time
+        for _ in range(2):
+            df.render()
+            assert sha(df.finish()) == want
+        # five frames queued back to back (pipelined slots, async gathers in flight)
+        for _ in range(5):
+            df.render()
         assert sha(df.finish()) == want
-    # five frames queued back to back (pipelined slots, async gathers in flight)
-    for _ in range(5):
-        df.render()
-    assert sha(df.finish()) == want
+    finally:
+        df.close()  # its registered host buffers leave the library's table before numpy frees them
     rt.close()
 
 
