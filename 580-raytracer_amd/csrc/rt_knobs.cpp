@@ -58,6 +58,7 @@ const char* const kTransport[] = {"rccl", "local", nullptr};
 const Knob kKnobs[] = {
     // rt_shim.cpp / raytracer.cpp
     {"RT580_PIPELINE", INT_SET, 0, 0, k01, nullptr},
+    {"RT580_PHASE_EVENTS", INT_SET, 0, 0, k01, nullptr},
     {"RT580_SLOTS", INT_SET, 0, 0, k234, nullptr},
     {"RT580_AO_ORDER", INT_SET, 0, 0, k01, nullptr},
     {"RT580_SMALL_SLOTS", INT_SET, 0, 0, k234, nullptr},

@@ -866,6 +866,8 @@ void note_rows(const rt_render_params* p, int n_rows, bool accel) {
 }
 
 // Phase 1: trace every level of the selected rows and count their AO calls.
+static hipError_t phase_mark(int e, hipStream_t s);
+
 int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_rows) {
     if (ensure_work(p, n_rows)) return RT_FAILURE;  // (launch_trace zeroes the per-frame counters)
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
@@ -889,7 +891,7 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
         if (!replay && frame_verified(p)) g.trace_valid = true;
     }
     HIP_TRY(launch_row_counts(sc, f, dev_work(), fs()));
-    HIP_TRY(hipEventRecord(g.ev[EV_TRACE], fs()));
+    HIP_TRY(phase_mark(EV_TRACE, fs()));
     note_rows(p, n_rows, sc.use_bvh != 0);
     return RT_SUCCESS;
 }
@@ -941,6 +943,20 @@ int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global
     return RT_SUCCESS;
 }
 
+// The frame's phase boundaries for rt_gpu_last_stats (ms_count, ms_scan,
+// ms_render). RT580_PHASE_EVENTS=0 (A/B): only the frame's start and end are
+// recorded -- each event between two kernels of a stream costs that stream a
+// few microseconds of idle.
+static hipError_t phase_mark(int e, hipStream_t s) {
+    static int on = -1;
+    if (on < 0) {
+        const char* v = std::getenv("RT580_PHASE_EVENTS");
+        on = v ? std::atoi(v) : 1;
+    }
+    if (!on && !g.profiling) return hipSuccess;
+    return hipEventRecord(g.ev[e], s);
+}
+
 // AO phases in frame order (RT580_AO_ORDER=1, rt580_set_ao_order): a frame's
 // AO kernels start after the previous frame's, so consecutive frames overlap
 // one frame's trace with the other's AO only. Off by default: AO phases that
@@ -968,7 +984,7 @@ int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
     DevFrame f = dev_frame(p, row_begin, row_step, n_rows);
     const DevScene sc = dev_scene(p, n_rows);
     HIP_TRY(launch_rank(sc, f, dev_work(), row_base_global, fs()));
-    HIP_TRY(hipEventRecord(g.ev[EV_RANK], fs()));
+    HIP_TRY(phase_mark(EV_RANK, fs()));
     if (prepare_mt_stream(p, row_base_global, n_rows)) return RT_FAILURE;
     DevWork w = dev_work();
     {
@@ -985,8 +1001,8 @@ int shade_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
         HIP_TRY(e);
         if (!replay && frame_verified(p)) g.ao_valid = true;
     }
-    HIP_TRY(hipEventRecord(g.ev[EV_AO], fs()));
-    if (g.pipeline) {
+    HIP_TRY(phase_mark(EV_AO, fs()));
+    if (g.pipeline && ao_order()) {  // only the ordered AO phases wait on it
         HIP_TRY(hipEventRecord(SL.ao_done, fs()));
         g.last_ao_slot = g.cur;
     }
