@@ -48,7 +48,7 @@ struct DevFrame {
     uint32_t step_pow2[32];
 };
 
-// One node of the reflect/refract recursion tree (a Raycast call). 64 bytes.
+// One node of the reflect/refract recursion tree (a Raycast call). 48 bytes.
 struct alignas(16) NodeRec {
     float hp[3];          // hit point (hitInfo.hitPoint)
     float n[3];           // geometric normal (hitInfo.normal)
@@ -94,8 +94,8 @@ struct DevWork {
     uint64_t* call_rng;    // [call_cap] minstd state at the call's first draw / mt19937 global call index
     uint32_t* occ;         // [call_cap] occluded samples
     const uint32_t* mt_stream;  // mt19937 draws [mt_base, ...) of the serial stream, else null
-    uint64_t mt_base;
-    uint32_t refill_min;   // RT580_AO_REFILL_MIN: idle lanes a persistent-lane wave refills at once           // absolute index of mt_stream[0]
+    uint64_t mt_base;      // absolute index (in the serial stream) of mt_stream[0]
+    uint32_t refill_min;   // RT580_AO_REFILL_MIN: idle lanes a persistent-lane wave refills at once
     uint32_t node_cap;
     uint32_t call_cap;
     // BVH scenes: AO rays that miss every near triangle, queued for the sorted
@@ -150,6 +150,10 @@ struct DevWork {
     // none yet. [call_cap] or null
     uint32_t* call_hint;
     uint32_t aofix_cap;
+    // the slot's replay-check word (count_check_kernel sets it when a replayed
+    // count differs from the frame's own): kernels of BVH frames return at
+    // entry when it is set (rt_kernels.hip frame_poisoned). Null: never set.
+    const uint32_t* poison;
 };
 
 // Host reads of device counts during a frame's enqueue (trace-level ray

@@ -49,6 +49,17 @@ namespace rt580 {
 #define NEAR_LDS 16  // traversal-stack entries per lane in LDS (trace_kernel's near phases)
 #define LVL_BASE (RT_MAX_DEPTH + 2)
 
+// A frame whose replayed count differed from its own (count_check_kernel set
+// the slot's check word, DevWork::poison). Launches enqueued after a replayed
+// count are sized by it; every kernel of a BVH frame that such a launch can
+// reach returns at entry once the word is set, so a wrong count (and the stale
+// queue entries it would cover) is never used to index anything. The word is
+// uniform over the grid: the whole launch returns. The call ends as RT_FAILURE
+// (rt_shim.cpp check_replay).
+__device__ __forceinline__ bool frame_poisoned(const DevWork& W) {
+    return W.poison != nullptr && __builtin_expect(*W.poison != 0u, 0);
+}
+
 // ---------------------------------------------------------------- RNG
 // minstd_rand0: x' = 16807 x mod (2^31-1), seed 1 (libstdc++ default_random_engine).
 __device__ __forceinline__ uint32_t mersenne31_mul(uint32_t a, uint32_t b) {
@@ -572,6 +583,7 @@ __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const 
 template <bool BVH, int PHASE, bool SCALAR = false, bool TSPEC = false, int WPE = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
                                                    uint32_t i1, int light = 0, int dl = 0, int wave_near = 0) {
+    if (BVH && frame_poisoned(W)) return;
     __shared__ rt_prim tile[TILE];
     __shared__ WaveEntry wstk[PHASE == 3 ? TB / 64 : 1][RT_WAVE_STACK];
     // the near queries' traversal stacks (4-wide tree): the first NEAR_LDS
@@ -863,6 +875,7 @@ __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE > 0
 // consecutive pixels; the runs' sums are scanned across the wave (shuffles)
 // and the workgroup's four waves (LDS), then each run writes its prefixes.
 __global__ void __launch_bounds__(TB) row_counts_kernel(DevScene S, DevFrame F, DevWork W) {
+    if (frame_poisoned(W)) return;
     __shared__ uint32_t wsum[TB / 64][3];
     const int lr = blockIdx.x;
     const uint32_t off = (uint32_t)lr * (uint32_t)F.width;
@@ -914,6 +927,7 @@ __global__ void __launch_bounds__(TB) row_counts_kernel(DevScene S, DevFrame F, 
 
 // Exclusive scan of this call's per-row AO calls (one workgroup) + the total.
 __global__ void __launch_bounds__(1024) row_scan_kernel(DevFrame F, DevWork W) {
+    if (frame_poisoned(W)) return;
     __shared__ uint64_t part[1024];
     __shared__ uint64_t carry;
     if (threadIdx.x == 0) carry = 0;
@@ -941,6 +955,7 @@ __global__ void __launch_bounds__(1024) row_scan_kernel(DevFrame F, DevWork W) {
 // of the recursion tree, lights in JSON order) and record each call's RNG position.
 __global__ void __launch_bounds__(TB) rank_kernel(DevScene S, DevFrame F, DevWork W,
                                                   const uint64_t* __restrict__ row_base_global) {
+    if (frame_poisoned(W)) return;
     const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
     const uint32_t p = blockIdx.x * TB + threadIdx.x;
     if (p >= npix || S.n_ambient == 0) return;
@@ -1270,6 +1285,7 @@ __device__ void ao_fix_item(const DevScene& S, const DevFrame& F, const DevWork&
 // every item of [b, e) is re-tested and the failing ones recomputed instead.
 __global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e,
                                                     const uint64_t* call_lo, const uint64_t* call_hi) {
+    if (frame_poisoned(W)) return;
     if (call_lo) b = *call_lo * (uint64_t)F.ao_samples;
     if (call_hi) e = *call_hi * (uint64_t)F.ao_samples;
     const uint32_t n = *W.aofix_count;
@@ -1299,6 +1315,7 @@ __global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevW
 
 // BVH scenes: near any-hit of AO items [b, e); misses are queued (far pass below).
 __global__ void __launch_bounds__(TB) ao_near_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
+    if (frame_poisoned(W)) return;
     ao_body<512 | 1024 | 2048 | 4096>(S, F, W, b, e);
 }
 
@@ -1308,6 +1325,7 @@ __global__ void __launch_bounds__(TB) ao_near_kernel(DevScene S, DevFrame F, Dev
 template <int WPE, int V = 512 | 1024 | 2048 | 4096>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_near_kernel_w(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
+    if (frame_poisoned(W)) return;
     ao_body<V>(S, F, W, b, e);
 }
 
@@ -1594,6 +1612,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
 template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0, int SPEC = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
+    if (frame_poisoned(W)) return;
     __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
     constexpr int SN = SORT > 0 ? SORT * TB : 1;
     constexpr int NB = 1 << (2 * KL);  // direction cells
@@ -1722,6 +1741,7 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
 template <int WPE, int LDS_D, int SORT, int KL, int BUDGET>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_trace_refill_kernel(DevScene S, DevWork W, uint64_t n) {
+    if (frame_poisoned(W)) return;
     static_assert(LDS_D > 0 && SORT > 0 && BUDGET > 0, "refill form: LDS stack, block sort, step budget");
     __shared__ uint32_t lstk[LDS_D][TB];
     constexpr int SN = SORT * TB;
@@ -1890,6 +1910,7 @@ ao_trace_refill_kernel(DevScene S, DevWork W, uint64_t n) {
 template <int WPE, int LDS_D, int BUDGET2 = 0, int SRC = 0, int REREAD = 1, int SPEC = 0>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_late_kernel(DevScene S, DevWork W) {
+    if (frame_poisoned(W)) return;
     __shared__ uint32_t lstk[LDS_D][TB];
     const uint32_t half = W.ao_cap / 2;
     const uint32_t cnt = W.ao_late_count[SRC];
@@ -1989,6 +2010,7 @@ ao_late_kernel(DevScene S, DevWork W) {
 template <int WPE, int LDS_D>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_late_refill_kernel(DevScene S, DevWork W) {
+    if (frame_poisoned(W)) return;
     __shared__ uint32_t lstk[LDS_D][TB];
     const BvhView& V = S.bv;
     const uint32_t cnt = W.ao_late_count[0];
@@ -2103,6 +2125,7 @@ __device__ __forceinline__ unsigned long long audit_mix(float4 a, float4 b, uint
 __global__ void __launch_bounds__(TB) ao_audit_expect_kernel(DevScene S, DevWork W, uint64_t n, uint32_t c_lo,
                                                              uint32_t* exp, unsigned long long* aud,
                                                              unsigned long long* out) {
+    if (frame_poisoned(W)) return;
     for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TB) {
         const float4 r0 = W.ao_rays[2 * i], r1 = W.ao_rays[2 * i + 1];
         const uint32_t flag = __float_as_uint(r1.w);
@@ -2127,6 +2150,7 @@ __global__ void __launch_bounds__(TB) ao_audit_compare_kernel(DevScene S, DevWor
                                                               uint32_t N, uint64_t item0, uint64_t n,
                                                               const uint32_t* occ_before, const uint32_t* exp,
                                                               unsigned long long* aud, unsigned long long* out) {
+    if (frame_poisoned(W)) return;
     const uint32_t nq = S.bv.has_far ? W.far_count[0] : 0u;
     for (uint32_t j = blockIdx.x * TB + threadIdx.x; j < nc; j += gridDim.x * TB) {
         const uint32_t got = W.occ[c_lo + j] - occ_before[j];
@@ -2711,6 +2735,7 @@ __device__ __forceinline__ void cell_full_tests(const DevScene& S, const float4 
 // equal for >= 32: the scalar loads' latency is exposed per candidate. Not kept.)
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
 far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
+    if (frame_poisoned(W)) return;
     __shared__ float4 sray[TB / 64][64][2];
     __shared__ uint32_t shit[TB / 64][64];
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
@@ -2865,6 +2890,7 @@ __device__ __forceinline__ void cell_closest_tests(const DevScene& S, const floa
 // entry -> plane -> record chain per step.
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
 far_cell_closest_kernel(DevScene S, DevWork W) {
+    if (frame_poisoned(W)) return;
     __shared__ float4 sray[TB / 64][64][2];
     __shared__ unsigned long long sbest[TB / 64][64];
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
@@ -2977,6 +3003,7 @@ far_cell_closest_kernel(DevScene S, DevWork W) {
 template <int U = 1>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
 far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
+    if (frame_poisoned(W)) return;
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
     __shared__ FarTri ftile[TB / 64][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -3014,6 +3041,7 @@ far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
 // Per-lane variants (each lane walks its own path): better than the wave union
 // when the queue is too sparse for sorted waves to share a direction.
 __global__ void __launch_bounds__(TB) far_any_lane_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
+    if (frame_poisoned(W)) return;
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
         const uint32_t r = W.far_vals_alt[i];
         const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
@@ -3022,6 +3050,7 @@ __global__ void __launch_bounds__(TB) far_any_lane_kernel(DevScene S, DevWork W,
 }
 
 __global__ void __launch_bounds__(TB) far_closest_lane_kernel(DevScene S, DevWork W, uint32_t n) {
+    if (frame_poisoned(W)) return;
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
         const uint32_t r = W.far_vals_alt[i];
         const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
@@ -3057,6 +3086,7 @@ __device__ unsigned long long g_brute_stats[5];
 #endif
 __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uint32_t first, uint32_t n, int closest,
                                                       int n_far, int brute, uint8_t* flag) {
+    if (frame_poisoned(W)) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_scan = brute ? S.n_prims : n_far;
     for (uint32_t i = first + blockIdx.x * (TB / 64) + wave; i < n; i += gridDim.x * (TB / 64)) {
@@ -3187,6 +3217,7 @@ __global__ void __launch_bounds__(TB) far_scan_kernel(DevScene S, DevWork W, uin
 template <int R>
 __global__ void __launch_bounds__(TB) far_brute_split_kernel(DevScene S, DevWork W, uint32_t first, uint32_t nb,
                                                              uint32_t splits, unsigned long long* best) {
+    if (frame_poisoned(W)) return;
     // the group's rays and each lane's best (t, primitive) per ray, in LDS (a
     // register copy per ray would cost the kernel its occupancy)
     __shared__ float4 sray[TB / 64][R][2];
@@ -3245,6 +3276,7 @@ __global__ void __launch_bounds__(TB) far_brute_split_kernel(DevScene S, DevWork
 // beta, gamma), merged into the ray's provisional hit with the same rule.
 __global__ void __launch_bounds__(TB) far_brute_merge_kernel(DevScene S, DevWork W, uint32_t first, uint32_t nb,
                                                              const unsigned long long* best) {
+    if (frame_poisoned(W)) return;
     for (uint32_t r = blockIdx.x * TB + threadIdx.x; r < nb; r += gridDim.x * TB) {
         const unsigned long long key = best[r];
         if (key == ~0ull) continue;
@@ -3282,6 +3314,7 @@ __global__ void __launch_bounds__(TB) far_brute_merge_kernel(DevScene S, DevWork
 template <int R>
 __global__ void __launch_bounds__(TB) far_brute_any_split_kernel(DevScene S, DevWork W, uint32_t first, uint32_t nb,
                                                                  uint32_t splits, uint32_t* done, uint8_t* flag) {
+    if (frame_poisoned(W)) return;
     __shared__ float4 sray[TB / 64][R][2];  // the group's rays (register copies would cost occupancy)
     __shared__ int sfk[TB / 64][R];         // an accepting record per ray (the AO call hint)
     const int lane = threadIdx.x & 63;
@@ -3470,6 +3503,7 @@ static int far_mode(uint32_t nq) {
 // entry -> plane -> record per step.
 template <int U>
 __global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, uint32_t n) {
+    if (frame_poisoned(W)) return;
     __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
     __shared__ FarTri ftile[TB / 64][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -3542,6 +3576,7 @@ __device__ __forceinline__ rpix node_local(const DevScene& S, const DevFrame& F,
 }
 
 __global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, DevWork W, int16_t* __restrict__ fb) {
+    if (S.use_bvh && frame_poisoned(W)) return;
     const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
     const uint32_t p = blockIdx.x * TB + threadIdx.x;
     if (p >= npix) return;
@@ -3612,6 +3647,7 @@ __device__ __forceinline__ rpix node_val_load(const DevWork& W, int32_t id) {
 // the pixels, deeper ones name theirs in W.rays).
 __global__ void __launch_bounds__(TB) resolve_level_kernel(DevScene S, DevFrame F, DevWork W, int level,
                                                            int16_t* __restrict__ fb, uint32_t p_lo, uint32_t p_hi) {
+    if (S.use_bvh && frame_poisoned(W)) return;
     uint32_t base = p_lo, count = p_hi - p_lo;
     if (level > 0) {  // the trace's own clamp to the node capacity
         base = W.lvl[LVL_BASE + level];
@@ -3783,17 +3819,26 @@ static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStre
         }
         const uint32_t pos = (uint32_t)g_cs->pos | (g_cs->tag << 16);
         for (int i = 0; i < n; i++) out[i] = g_cs->vals[g_cs->pos++];
+#ifdef RT580_DIAGNOSTICS
+        // DIAGNOSTIC build only, RT580_REPLAY_CORRUPT: 1 makes every device
+        // check fail (the launches are still sized by the right counts); 2
+        // replays a wrong far-queue segment count itself (its capacity, the
+        // queue length), so the launches after it are sized by a count larger
+        // than the frame's and would cover stale entries (frame_poisoned, the
+        // bound in far_chunk_*_kernel: the call must end as RT_FAILURE, with no
+        // device fault)
+        static int corrupt = -1;
+        if (corrupt < 0) {
+            const char* ev = getenv("RT580_REPLAY_CORRUPT");
+            corrupt = ev ? atoi(ev) : 0;
+        }
+        if (corrupt == 2 && n == 1 && !strcmp(g_where, "far queue segments"))
+            out[0] = out[0] < cap0 ? cap0 : out[0] - 1u;
+#endif
         if (counts_fit(out, n, cap0, cap1) != hipSuccess) return hipErrorInvalidValue;
         uint32_t e0 = out[0];
 #ifdef RT580_DIAGNOSTICS
-        {   // DIAGNOSTIC build only: RT580_REPLAY_CORRUPT=1 makes every check fail (tests the detection)
-            static int corrupt = -1;
-            if (corrupt < 0) {
-                const char* ev = getenv("RT580_REPLAY_CORRUPT");
-                corrupt = ev ? atoi(ev) : 0;
-            }
-            if (corrupt) e0 ^= 1u;
-        }
+        if (corrupt == 1) e0 ^= 1u;
 #endif
         hipLaunchKernelGGL(count_check_kernel, dim3(1), dim3(64), 0, s, dev, e0, n > 1 ? out[1] : 0u, n, g_cs->bad,
                            pos);
@@ -3854,9 +3899,15 @@ small_sort_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict_
 // ceil(count / 64) chunks; chunk counts first (into far_keys_alt, free after
 // the run-length encoding), then, after their scan into far_wofs, one entry
 // per chunk naming its segment, and the total.
+// nseg is the host's (possibly replayed) count; both kernels also bound it by
+// the device's own (far_seg_n[0], written by the run-length encoding), so a
+// replayed count larger than the frame's never reads the stale entries beyond
+// it (their chunk counts would size work items past far_work's end).
 __global__ void far_chunk_count_kernel(DevWork W, uint32_t nseg) {
+    if (frame_poisoned(W)) return;
+    const uint32_t m = min(nseg, W.far_seg_n[0]);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nseg; k += gridDim.x * blockDim.x)
-        W.far_keys_alt[k] = (W.far_vals[k] + 63u) / 64u;
+        W.far_keys_alt[k] = k < m ? (W.far_vals[k] + 63u) / 64u : 0u;
 }
 // One descriptor per work item (sorted rays [x, y), the cell list's first
 // entry z and length w; w = ~0: a plane-tree segment), so the cell pass reads
@@ -3865,8 +3916,10 @@ __global__ void far_chunk_count_kernel(DevWork W, uint32_t nseg) {
 // light's shadow rays all share a cell) get their other items from the whole
 // wave. (A wave per segment: 265-350 us for the AO queue's ~3M segments.)
 __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, uint32_t n) {
+    if (frame_poisoned(W)) return;
     const int lane = threadIdx.x & 63;
     const int shift = 24 - 2 * S.bv.grid_log2;
+    nseg = min(nseg, W.far_seg_n[0]);  // (see far_chunk_count_kernel)
     for (uint32_t base = (blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64u; base < nseg;
          base += gridDim.x * blockDim.x) {
         const uint32_t k = base + (uint32_t)lane;
@@ -3908,6 +3961,7 @@ __global__ void far_chunk_expand_kernel(DevScene S, DevWork W, uint32_t nseg, ui
 // [r0, r1), the cell list's first entry and length, or ~0 for a plane-tree
 // key), in segment order; far_seg_n = (segments, work items).
 __global__ void __launch_bounds__(kSmallSortThreads) small_cells_kernel(DevScene S, DevWork W, uint32_t n) {
+    if (frame_poisoned(W)) return;
     using Scan = hipcub::BlockScan<uint32_t, kSmallSortThreads>;
     __shared__ typename Scan::TempStorage scan_tmp;
     __shared__ uint32_t seg_start[kSmallSort + 1];

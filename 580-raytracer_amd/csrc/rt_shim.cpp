@@ -652,6 +652,7 @@ DevWork dev_work() {
         w.call_hint = hint ? (uint32_t*)SL.call_hint.p : nullptr;
     }
     w.aofix_cap = (uint32_t)(SL.aofix_items.bytes / 8);
+    w.poison = (const uint32_t*)SL.bad.p;
     return w;
 }
 
@@ -707,6 +708,16 @@ int ensure_work(const rt_render_params* p, int n_rows) {
         ensure(SL.totals, 64) || ensure(SL.call_node, ccap * 4) || ensure(SL.call_rng, ccap * 8) ||
         ensure(SL.occ, ccap * 4) || ensure(SL.aofix_items, (size_t)8 << 20) || ensure(SL.aofix_count, 64))
         return RT_FAILURE;
+    // the slot's replay-check word (count_check_kernel sets it; DevWork::poison)
+    // and its pinned host copy: zero from the start, and again after a failure
+    if (!SL.bad.p) {
+        if (ensure(SL.bad, 64)) return RT_FAILURE;
+        HIP_TRY(hipMemsetAsync(SL.bad.p, 0, 64, fs()));
+    }
+    if (!SL.bad_host) {
+        HIP_TRY(hipHostMalloc((void**)&SL.bad_host, 64, hipHostMallocDefault));
+        std::memset(SL.bad_host, 0, 64);
+    }
     if (g.bvh_ok && !g.bvh.far_nodes.empty() && ensure(SL.call_hint, ccap * 4)) return RT_FAILURE;
     g.node_cap = (uint32_t)cap;
     g.call_cap = (uint32_t)ccap;
@@ -783,12 +794,6 @@ bool frame_verified(const rt_render_params* p) {
 
 int begin_schedule(CountSchedule& cs, bool replay) {
     if (replay) {
-        if (ensure(SL.bad, 64)) return RT_FAILURE;
-        if (!SL.bad_host) {
-            HIP_TRY(hipHostMalloc((void**)&SL.bad_host, 64, hipHostMallocDefault));
-            *SL.bad_host = 0;
-            HIP_TRY(hipMemsetAsync(SL.bad.p, 0, 64, fs()));
-        }
         cs.mode = CountSchedule::REPLAY;
         cs.pos = 0;
         cs.broken = false;

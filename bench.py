@@ -52,7 +52,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 # every 2 cycles, 2.4 GHz; HBM3E 8.0 TB/s.
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0   # 1228.8 G wave-instructions/s
 HBM_PEAK_GBS = 8000.0
-PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")  # newest committed counter profiles first
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03", "r02")  # newest committed counter profiles first
 
 # name -> (scene, synthetic?, width, height, depth, AO samples, label)
 WORKLOADS = {
@@ -259,7 +259,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     for i in range(warmup):
         step()
         finish()
-        if synth:
+        if synth and W * H > 1920 * 1080:
             torch.cuda.synchronize()
             log("%s: warmup step %d done" % (name, i))
     torch.cuda.synchronize()
@@ -277,7 +277,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
         if i == steps - 1:
             # the last frame's gather + de-interleave belong to the timed region
             last = finish() if dframe is not None else r
-        if synth and ctx.rank == 0:  # long frames: a progress line per enqueued step (no sync: frames overlap)
+        if synth and W * H > 1920 * 1080 and ctx.rank == 0:  # 4K/8K frames: a progress line per enqueued step
             log("%s: step %d enqueued" % (name, i))
     ctx.barrier()
     torch.cuda.synchronize()
@@ -491,21 +491,20 @@ def roofline(workload, k_ms, k_launches, k_rays, iso=None):
     """Roofline of the AO ray kernel (the scene query of every AO sample; 95 %
     of the frame's rays). Neither MFMA nor HBM bounds it (no dense
     contraction; the scene is re-read from L2/MALL, see `traffic`): it is
-    bound by VALU instruction issue. achieved = VALU wave-instructions per AO
-    ray (rocprofv3 SQ_INSTS_VALU per dispatch / AO rays per dispatch, from the
-    committed profile summary profiles/<round>/roofline_<workload>.json) x the AO
-    rays of one launch / that launch's mean duration, measured here with HIP
-    events around every launch on its own stream (rt_gpu_profile_ao_kernel).
-    peak = 1024 SIMDs x one wave64 VALU instruction per 2 cycles x 2.4 GHz."""
+    bound by VALU instruction issue; peak = 1024 SIMDs x one wave64 VALU
+    instruction per 2 cycles x 2.4 GHz.
+
+    frac / achieved: the committed rocprofv3 profile's own figure
+    (profiles/<round>/roofline_<workload>.json: SQ_INSTS_VALU per AO ray x AO
+    rays per launch / the kernel trace's mean launch duration), so the headline
+    is reproducible from profiles/. Beside it, this run's measurements of the
+    same launch with HIP events on its own stream (rt_gpu_profile_ao_kernel):
+    `isolated` (frames rendered one at a time: the kernel's own rate, which must
+    agree with the profile's mean -- `isolated_over_rocprof`) and `live_frac`
+    (the timed frames, whose AO phases overlap and stretch each other's
+    launches: a share of a shared chip, not the kernel's cost)."""
     res = {"kernel": "ao_kernel (AO ray scene query)", "bound": "valu", "unit": "Ginst/s",
            "peak": VALU_PEAK_GINST, "achieved": None, "frac": None, "traffic": None}
-    if k_launches <= 0 or k_ms <= 0:
-        res["note"] = "no AO kernel launch was timed"
-        return res
-    launch_s = k_ms / k_launches * 1e-3
-    rays_launch = k_rays / k_launches
-    res["launch_ms"] = round(launch_s * 1e3, 4)
-    res["ao_rays_per_launch"] = int(rays_launch)
     prof, path = None, None
     for rnd in PROFILE_ROUNDS:
         p = os.path.join(REPO, "profiles", rnd, "roofline_%s.json" % workload)
@@ -518,31 +517,30 @@ def roofline(workload, k_ms, k_launches, k_rays, iso=None):
     if not prof or not prof.get("valu_per_ao_ray"):
         res["note"] = "no committed counter profile for this workload (profiles/*/roofline_%s.json)" % workload
         return res
+    vpr = prof["valu_per_ao_ray"]
     res["kernel"] = prof["kernel"]
-    achieved = prof["valu_per_ao_ray"] * rays_launch / launch_s / 1e9
-    res["achieved"] = round(achieved, 2)
-    res["frac"] = round(achieved / VALU_PEAK_GINST, 4)
-    if prof.get("hbm_bytes_per_ao_ray") is not None:
-        traffic = prof["hbm_bytes_per_ao_ray"] * rays_launch
-        res["traffic"] = round(traffic)
-        res["hbm"] = {"achieved": round(traffic / launch_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                      "frac": round(traffic / launch_s / 1e9 / HBM_PEAK_GBS, 4)}
-    res["per_ray"] = {"valu_wave_insts": round(prof["valu_per_ao_ray"], 4),
-                      "hbm_bytes": prof.get("hbm_bytes_per_ao_ray")}
-    res["profile"] = {"file": os.path.relpath(path, REPO), "launch_ms_rocprof": prof.get("avg_ms"),
-                      "valu_issue_frac_rocprof": prof.get("valu_issue_frac"),
-                      "frame_share_rocprof": prof.get("frame_share"), "top_kernels": prof.get("top_kernels")}
+    if prof.get("avg_ms") and prof.get("ao_rays_per_launch"):
+        a = vpr * prof["ao_rays_per_launch"] / (prof["avg_ms"] * 1e-3) / 1e9
+        res["achieved"] = round(a, 2)
+        res["frac"] = round(a / VALU_PEAK_GINST, 4)
+        res["launch_ms"] = prof["avg_ms"]
+        res["ao_rays_per_launch"] = int(prof["ao_rays_per_launch"])
+        if prof.get("hbm_bytes_per_ao_ray") is not None:
+            traffic = prof["hbm_bytes_per_ao_ray"] * prof["ao_rays_per_launch"]
+            res["traffic"] = round(traffic)
+            res["hbm_frac"] = round(traffic / (prof["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    res["per_ray"] = {"valu_wave_insts": round(vpr, 3), "hbm_bytes": prof.get("hbm_bytes_per_ao_ray")}
+    res["profile"] = os.path.relpath(path, REPO)
+    if k_launches > 0 and k_ms > 0:
+        launch_s = k_ms / k_launches * 1e-3
+        res["live_frac"] = round(vpr * (k_rays / k_launches) / launch_s / 1e9 / VALU_PEAK_GINST, 4)
+        res["live_launch_ms"] = round(launch_s * 1e3, 4)
     if iso:
-        a_iso = prof["valu_per_ao_ray"] * iso["rays_per_launch"] / (iso["launch_ms"] * 1e-3) / 1e9
+        a_iso = vpr * iso["rays_per_launch"] / (iso["launch_ms"] * 1e-3) / 1e9
         res["isolated"] = {"launch_ms": round(iso["launch_ms"], 4), "ao_rays_per_launch": int(iso["rays_per_launch"]),
-                           "achieved": round(a_iso, 2), "frac": round(a_iso / VALU_PEAK_GINST, 4),
-                           "note": "the same kernel timed over %d further frames rendered one at a time (untimed; "
-                                   "each frame complete before the next is queued): no other frame's kernels beside "
-                                   "the launch" % iso["frames"]}
-    res["note"] = ("VALU-issue roofline: counter-measured VALU wave-instructions per AO ray x AO rays per launch "
-                   "/ live launch time (frames overlap: AO phases of consecutive frames may run together, which "
-                   "stretches each launch; `isolated` times it without that); traffic = FETCH_SIZE+WRITE_SIZE "
-                   "(x1 KiB) per AO ray x rays per launch (HBM is not the bound: see hbm.frac)")
+                           "frac": round(a_iso / VALU_PEAK_GINST, 4)}
+        if prof.get("avg_ms"):
+            res["isolated_over_rocprof"] = round(iso["launch_ms"] / prof["avg_ms"], 4)
     return res
 
 
@@ -663,6 +661,44 @@ def cpu_baseline(ctx, name, root, params, gpu_px, row_counts=None):
     return res
 
 
+def compact(rec):
+    """A sub-record's numbers in a few hundred bytes (the driver keeps the
+    tail of stdout: the whole line must stay short)."""
+    fc, rf, cb = rec.get("frame_check", {}), rec.get("roofline", {}), rec.get("cpu_baseline") or {}
+    return {"value": rec["value"], "unit": rec["unit"], "ms_per_step": rec["ms_per_step"], "steps": rec["steps"],
+            "rays_per_frame": rec["config"]["rays_per_frame"], "workload": rec["config"]["workload"],
+            "frame_check": {k: fc[k] for k in ("matches_reference", "matches_oracle_rows", "pixels_checked",
+                                               "matches_single_gpu") if k in fc},
+            "roofline": {k: rf.get(k) for k in ("kernel", "frac", "achieved", "launch_ms", "live_frac",
+                                                "isolated_over_rocprof", "profile")},
+            "render_call_ms": rec.get("render_call_ms"),
+            "cpu_baseline": {k: cb[k] for k in ("value", "cores", "kind", "matches_gpu_frame") if k in cb}}
+
+
+def headline(out):
+    """The printed line: the contract's keys first, the north-star and config-3
+    summaries right after the headline numbers, then the rest (sub-records
+    compact; --detail writes them in full)."""
+    first = ("metric", "value", "unit", "ms_per_step")
+    res = {k: out[k] for k in first}
+    for sub in ("north_star", "config3"):
+        if out.get(sub):
+            res[sub] = compact(out[sub])
+    for k, v in out.items():
+        if k not in res:
+            res[k] = v
+    rf = res.get("roofline")
+    if rf:
+        res["roofline"] = {k: v for k, v in rf.items()}
+    if res.get("cpu_baseline", {}).get("calibration"):
+        res["cpu_baseline"] = dict(res["cpu_baseline"])
+        res["cpu_baseline"].pop("calibration")
+    fc = res.get("frame_check")
+    if fc:
+        res["frame_check"] = {k: v for k, v in fc.items() if k not in ("segments", "oracle")}
+    return res
+
+
 def main():
     # a Python stack dump to stderr every $BENCH_WATCHDOG_S seconds (where a
     # GPU run is when it stops making progress)
@@ -686,6 +722,9 @@ def main():
     ap.add_argument("--no-north-star", action="store_true", help="skip the north_star sub-record (config2)")
     ap.add_argument("--no-config3", action="store_true", help="skip the config3 sub-record (config2)")
     ap.add_argument("--no-check", action="store_true", help="skip the reference-hash check of the last frame")
+    ap.add_argument("--detail", default=None,
+                    help="also write the full record (every sub-record in full) to this file; stdout keeps the "
+                         "compact line")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     ap.add_argument("--dist", action="store_true",
                     help="the multi-rank path (torch.distributed + DistFrame) even with one rank: rehearses the "
@@ -735,7 +774,10 @@ def main():
         if out is not None:
             out["config3"] = c3
     if out is not None:
-        print(json.dumps(out), file=json_out, flush=True)
+        if args.detail:
+            with open(args.detail, "w") as f:
+                json.dump(out, f, indent=1)
+        print(json.dumps(headline(out)), file=json_out, flush=True)
     if ctx.dist_on:
         ctx.dist.barrier()
         ctx.dist.destroy_process_group()

@@ -208,6 +208,66 @@ def test_replay_count_mismatch_fails_the_frame(tmp_path):
     assert "first mismatch: count #" in line[0] and "recorded" in line[0], line[0]
 
 
+_INFLATE_CHILD = r"""
+import ctypes, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import helpers
+rt580 = helpers.rt580()
+lib = rt580.load()
+rt = rt580.Raytracer(96, 54, helpers.synthetic_root("cornell10k"))
+assert rt.LoadSceneJSON("cornell10k.json") == 0
+rt.set_depth(2)
+rt.set_ao(16, True)
+codes, errs = [], []
+for k in range(6):
+    codes.append(rt.Render(""))
+    e = lib.rt_gpu_last_error()
+    errs.append(e.decode() if isinstance(e, bytes) else str(e))
+    if codes[-1] == 0:
+        np.save(sys.argv[2], rt.framebuffer())
+print("CODES", codes)
+for e in errs:
+    print("ERR", e)
+"""
+
+
+def test_replayed_segment_count_inflated_fails_without_fault(tmp_path):
+    """Diagnostic build, RT580_REPLAY_CORRUPT=2: a replayed far-queue segment
+    count is replaced by a larger one (the queue length), so the launches after
+    it are sized past the frame's segments and would read stale queue entries
+    (round 5's illegal memory access: far_chunk_expand_kernel wrote work items
+    past far_work from those entries' chunk counts). Every replayed frame must
+    end as RT_FAILURE naming the count, with no device fault: the process
+    keeps rendering, and the frames that record again equal the oracle's."""
+    import os
+    import subprocess
+    import sys
+    diag = os.path.join(helpers.REPO, "580-raytracer_amd", "lib580rt_diag.so")
+    if not os.path.exists(diag):
+        pytest.skip("diagnostic build absent (make diag)")
+    env = dict(os.environ, RT580_LIB=diag, RT580_REPLAY_CORRUPT="2")
+    script = tmp_path / "child.py"
+    script.write_text(_INFLATE_CHILD)
+    last = tmp_path / "last.npy"
+    r = subprocess.run([sys.executable, str(script), os.path.dirname(os.path.abspath(__file__)), str(last)], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [l for l in r.stdout.splitlines() if l.startswith("CODES")]
+    assert line, r.stdout + r.stderr
+    codes = eval(line[0][len("CODES "):])
+    errs = [l[4:] for l in r.stdout.splitlines() if l.startswith("ERR ")]
+    # the first frame records; every frame that replays the AO schedule fails (then records again)
+    assert set(codes) <= {0, 1} and codes[0] == 0 and codes.count(1) >= 2 and codes[-1] == 0, (codes, errs)
+    failed = [e for c, e in zip(codes, errs) if c == 1]
+    assert all("replayed count schedule" in e for e in failed), failed
+    assert any("far queue segments" in e for e in failed), failed
+    assert not any("illegal" in e or "fault" in e.lower() for e in errs), errs
+    assert "recorded" in failed[0] and "this frame" in failed[0]
+    ref, _ = helpers.oracle_render("cornell10k.json", 96, 54, 2, 16, True, root=helpers.synthetic_root("cornell10k"))
+    assert np.array_equal(np.load(last), ref), "the last recorded frame differs from the oracle"
+
+
 def test_accel_toggle_on_repeated_frame_keeps_rendering():
     """The same params on a resident BVH scene, rendered (verified, recorded),
     then again (replayed), then under RT_ACCEL_BRUTE and back under AUTO: the
