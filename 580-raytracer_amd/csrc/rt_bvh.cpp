@@ -14,18 +14,10 @@ namespace rt580 {
 namespace {
 
 constexpr int kBins = 16;
-// triangles per spatial leaf (RT580_LEAF_MAX, 1..8, for A/B). 2: a wave's
-// lanes test fewer triangles per leaf step (tools/simd_sim.cpp); AO
-// cornell10k 82.5 -> 80.9 ms, field100k 1080p 61.4 -> 59.1 ms against 4.
-static int leaf_max() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("RT580_LEAF_MAX");
-        v = e ? std::atoi(e) : 2;
-        if (v < 1 || v > 8) v = 2;
-    }
-    return v;
-}
+// triangles per spatial leaf. 2: a wave's lanes test fewer triangles per leaf
+// step (tools/simd_sim.cpp); AO cornell10k 82.5 -> 80.9 ms, field100k 1080p
+// 61.4 -> 59.1 ms against 4.
+static int leaf_max() { return 2; }
 constexpr int kFarLeaf = 8;   // planes per far-tree leaf
 constexpr int kSahDepth = 40; // below this depth: median splits (bounded stack)
 constexpr double kU = 5.9604644775390625e-08;  // 2^-24
@@ -301,9 +293,7 @@ struct FarBuilder {
 bool build_bvh(const rt_prim* prims, int n, BvhBuild& out) {
     const auto t0 = std::chrono::steady_clock::now();
     out = BvhBuild();
-    const char* env = std::getenv("RT580_BVH_INFLATE");
-    out.inflate = env ? std::atof(env) : 0.0;
-    if (!(out.inflate >= 0)) out.inflate = 0.0;
+    out.inflate = 0.0;
     float S = 0.0f;
     for (int i = 0; i < n; i++) {
         const rt_prim& p = prims[i];
@@ -610,8 +600,7 @@ void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells) {
     if (out.far_tris.empty() || log2_cells <= 0) return;
     const int L = log2_cells, M = 1 << L;
     const double S = out.scale;
-    double rmul = 4.0;  // (RT580_GRID_R: A/B of the origin radius, in units of S)
-    if (const char* e = std::getenv("RT580_GRID_R")) rmul = std::atof(e);
+    constexpr double rmul = 4.0;  // the origin radius, in units of S
     const double R = rmul * S;  // origins on (or 0.2 off) the scene's surfaces; farther ones walk the plane tree
     std::vector<GridTri> gt(out.far_tris.size());
     std::vector<uint8_t> ok(out.far_tris.size());

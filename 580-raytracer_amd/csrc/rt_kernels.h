@@ -95,7 +95,6 @@ struct DevWork {
     uint32_t* occ;         // [call_cap] occluded samples
     const uint32_t* mt_stream;  // mt19937 draws [mt_base, ...) of the serial stream, else null
     uint64_t mt_base;      // absolute index (in the serial stream) of mt_stream[0]
-    uint32_t refill_min;   // RT580_AO_REFILL_MIN: idle lanes a persistent-lane wave refills at once
     uint32_t node_cap;
     uint32_t call_cap;
     // BVH scenes: AO rays that miss every near triangle, queued for the sorted
@@ -125,11 +124,11 @@ struct DevWork {
     // ao_trace_kernel (item index in the chunk), finished by ao_late_kernel
     uint32_t* ao_late;       // [ao_cap] or null
     uint32_t* ao_late_count; // [1]
-    // the walk state of late rays [0, ao_state_cap) of each late queue (region
-    // 0: ao_trace_kernel's, region 1: a budgeted ao_late_kernel's), resumed by
-    // the next level instead of starting over: per slot kLateWords words -- the
-    // entry about to be descended (c), n | sp << 8 (~0: not saved, the stack was
-    // deeper than kLateSaved), then the stack [0, sp). Null: late rays start over.
+    // the walk state of late rays [0, ao_state_cap) of the late queue, saved by
+    // ao_trace_kernel and resumed by ao_late_kernel instead of starting over:
+    // per slot kLateWords words -- the entry about to be descended (c), n | sp << 8
+    // (~0: not saved, the stack was deeper than kLateSaved), then the stack
+    // [0, sp). Rays past ao_state_cap start over.
     uint32_t* ao_state;
     uint32_t ao_state_cap;
     // provisional closest hits of the tree rays (node id) between the near and

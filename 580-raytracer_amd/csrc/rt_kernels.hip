@@ -71,7 +71,6 @@ __device__ __forceinline__ uint32_t mersenne31_mul(uint32_t a, uint32_t b) {
 }
 
 __constant__ uint32_t c_minstd_j1[512];    // 16807^(2s+1) mod m: state offset of sample s's first draw
-__constant__ uint32_t c_xcd_order = 0u;    // xcd_block on (RT580_XCD_ORDER=1, A/B only: measured slower; set at rt_gpu_init)
 
 
 // generate_canonical<float,24> (libstdc++ random.tcc:3348-3378) for one draw.
@@ -457,106 +456,6 @@ __device__ __forceinline__ FarTri load_far_tri(const FarTri* tris, int j) {
     return t;
 }
 
-// ---------------------------------------------------------------- wave-cooperative near any-hit
-// bvh_any's near part (brute list + spatial BVH, rt_isect.h) for the 64 rays
-// of a wave at once: the wave walks one node sequence with wave-uniform scalar
-// node loads; a child is entered if the fat-ray slab test of any lane that is
-// still undecided meets its box, and only those lanes (a 64-bit mask kept with
-// the stack entry) continue below it. Each lane runs the unchanged per-ray slab
-// and triangle tests, so a lane's set of tested triangles contains everything
-// its own per-lane traversal would test (the culling is conservative for every
-// lane), and its boolean is the same. Suited to coherent waves: the samples of
-// one AO call (common origin), the shadow rays of neighbouring pixels toward
-// one directional light (common direction).
-// Every lane of the wave must call it (convergent); `active` selects the rays.
-struct WaveEntry {
-    int32_t c, n;
-    uint32_t m_lo, m_hi;
-};
-#define RT_WAVE_STACK RT_BVH_STACK
-
-__device__ __forceinline__ BvhNode load_bvh_node_scalar(const BvhNode* nodes, int j) {
-    const cu32_ptr src = (cu32_ptr)(nodes + j);
-    BvhNode nd;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&nd);
-#pragma unroll
-    for (int k = 0; k < 16; k++) dst[k] = src[k];
-    return nd;
-}
-
-__device__ bool bvh_any_near_wave(const BvhView& V, bool active, rv3 o, rv3 d, WaveEntry* stk) {
-    const int lane = threadIdx.x & 63;
-    bool hit = false;
-    for (int k = 0; k < V.n_brute; k++) {  // spheres + unanalysable triangles, every ray
-        if (__ballot(active && !hit) == 0) break;
-        const int j = (int)__builtin_amdgcn_readfirstlane(V.brute[k]);
-        const rt_prim P = load_prim_scalar(V.all, j);
-        if (active && !hit) hit = prim_test_any(P, o, d);
-    }
-    if (!V.has_tree) return hit;
-    bool live = active && !hit && !dir_zero(d);
-    if (__ballot(live) == 0) return hit;
-    const SlabRay sr = slab_ray(V, o, d);
-    int sp = 0;
-    int32_t c = 0, n = 0;  // root (internal)
-    for (;;) {
-        if (n == 0) {
-            const BvhNode nd = load_bvh_node_scalar(V.nodes, c);
-            float t0, t1;
-            const bool h0 = live && nd.n0 >= 0 && slab(nd.lo0, nd.hi0, sr, t0);
-            const bool h1 = live && nd.n1 >= 0 && slab(nd.lo1, nd.hi1, sr, t1);
-            const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
-            if (b0 && b1) {
-                // the child more lanes need first (any order gives the same booleans)
-                const bool first0 = __popcll(b0) >= __popcll(b1);
-                const uint64_t mp = first0 ? b1 : b0;
-                WaveEntry e;
-                e.c = first0 ? nd.c1 : nd.c0;
-                e.n = first0 ? nd.n1 : nd.n0;
-                e.m_lo = (uint32_t)mp;
-                e.m_hi = (uint32_t)(mp >> 32);
-                stk[sp] = e;  // every lane writes the same value
-                sp++;
-                c = first0 ? nd.c0 : nd.c1;
-                n = first0 ? nd.n0 : nd.n1;
-                live = ((first0 ? b0 : b1) >> lane) & 1ull;
-                continue;
-            }
-            if (b0 || b1) {
-                c = b0 ? nd.c0 : nd.c1;
-                n = b0 ? nd.n0 : nd.n1;
-                live = ((b0 ? b0 : b1) >> lane) & 1ull;
-                continue;
-            }
-        } else {
-            for (int k = c; k < c + n; k++) {
-                const rt_prim P = load_prim_scalar(V.prims, k);
-                float t, a, b, g;
-                if (live && tri_test<false, true>(P, o, d, t, a, b, g)) {
-                    hit = true;
-                    live = false;
-                }
-                if (__ballot(live) == 0) break;
-            }
-        }
-        bool resumed = false;
-        while (sp > 0) {
-            sp--;
-            const WaveEntry e = stk[sp];
-            const uint64_t m = ((uint64_t)e.m_hi << 32) | e.m_lo;
-            live = ((m >> lane) & 1ull) && !hit;
-            if (__ballot(live)) {
-                c = __builtin_amdgcn_readfirstlane(e.c);
-                n = __builtin_amdgcn_readfirstlane(e.n);
-                resumed = true;
-                break;
-            }
-        }
-        if (!resumed) break;
-    }
-    return hit;
-}
-
 // ---------------------------------------------------------------- trace (one tree level)
 __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { return F.row_begin + lr * F.row_step; }
 
@@ -570,22 +469,22 @@ __device__ __forceinline__ int pixel_frame_row(const DevFrame& F, int lr) { retu
 // [i0, i1) of the level.
 // SCALAR (small brute-force scenes): wave-uniform scalar scene loads and the
 // division-free sign rejections (tri_test<SIGN>) instead of the LDS tile.
-template <class STK, class TSTK>
-__device__ bool bvh4_closest_spec(const BvhView& V, bool live, rv3 o, rv3 d, Hit& h, const STK& stk, const TSTK& tstk);
 
 template <int HOLD2, bool BOUND, class STK>
 __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const STK& stk, int budget, bool live,
                                           int& sp, int32_t& c, int32_t& n, float tmax = INFINITY);
 
-// TSPEC (BVH): the near walks in speculative form -- PHASE 1 the closest-hit
-// walk (bvh4_closest_spec), PHASE 3 the shadow rays' bounded any-hit walk.
-// WPE > 0: an occupancy target (small-scene A/B, RT580_SMALL_TRACE_WPE).
-template <bool BVH, int PHASE, bool SCALAR = false, bool TSPEC = false, int WPE = 0>
-__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
-                                                   uint32_t i1, int light = 0, int dl = 0, int wave_near = 0) {
+// PHASE 3 (shadow rays) walks the 4-wide tree in speculative while-while form
+// (bvh4_any_spec_budget_state, the whole wave; profiles/r05/ab/trace_spec.txt:
+// 283.5 -> 271.9 us per launch on the north-star frame, 451 -> 404 us on
+// Cornell). The closest-hit walk of PHASE 1 stays per lane: its speculative
+// form was slower (392 -> 526 us), its descents running with the bound of
+// before the held leaf's test, which is what prunes most of the tree.
+template <bool BVH, int PHASE, bool SCALAR = false>
+__global__ void __launch_bounds__(TB) trace_kernel(DevScene S, DevFrame F, DevWork W, int level, uint32_t i0,
+                                                   uint32_t i1, int light = 0, int dl = 0) {
     if (BVH && frame_poisoned(W)) return;
     __shared__ rt_prim tile[TILE];
-    __shared__ WaveEntry wstk[PHASE == 3 ? TB / 64 : 1][RT_WAVE_STACK];
     // the near queries' traversal stacks (4-wide tree): the first NEAR_LDS
     // entries of each lane in LDS, one column per lane (PHASE 1: node links
     // and entry distances; PHASE 3: node links), the rest in scratch
@@ -629,11 +528,7 @@ __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE > 0
             const FarNode root = load_far_node(S.bv.far_nodes, 0);
             const bool brute = active && far_origin(S, o);
             bool nh = false;
-            if (TSPEC && S.bv.nodes4) {  // the whole wave walks (speculative form)
-                uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS], ta[RT_BVH_STACK + 4 - NEAR_LDS];
-                nh = bvh4_closest_spec(S.bv, active && !brute, o, d, h, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa},
-                                       LdsStack<NEAR_LDS, TB>{&ntstk[0][threadIdx.x], ta});
-            } else if (active && !brute) {
+            if (active && !brute) {
                 if (S.bv.nodes4) {
                     uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS], ta[RT_BVH_STACK + 4 - NEAR_LDS];
                     nh = bvh4_closest_near_s(S.bv, o, d, h, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa},
@@ -700,20 +595,13 @@ __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE > 0
                 }
                 lit = true;
             }
-            // per lane, or (wave_near, A/B) one wave-cooperative near traversal:
-            // neighbouring pixels' shadow rays share a directional light's direction
             bool nh;
-            if (wave_near && isinf(tmax)) {
-                nh = bvh_any_near_wave(S.bv, lit && !brute, so, L2, wstk[threadIdx.x >> 6]);
-            } else if (TSPEC && S.bv.nodes4) {  // the whole wave walks (speculative form)
+            if (S.bv.nodes4) {  // the whole wave walks (speculative form)
                 uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS];
                 int ssp = 0;
                 int32_t sc = 0, sn = 0;
                 nh = bvh4_any_spec_budget_state<0, true>(S.bv, so, L2, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa},
                                                          1 << 30, lit && !brute, ssp, sc, sn, tmax) > 0;
-            } else if (S.bv.nodes4) {
-                uint32_t sa[RT_BVH_STACK + 4 - NEAR_LDS];
-                nh = lit && !brute && bvh4_any_near_s(S.bv, so, L2, LdsStack<NEAR_LDS, TB>{&nstk[0][threadIdx.x], sa}, tmax);
             } else {
                 nh = lit && !brute && bvh_any_near(S.bv, so, L2, tmax);
             }
@@ -1124,23 +1012,14 @@ __device__ __forceinline__ void ao_sample(const DevScene& S, const DevFrame& F, 
             v = v3(vx, vy, z);
         } else {
             double sa, ca;
-#ifdef RT580_DIAGNOSTICS
-            if (VARIANT & 64) { sa = ang; ca = z; }  // DIAGNOSTIC build only (wrong output)
-            else
-#endif
             rt_glibc_sincos_simd_t(sct, (double)ang, &sa, &ca);
             v = v3((float)((double)r * ca), (float)((double)r * sa), z);
         }
-#ifdef RT580_DIAGNOSTICS
-        constexpr bool skip_norm = (VARIANT & 128) != 0;  // DIAGNOSTIC build only (wrong output)
-#else
-        constexpr bool skip_norm = false;
-#endif
-        if (!skip_norm) v = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
+        v = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
         if (!(v3_dot(v, n) > 0.0f)) v = v3_neg(v);
         o = v3_add(hp, v3_scale(v, 0.2f));
         // Ray constructor (Raytracer.h:431-433)
-        d = skip_norm ? v : ((VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v));
+        d = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
         if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o);
     }
 }
@@ -1150,7 +1029,6 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                                         uint64_t item_begin = 0, uint64_t item_end = ~0ull) {
     __shared__ rt_prim tile[TILE];
     __shared__ double sct_lds[440];  // glibc __sincostab, staged once per workgroup
-    __shared__ WaveEntry ao_wstk[(VARIANT & 8192) ? TB / 64 : 1][RT_WAVE_STACK];
     const double* sct = rt_dev::rt_sincostab;
     if (VARIANT & 1) {
         for (int i = threadIdx.x; i < 440; i += TB) sct_lds[i] = rt_dev::rt_sincostab[i];
@@ -1217,14 +1095,10 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
 #pragma unroll
             for (int k = 0; k < SPL; k++)
                 hit[k] =
-#ifdef RT580_DIAGNOSTICS
-                    (VARIANT & 32) ? (d[k].x > 2.0f) :  // DIAGNOSTIC build only (wrong output)
-#endif
-                    (VARIANT & 8192) ? bvh_any_near_wave(S.bv, active[k] && !ao_brute[k], o[k], d[k], ao_wstk[threadIdx.x >> 6])
 #ifdef RT580_DIAG_NO_NEAR
-                  : (VARIANT & 512) ? (active[k] && !ao_brute[k])  // DIAGNOSTIC build only: every AO ray occluded, no traversal
+                    (VARIANT & 512) ? (active[k] && !ao_brute[k]) :  // DIAGNOSTIC build only: every AO ray occluded, no traversal
 #endif
-                  : (VARIANT & 512) ? (active[k] && !ao_brute[k] && bvh_any_near(S.bv, o[k], d[k]))
+                    (VARIANT & 512) ? (active[k] && !ao_brute[k] && bvh_any_near(S.bv, o[k], d[k]))
                   : (VARIANT & 8) ? any_hit_scalar<(VARIANT & 4) != 0>(S, active[k], o[k], d[k])
                                   : any_hit<(VARIANT & 4) != 0>(S, tile, resident, active[k], o[k], d[k]);
         }
@@ -1234,10 +1108,6 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
     }
 }
 
-template <int VARIANT>
-__global__ void __launch_bounds__(TB) ao_kernel(DevScene S, DevFrame F, DevWork W) {
-    ao_body<VARIANT>(S, F, W);
-}
 
 // ---------------------------------------------------------------- AO fix-up
 // Samples of ao_body<... | 4096> whose fast rounding test failed (rt_libm.h
@@ -1311,12 +1181,6 @@ __global__ void __launch_bounds__(TB) ao_fix_kernel(DevScene S, DevFrame F, DevW
         const double X = (double)r * ca, Y = (double)r * sa;
         if (!(rt_f32_round_safe(X, (float)X) && rt_f32_round_safe(Y, (float)Y))) ao_fix_item(S, F, W, item);
     }
-}
-
-// BVH scenes: near any-hit of AO items [b, e); misses are queued (far pass below).
-__global__ void __launch_bounds__(TB) ao_near_kernel(DevScene S, DevFrame F, DevWork W, uint64_t b, uint64_t e) {
-    if (frame_poisoned(W)) return;
-    ao_body<512 | 1024 | 2048 | 4096>(S, F, W, b, e);
 }
 
 // Occupancy-capped flavours of ao_near_kernel (RT580_NEAR_WPE=0|5|6|8 for A/B;
@@ -1462,222 +1326,86 @@ __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const 
     return bvh4_any_spec_walk<HOLD2, BOUND>(V, o, d, stk, budget, live, sp, c, n, tmax);
 }
 
-// bvh4_closest_near_s in speculative while-while form (the closest-hit walk
-// of the trace levels' near phase; see bvh4_any_spec_walk): a lane that holds
-// a leaf goes on descending while the wave's other lanes look for theirs, with
-// the culling bound it has (h.t only shrinks, so a stale bound visits more,
-// never less); the leaf phase tests the held leaf and the current entry if it
-// is a leaf, each skipped when its entry t is already beyond h.t. The result is
-// the lexicographic minimum of (t, primitive) over the same candidates: the
-// order of the tests does not change it (lex_better).
-template <class STK, class TSTK>
-__device__ __forceinline__ bool spec_pop_closest(const STK& stk, const TSTK& tstk, int& sp, int32_t& c, int32_t& n,
-                                                 float& ct, bool found, float ht) {
-    while (sp > 0) {
-        sp--;
-        const float te = rt_bits_f32(tstk.get_lds_first(sp));
-        if (found && te > ht) continue;
-        const uint32_t e = stk.get_lds_first(sp);
-        c = (int32_t)(e & 0x7ffffffu);
-        n = (int32_t)(e >> 27);
-        ct = te;
-        return true;
-    }
-    return false;
-}
-
-__device__ __forceinline__ void spec_leaf_closest(const BvhView& V, rv3 o, rv3 d, int32_t c, int32_t n, Hit& h,
-                                                  bool& found) {
-    for (int k = c; k < c + n; k++) {
-        rt_prim P;
-        load_prim(V.prims + k, P);
-        float t, a, b, g;
-        if (tri_test<true, true>(P, o, d, t, a, b, g, found ? h.t : INFINITY)) {
-            const int id = (int)V.ids[k];
-            if (lex_better(t, id, found, h)) {
-                found = true;
-                h.t = t; h.a = a; h.b = b; h.g = g; h.prim = id;
-            }
-        }
-    }
-}
-
-// Whole wave; inactive lanes pass live = false.
-template <class STK, class TSTK>
-__device__ bool bvh4_closest_spec(const BvhView& V, bool live, rv3 o, rv3 d, Hit& h, const STK& stk,
-                                  const TSTK& tstk) {
-    bool found = false;
-    h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
-    if (!live) return false;
-    for (int k = 0; k < V.n_brute; k++) {
-        const int j = (int)V.brute[k];
-        float t, a, b, g;
-        if (prim_test_closest(V.all[j], o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, j, found, h)) {
-            found = true;
-            h.t = t; h.a = a; h.b = b; h.g = g; h.prim = j;
-        }
-    }
-    if (!V.has_tree || dir_zero(d)) return found;
-    const SlabRay sr = slab_ray(V, o, d);
-    int sp = 0;
-    int32_t c = 0, n = 0;  // root (internal); n < 0: nothing left
-    float ct = 0.0f;       // the current entry's t
-    int32_t pc = 0, pn = 0;
-    float pt = 0.0f;       // the held leaf and its entry t
-    while (live) {
-        for (;;) {  // node phase
-            if (pn == 0 && n > 0) {
-                pc = c;
-                pn = n;
-                pt = ct;
-                if (!spec_pop_closest(stk, tstk, sp, c, n, ct, found, h.t)) n = -1;
-            }
-            if (!__any(pn == 0 && n == 0)) break;
-            if (n == 0) {
-                Node4 nd;
-                float t[4];
-                bool ok[4];
-                node4_slab(V.nodes4 + c, sr, t, ok, nd.link);
-#pragma unroll
-                for (int j = 0; j < 4; j++) ok[j] = (nd.link[j] != 0xffffffffu) & ok[j] & (!found || t[j] <= h.t);
-                int best = -1;
-                float bt = INFINITY;
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (ok[j] & ((best < 0) | (t[j] < bt))) {
-                        best = j;
-                        bt = t[j];
-                    }
-                bool take[4];
-                uint32_t tb[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    take[j] = ok[j] & (j != best);
-                    tb[j] = rt_f32_bits(t[j]);
-                }
-                int sp2 = sp;
-                stk.push4(sp2, nd.link, take);
-                tstk.push4(sp, tb, take);
-                if (best >= 0) {
-                    const uint32_t e = best == 0 ? nd.link[0] : best == 1 ? nd.link[1] : best == 2 ? nd.link[2] : nd.link[3];
-                    c = (int32_t)(e & 0x7ffffffu);
-                    n = (int32_t)(e >> 27);
-                    ct = bt;
-                } else if (!spec_pop_closest(stk, tstk, sp, c, n, ct, found, h.t)) {
-                    n = -1;
-                }
-            }
-        }
-        // leaf phase
-        if (pn > 0) {
-            if (!(found && pt > h.t)) spec_leaf_closest(V, o, d, pc, pn, h, found);
-            pn = 0;
-            if (n > 0) {
-                if (!(found && ct > h.t)) spec_leaf_closest(V, o, d, c, n, h, found);
-                if (!spec_pop_closest(stk, tstk, sp, c, n, ct, found, h.t)) n = -1;
-            }
-        }
-        if (n < 0) live = false;
-    }
-    return found;
-}
-
-// XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs
-// (MI355X_MICROARCH.md, workgroup dispatch: b and b + 8 share an XCD and its
-// 4 MiB L2), so consecutive blocks of work land on 8 different L2s. With
-// xcd_block the grid's G / 8 workgroups of one XCD take G / 8 consecutive
-// blocks per grid-stride round instead: an XCD's resident workgroups then
-// trace rays of a narrow band of neighbouring AO calls and share the BVH
-// nodes and leaf triangles they read. Speed only: a permutation of [0, G).
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t G) {
-    if (!c_xcd_order || (G & 7u)) return b;
-    return (b & 7u) * (G >> 3) + (b >> 3);
-}
-
-// Split AO pass (default for BVH scenes): ao_near_kernel_w<.., V | 16384>
-// writes each item's ray (W.ao_rays), this kernel runs the near any-hit query
-// over the 4-wide tree with nothing else live, then ao_finish. Rays
-// [0, e - b) of the chunk whose first item is b.
-// LDS_D > 0: the first LDS_D traversal-stack entries of each lane live in LDS.
-// SORT > 0: the workgroup takes SORT * TB consecutive samples (SORT * TB / N
-// calls of neighbouring pixels) at a time and traces them in the order of a
-// counting sort by octahedral direction cell (8 x 8): a wave then holds rays
-// of similar direction from nearby origins, which share more of their paths
-// (tools/simd_sim.cpp "block sort"). Hits are then counted per lane.
-// BUDGET > 0: a lane gives up after BUDGET leaf visits; its item goes to
-// W.ao_late (ao_late_kernel re-runs the full query), so a wave is not held by
-// its few long traversals (tools/simd_sim.cpp "budget").
-// SPEC: the budgeted walk in speculative while-while form (bvh4_any_spec_budget_state);
-// 2: holding up to two leaves.
-template <int WPE, int LDS_D = 0, int SORT = 0, int KL = 3, int BUDGET = 0, int SPEC = 0>
+// Split AO pass of BVH scenes: ao_near_kernel_w<.., V | 16384> writes each
+// item's ray (W.ao_rays); this kernel runs the near any-hit query over the
+// 4-wide tree with nothing else live, then ao_finish. Rays [0, n) of the chunk.
+// LDS_D: the first LDS_D traversal-stack entries of each lane live in LDS (a
+//   column per lane), the rest in scratch.
+// SORT: the workgroup takes SORT * TB consecutive samples (SORT * TB / N calls
+//   of neighbouring pixels) at a time and traces them in the order of an LDS
+//   counting sort by octahedral direction cell (2^KL x 2^KL): a wave then holds
+//   rays of similar direction from nearby origins, which share more of their
+//   paths (tools/simd_sim.cpp "block sort"). Hits are counted per lane.
+// BUDGET: a lane gives up after BUDGET leaf visits; its item and its walk so
+//   far (W.ao_state) go to W.ao_late, and ao_late_kernel resumes the walk, so
+//   a wave is not held by its few long traversals (tools/simd_sim.cpp "budget").
+// The walk is in speculative while-while form (bvh4_any_spec_budget_state).
+template <int WPE, int LDS_D, int SORT, int KL, int BUDGET>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
-ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
+ao_trace_kernel(DevScene S, DevWork W, uint64_t n) {
+    static_assert(LDS_D > 0 && SORT > 0 && BUDGET > 0, "LDS stack, block sort, step budget");
     if (frame_poisoned(W)) return;
-    __shared__ uint32_t lstk[LDS_D > 0 ? LDS_D : 1][TB];
-    constexpr int SN = SORT > 0 ? SORT * TB : 1;
+    __shared__ uint32_t lstk[LDS_D][TB];
+    constexpr int SN = SORT * TB;
     constexpr int NB = 1 << (2 * KL);  // direction cells
     __shared__ uint32_t s_order[SN];
-    __shared__ uint32_t s_bin[SORT > 0 ? NB + 1 : 1];
-    const uint64_t span = SORT > 0 ? (uint64_t)SN : (uint64_t)TB;
-    for (uint64_t blk = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * span; blk < n; blk += (uint64_t)gridDim.x * span)
-    for (int round = 0; round < (SORT > 0 ? SORT : 1); round++) {
-        uint64_t i = blk + threadIdx.x;
-        if (SORT > 0) {
-            if (round == 0) {
-                // counting sort of the block's samples by direction cell
-                __syncthreads();
-                for (int k = threadIdx.x; k < NB + 1; k += TB) s_bin[k] = 0;
-                __syncthreads();
-                uint32_t key[SORT > 0 ? SORT : 1];
+    __shared__ uint32_t s_bin[NB + 1];
+    __shared__ uint32_t s_wsum[TB / 64];
+    for (uint64_t blk = (uint64_t)blockIdx.x * SN; blk < n; blk += (uint64_t)gridDim.x * SN)
+    for (int round = 0; round < SORT; round++) {
+        if (round == 0) {
+            // counting sort of the block's samples by direction cell
+            __syncthreads();
+            for (int k = threadIdx.x; k < NB + 1; k += TB) s_bin[k] = 0;
+            __syncthreads();
+            uint32_t key[SORT];
 #pragma unroll
-                for (int q = 0; q < SORT; q++) {
-                    const uint64_t j = blk + (uint64_t)q * TB + threadIdx.x;
-                    key[q] = NB;  // past the end: last
-                    if (j < n) {
-                        const float4 r1 = W.ao_rays[2 * j + 1];
-                        key[q] = grid_cell(v3(r1.x, r1.y, r1.z), KL);
-                    }
-                    atomicAdd(&s_bin[key[q]], 1u);
+            for (int q = 0; q < SORT; q++) {
+                const uint64_t j = blk + (uint64_t)q * TB + threadIdx.x;
+                key[q] = NB;  // past the end: last
+                if (j < n) {
+                    const float4 r1 = W.ao_rays[2 * j + 1];
+                    key[q] = grid_cell(v3(r1.x, r1.y, r1.z), KL);
                 }
-                __syncthreads();
-                {   // exclusive scan of the NB + 1 bins: runs of PER bins per thread,
-                    // their sums scanned across the wave (shuffles) and the waves (LDS)
-                    constexpr int PER = (NB + 1 + TB - 1) / TB;
-                    __shared__ uint32_t s_wsum[TB / 64];
-                    const int k0 = threadIdx.x * PER;
-                    uint32_t run = 0;
-#pragma unroll
-                    for (int q = 0; q < PER; q++)
-                        if (k0 + q < NB + 1) run += s_bin[k0 + q];
-                    const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
-                    uint32_t inc = run;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
-                        if (ln >= o) inc += v;
-                    }
-                    if (ln == 63) s_wsum[wv] = inc;
-                    __syncthreads();
-                    uint32_t acc = inc - run;
-                    for (int w2 = 0; w2 < wv; w2++) acc += s_wsum[w2];
-#pragma unroll
-                    for (int q = 0; q < PER; q++)
-                        if (k0 + q < NB + 1) {
-                            const uint32_t c = s_bin[k0 + q];
-                            s_bin[k0 + q] = acc;
-                            acc += c;
-                        }
-                }
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < SORT; q++) {
-                    const uint32_t pos = atomicAdd(&s_bin[key[q]], 1u);
-                    s_order[pos] = (uint32_t)(q * TB + threadIdx.x);
-                }
-                __syncthreads();
+                atomicAdd(&s_bin[key[q]], 1u);
             }
-            i = blk + s_order[round * TB + threadIdx.x];
+            __syncthreads();
+            {   // exclusive scan of the NB + 1 bins: runs of PER bins per thread,
+                // their sums scanned across the wave (shuffles) and the waves (LDS)
+                constexpr int PER = (NB + 1 + TB - 1) / TB;
+                const int k0 = threadIdx.x * PER;
+                uint32_t run = 0;
+#pragma unroll
+                for (int q = 0; q < PER; q++)
+                    if (k0 + q < NB + 1) run += s_bin[k0 + q];
+                const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+                uint32_t inc = run;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
+                    if (ln >= o) inc += v;
+                }
+                if (ln == 63) s_wsum[wv] = inc;
+                __syncthreads();
+                uint32_t acc = inc - run;
+                for (int w2 = 0; w2 < wv; w2++) acc += s_wsum[w2];
+#pragma unroll
+                for (int q = 0; q < PER; q++)
+                    if (k0 + q < NB + 1) {
+                        const uint32_t c = s_bin[k0 + q];
+                        s_bin[k0 + q] = acc;
+                        acc += c;
+                    }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < SORT; q++) {
+                const uint32_t pos = atomicAdd(&s_bin[key[q]], 1u);
+                s_order[pos] = (uint32_t)(q * TB + threadIdx.x);
+            }
+            __syncthreads();
         }
+        const uint64_t i = blk + s_order[round * TB + threadIdx.x];
         float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
         if (i < n) {
             r0 = W.ao_rays[2 * i];
@@ -1686,255 +1414,71 @@ ao_trace_kernel(DevScene S, DevWork W, uint32_t N, uint64_t n) {
         const uint32_t flag = __float_as_uint(r1.w);
         const bool active = flag != 0u, ao_brute = flag == 2u;
         const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
-        bool hit, late = false;
-        if (BUDGET > 0 && LDS_D > 0) {
-            uint32_t stk_a[RT_BVH_STACK + 4 - (LDS_D > 0 ? LDS_D : 0)];
-            const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
-            int sp = 0;
-            int32_t wc = 0, wn = 0;
-            const int r = SPEC ? bvh4_any_spec_budget_state<SPEC == 2>(S.bv, o, d, stk, BUDGET, flag == 1u, sp, wc, wn)
-                          : flag == 1u ? bvh4_any_near_budget_state(S.bv, o, d, stk, BUDGET, sp, wc, wn) : 0;
-            hit = r > 0;
-            late = r < 0;
-            const uint64_t lm = __ballot(late);
-            if (lm) {
-                const int leader = __ffsll((unsigned long long)lm) - 1;
-                uint32_t base = 0;
-                if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count, (uint32_t)__popcll(lm));
-                base = __shfl(base, leader);
-                if (late) {
-                    const uint32_t slot = base + (uint32_t)__popcll(lm & lanemask_lt());
-                    W.ao_late[slot] = (uint32_t)i;
-                    if (slot < W.ao_state_cap) {  // the walk so far, for ao_late_kernel to resume
-                        uint32_t* rec = W.ao_state + (size_t)slot * kLateWords;
-                        rec[0] = (uint32_t)wc;
-                        rec[1] = sp <= kLateSaved ? ((uint32_t)wn | ((uint32_t)sp << 8)) : 0xffffffffu;
-                        if (sp <= kLateSaved)
-                            for (int t = 0; t < sp; t++) rec[2 + t] = stk.get(t);
-                    }
+        uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
+        const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
+        int sp = 0;
+        int32_t wc = 0, wn = 0;
+        const int r = bvh4_any_spec_budget_state<0>(S.bv, o, d, stk, BUDGET, flag == 1u, sp, wc, wn);
+        const bool hit = r > 0, late = r < 0;
+        const uint64_t lm = __ballot(late);
+        if (lm) {
+            const int leader = __ffsll((unsigned long long)lm) - 1;
+            uint32_t base = 0;
+            if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count, (uint32_t)__popcll(lm));
+            base = __shfl(base, leader);
+            if (late) {
+                const uint32_t slot = base + (uint32_t)__popcll(lm & lanemask_lt());
+                W.ao_late[slot] = (uint32_t)i;
+                if (slot < W.ao_state_cap) {  // the walk so far, for ao_late_kernel to resume
+                    uint32_t* rec = W.ao_state + (size_t)slot * kLateWords;
+                    rec[0] = (uint32_t)wc;
+                    rec[1] = sp <= kLateSaved ? ((uint32_t)wn | ((uint32_t)sp << 8)) : 0xffffffffu;
+                    if (sp <= kLateSaved)
+                        for (int t = 0; t < sp; t++) rec[2 + t] = stk.get(t);
                 }
             }
-        } else if (LDS_D > 0) {
-            uint32_t stk_a[RT_BVH_STACK + 4 - (LDS_D > 0 ? LDS_D : 0)];
-            const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
-            hit = flag == 1u && bvh4_any_near_s(S.bv, o, d, stk);
-        } else {
-            hit = flag == 1u && bvh4_any_near(S.bv, o, d);
         }
         // sorted: a wave's lanes are no longer one call's samples
-        ao_finish<true>(S, W, SORT > 0 ? 1u : N, active && !late, ao_brute, hit,
-                        (uint64_t)__float_as_uint(r0.w), o, d);
-    }
-}
-
-// Persistent-lane form of ao_trace_kernel<WPE, LDS_D, SORT, KL, BUDGET>
-// (RT580_AO_REFILL=1): the block's SORT * TB samples are ordered by direction
-// cell as there; each wave then owns SORT * 64 consecutive sorted samples and
-// gives a lane the next one as soon as its ray is decided (hit, miss, or out
-// of budget: queued for ao_late_kernel), instead of running rounds of 64 rays
-// in lock step, where a round lasts as long as its longest ray
-// (tools/simd_sim.cpp "persistent refill" on the 100k field: node-step
-// efficiency 0.16 -> 0.30, leaf tests 0.10 -> 0.49). One step per loop
-// iteration = a descent to a leaf and its tests (bvh4_descend /
-// bvh4_leaf_hit / bvh4_pop, the visits of bvh4_any_near_budget_state); the
-// answers, queues and counts are the same as the round form's.
-template <int WPE, int LDS_D, int SORT, int KL, int BUDGET>
-__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
-ao_trace_refill_kernel(DevScene S, DevWork W, uint64_t n) {
-    if (frame_poisoned(W)) return;
-    static_assert(LDS_D > 0 && SORT > 0 && BUDGET > 0, "refill form: LDS stack, block sort, step budget");
-    __shared__ uint32_t lstk[LDS_D][TB];
-    constexpr int SN = SORT * TB;
-    constexpr int NB = 1 << (2 * KL);  // direction cells
-    __shared__ uint32_t s_order[SN];
-    __shared__ uint32_t s_bin[NB + 1];
-    __shared__ uint32_t s_wsum[TB / 64];
-    const BvhView& V = S.bv;
-    const int wave = threadIdx.x >> 6;
-    const uint64_t lt_mask = lanemask_lt();
-    uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
-    const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
-    for (uint64_t blk = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * SN; blk < n; blk += (uint64_t)gridDim.x * SN) {
-        // counting sort of the block's samples by direction cell (as ao_trace_kernel)
-        __syncthreads();
-        for (int k = threadIdx.x; k < NB + 1; k += TB) s_bin[k] = 0;
-        __syncthreads();
-        uint32_t key[SORT];
-#pragma unroll
-        for (int q = 0; q < SORT; q++) {
-            const uint64_t j = blk + (uint64_t)q * TB + threadIdx.x;
-            key[q] = NB;  // past the end: last
-            if (j < n) {
-                const float4 r1 = W.ao_rays[2 * j + 1];
-                key[q] = grid_cell(v3(r1.x, r1.y, r1.z), KL);
-            }
-            atomicAdd(&s_bin[key[q]], 1u);
-        }
-        __syncthreads();
-        {
-            constexpr int PER = (NB + 1 + TB - 1) / TB;
-            const int k0 = threadIdx.x * PER;
-            uint32_t run = 0;
-#pragma unroll
-            for (int q = 0; q < PER; q++)
-                if (k0 + q < NB + 1) run += s_bin[k0 + q];
-            const int ln = threadIdx.x & 63;
-            uint32_t inc = run;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
-                if (ln >= o) inc += v;
-            }
-            if (ln == 63) s_wsum[wave] = inc;
-            __syncthreads();
-            uint32_t acc = inc - run;
-            for (int w2 = 0; w2 < wave; w2++) acc += s_wsum[w2];
-#pragma unroll
-            for (int q = 0; q < PER; q++)
-                if (k0 + q < NB + 1) {
-                    const uint32_t cnt = s_bin[k0 + q];
-                    s_bin[k0 + q] = acc;
-                    acc += cnt;
-                }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < SORT; q++) {
-            const uint32_t pos = atomicAdd(&s_bin[key[q]], 1u);
-            s_order[pos] = (uint32_t)(q * TB + threadIdx.x);
-        }
-        __syncthreads();
-        // this wave's pool of sorted positions
-        const uint32_t p_end = (uint32_t)((wave + 1) * SORT * 64);
-        uint32_t p_next = (uint32_t)(wave * SORT * 64);  // wave-uniform
-        bool busy = false;  // the lane holds an undecided near query
-        uint64_t i = 0;
-        uint32_t call = 0;
-        rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-        SlabRay sr;
-        int sp = 0, visits = 0;
-        int32_t c = 0, nn = 0;
-        for (;;) {
-            bool fin = false, hit = false, brute = false, late = false;
-            // idle lanes take the next samples of the pool, in batches of at
-            // least W.refill_min lanes (or when the wave is empty): refilled
-            // lanes start at the root together, so their first node loads
-            // coalesce as in the round form
-            const uint64_t want = __ballot(!busy);
-            if (want && p_next < p_end &&
-                ((uint32_t)__popcll(want) >= W.refill_min || want == __builtin_amdgcn_read_exec())) {
-                const uint32_t pos = p_next + (uint32_t)__popcll(want & lt_mask);
-                p_next += (uint32_t)__popcll(want);
-                if (!busy && pos < p_end) {
-                    i = blk + s_order[pos];
-                    if (i < n) {
-                        const float4 r0 = W.ao_rays[2 * i], r1 = W.ao_rays[2 * i + 1];
-                        const uint32_t flag = __float_as_uint(r1.w);
-                        o = v3(r0.x, r0.y, r0.z);
-                        d = v3(r1.x, r1.y, r1.z);
-                        call = __float_as_uint(r0.w);
-                        if (flag == 2u) {
-                            fin = brute = true;
-                        } else if (flag == 1u) {
-                            // bvh4_any_near_budget_state's start: the brute list, then the tree
-                            for (int k = 0; k < V.n_brute && !hit; k++)
-                                hit = prim_hit_within(V.all[V.brute[k]], o, d, INFINITY);
-                            if (hit || !V.has_tree || dir_zero(d)) {
-                                fin = true;
-                            } else {
-                                sr = slab_ray(V, o, d);
-                                sp = 0;
-                                c = 0;
-                                nn = 0;  // root (internal)
-                                visits = 0;
-                                busy = true;
-                            }
-                        }
-                    }
-                }
-            }
-            // one leaf visit of every undecided ray
-            if (busy) {
-                if (visits == BUDGET) {
-                    late = true;
-                    busy = false;
-                } else {
-                    visits++;
-                    if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, nn)) {
-                        fin = true;
-                    } else if (bvh4_leaf_hit(V, o, d, INFINITY, c, nn)) {
-                        fin = hit = true;
-                    } else if (!bvh4_pop(stk, sp, c, nn)) {
-                        fin = true;
-                    }
-                    if (fin) busy = false;
-                }
-            }
-            // rays out of budget: queued for ao_late_kernel with their walk
-            const uint64_t lm = __ballot(late);
-            if (lm) {
-                const int leader = __ffsll((unsigned long long)lm) - 1;
-                uint32_t base = 0;
-                if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count, (uint32_t)__popcll(lm));
-                base = __shfl(base, leader);
-                if (late) {
-                    const uint32_t slot = base + (uint32_t)__popcll(lm & lt_mask);
-                    W.ao_late[slot] = (uint32_t)i;
-                    if (slot < W.ao_state_cap) {
-                        uint32_t* rec = W.ao_state + (size_t)slot * kLateWords;
-                        rec[0] = (uint32_t)c;
-                        rec[1] = sp <= kLateSaved ? ((uint32_t)nn | ((uint32_t)sp << 8)) : 0xffffffffu;
-                        if (sp <= kLateSaved)
-                            for (int t = 0; t < sp; t++) rec[2 + t] = stk.get(t);
-                    }
-                }
-            }
-            // decided rays: occlusion counts and the far queue
-            // (a far-origin ray is active with ao_brute: queued for the brute scan, as in the round form)
-            if (__ballot(fin)) ao_finish<true>(S, W, 1u, fin, fin && brute, hit, (uint64_t)call, o, d);
-            if (__ballot(busy) == 0 && p_next >= p_end) break;
-        }
+        ao_finish<true>(S, W, 1u, active && !late, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o, d);
     }
 }
 
 // The chunk's AO rays that ran out of ao_trace_kernel's step budget: the full
-// near query, then the same bookkeeping (hits counted per call, misses queued
-// for the far pass). Grid-stride over the device-side count.
-// SRC: the queue read (0: ao_trace_kernel's, at W.ao_late; 1: this kernel's
-// own second level, at W.ao_late + ao_cap / 2). BUDGET2 > 0 (with SRC 0): a
-// second budget, the rays still undecided go to queue 1 for a last launch
-// (RT580_AO_BUDGET2, A/B); skipped when queue 0 fills more than half the buffer.
-// REREAD = 0 (diagnostic builds only, RT580_LATE_REREAD=0): the round-4 form
-// that queues the ray from the registers of the traversal (see below).
-// SPEC (no second budget): the walks in speculative while-while form.
-template <int WPE, int LDS_D, int BUDGET2 = 0, int SRC = 0, int REREAD = 1, int SPEC = 0>
+// near query (resuming the walk saved for the ray, or from the root when its
+// stack was too deep to save), in speculative form, then the same bookkeeping
+// (hits counted per call, misses queued for the far pass). Grid-stride over the
+// device-side count.
+// The ray's record is read again after the walk (a volatile load, not the
+// registers of the first read), so that nothing of the ray but its index is
+// live across the traversal. History: round 4's 64-VGPR build of this kernel
+// (8 waves per SIMD, since removed) queued ~2 % of its far-pass rays with
+// origins not their own when the origin stayed live across the walk; every
+// answer it computed was right ("The 8-wave late-pass defect").
+template <int WPE, int LDS_D>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
 ao_late_kernel(DevScene S, DevWork W) {
     if (frame_poisoned(W)) return;
     __shared__ uint32_t lstk[LDS_D][TB];
-    const uint32_t half = W.ao_cap / 2;
-    const uint32_t cnt = W.ao_late_count[SRC];
-    const uint32_t* q = W.ao_late + (SRC ? half : 0u);
-    const bool two = BUDGET2 > 0 && cnt <= half;
+    const uint32_t cnt = W.ao_late_count[0];
     for (uint32_t b0 = blockIdx.x * TB; b0 < cnt; b0 += gridDim.x * TB) {
         const uint32_t k = b0 + threadIdx.x;
         const bool live = k < cnt;
         uint32_t i = 0;
         float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
         if (live) {
-            i = q[k];
+            i = W.ao_late[k];
             r0 = W.ao_rays[2 * (size_t)i];
             r1 = W.ao_rays[2 * (size_t)i + 1];
         }
         const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
         uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
         const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
-        // the walk saved for this ray by the previous level (region SRC of ao_state)
+        // the walk ao_trace_kernel saved for this ray
         int sp = 0;
         int32_t wc = 0, wn = 0;
         bool saved = false;
         if (live && k < W.ao_state_cap) {
-            const uint32_t* rec = W.ao_state + ((size_t)SRC * W.ao_state_cap + k) * kLateWords;
+            const uint32_t* rec = W.ao_state + (size_t)k * kLateWords;
             const uint32_t h1 = rec[1];
             if (h1 != 0xffffffffu) {
                 saved = true;
@@ -1944,141 +1488,20 @@ ao_late_kernel(DevScene S, DevWork W) {
                 for (int t = 0; t < sp; t++) stk.put(t, rec[2 + t]);
             }
         }
-        bool hit, late = false;
-        if (BUDGET2 > 0 && two) {
-            int r = 0;
-            if (live)
-                r = saved ? bvh4_any_near_resume_budget(S.bv, o, d, stk, BUDGET2, sp, wc, wn)
-                          : bvh4_any_near_budget_state(S.bv, o, d, stk, BUDGET2, sp, wc, wn);
-            hit = r > 0;
-            late = r < 0;
-            const uint64_t lm = __ballot(late);
-            if (lm) {
-                const int leader = __ffsll((unsigned long long)lm) - 1;
-                uint32_t base = 0;
-                if ((threadIdx.x & 63) == leader) base = atomicAdd(W.ao_late_count + 1, (uint32_t)__popcll(lm));
-                base = __shfl(base, leader);
-                if (late) {
-                    const uint32_t slot = base + (uint32_t)__popcll(lm & lanemask_lt());
-                    W.ao_late[half + slot] = i;
-                    if (slot < W.ao_state_cap) {  // region 1: for the last level
-                        uint32_t* rec = W.ao_state + ((size_t)W.ao_state_cap + slot) * kLateWords;
-                        rec[0] = (uint32_t)wc;
-                        rec[1] = sp <= kLateSaved ? ((uint32_t)wn | ((uint32_t)sp << 8)) : 0xffffffffu;
-                        if (sp <= kLateSaved)
-                            for (int t = 0; t < sp; t++) rec[2 + t] = stk.get(t);
-                    }
-                }
-            }
-        } else if (SPEC) {  // one walk for the saved and the restarted rays (the wave votes together)
-            bool go = live, pre = false;
-            if (live && !saved) {  // from the root, after the brute list
-                for (int t = 0; t < S.bv.n_brute && !pre; t++) pre = prim_hit_within(S.bv.all[S.bv.brute[t]], o, d, INFINITY);
-                go = !pre && S.bv.has_tree && !dir_zero(d);
-            }
-            hit = pre || bvh4_any_spec_walk<SPEC == 2>(S.bv, o, d, stk, 1 << 30, go, sp, wc, wn) > 0;
-        } else if (saved) {  // the saved walk, continued (same boolean)
-            hit = bvh4_any_near_resume(S.bv, o, d, stk, sp, wc, wn);
-        } else {
-            hit = live && bvh4_any_near_s(S.bv, o, d, stk);
+        // one walk for the saved and the restarted rays (the wave votes together)
+        bool go = live, pre = false;
+        if (live && !saved) {  // from the root, after the brute list
+            for (int t = 0; t < S.bv.n_brute && !pre; t++) pre = prim_hit_within(S.bv.all[S.bv.brute[t]], o, d, INFINITY);
+            go = !pre && S.bv.has_tree && !dir_zero(d);
         }
-        // The ray's record again (a volatile read: a real load, not the
-        // registers of the one above), so that nothing of the ray but its index
-        // is live across the traversal. The 64-VGPR build of this kernel
-        // (RT580_LATE_WPE=8) queued ~2 % of its far-pass rays with origins not
-        // their own when the origin stayed live here (the
-        // replayed-count mismatch of round 4); every answer it computed was right.
-        if (REREAD && live) {
+        const bool hit = pre || bvh4_any_spec_walk<0>(S.bv, o, d, stk, 1 << 30, go, sp, wc, wn) > 0;
+        if (live) {
             const volatile float4* rv = W.ao_rays + 2 * (size_t)i;
             r0 = make_float4(rv[0].x, rv[0].y, rv[0].z, rv[0].w);
             r1 = make_float4(rv[1].x, rv[1].y, rv[1].z, rv[1].w);
         }
-        if (REREAD)
-            ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w),
-                            v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z));
-        else
-            ao_finish<true>(S, W, 1u, live && !late, false, hit, (uint64_t)__float_as_uint(r0.w), o, d);
-    }
-}
-
-// Persistent-lane form of ao_late_kernel<WPE, LDS_D> (RT580_AO_REFILL=1, no
-// second budget): each wave owns a contiguous range of the late queue and
-// gives a lane the next ray as soon as its walk is decided -- the late rays
-// are the long, uneven walks, where a lock-step round of 64 lasts as long as
-// its longest. A ray resumes the walk ao_trace_*_kernel saved for it, else
-// starts over (brute list, then the tree), as in ao_late_kernel.
-template <int WPE, int LDS_D>
-__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
-ao_late_refill_kernel(DevScene S, DevWork W) {
-    if (frame_poisoned(W)) return;
-    __shared__ uint32_t lstk[LDS_D][TB];
-    const BvhView& V = S.bv;
-    const uint32_t cnt = W.ao_late_count[0];
-    const uint32_t nwaves = gridDim.x * (TB / 64);
-    const uint32_t wid = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
-    const uint32_t per = (cnt + nwaves - 1) / nwaves;
-    uint32_t p_next = wid * per;  // wave-uniform
-    const uint32_t p_end = p_next + per < cnt ? p_next + per : cnt;
-    if (p_next >= p_end) return;  // whole waves only (no barrier in this kernel)
-    const uint64_t lt_mask = lanemask_lt();
-    uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
-    const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
-    bool busy = false;
-    uint32_t call = 0;
-    rv3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-    SlabRay sr;
-    int sp = 0;
-    int32_t c = 0, nn = 0;
-    for (;;) {
-        bool fin = false, hit = false;
-        const uint64_t want = __ballot(!busy);
-        if (want && p_next < p_end &&
-            ((uint32_t)__popcll(want) >= W.refill_min || want == __builtin_amdgcn_read_exec())) {
-            const uint32_t k = p_next + (uint32_t)__popcll(want & lt_mask);
-            p_next += (uint32_t)__popcll(want);
-            if (!busy && k < p_end) {
-                const uint32_t i = W.ao_late[k];
-                const float4 r0 = W.ao_rays[2 * (size_t)i], r1 = W.ao_rays[2 * (size_t)i + 1];
-                o = v3(r0.x, r0.y, r0.z);
-                d = v3(r1.x, r1.y, r1.z);
-                call = __float_as_uint(r0.w);
-                sp = 0;
-                c = 0;
-                nn = 0;  // root (internal)
-                bool saved = false;
-                if (k < W.ao_state_cap) {
-                    const uint32_t* rec = W.ao_state + (size_t)k * kLateWords;
-                    const uint32_t h1 = rec[1];
-                    if (h1 != 0xffffffffu) {
-                        saved = true;
-                        sp = (int)(h1 >> 8);
-                        nn = (int32_t)(h1 & 255u);
-                        c = (int32_t)rec[0];
-                        for (int t = 0; t < sp; t++) stk.put(t, rec[2 + t]);
-                    }
-                }
-                if (!saved)  // start over: bvh4_any_near_s's brute list first
-                    for (int j = 0; j < V.n_brute && !hit; j++) hit = prim_hit_within(V.all[V.brute[j]], o, d, INFINITY);
-                if (hit) {
-                    fin = true;
-                } else {
-                    sr = slab_ray(V, o, d);
-                    busy = true;
-                }
-            }
-        }
-        if (busy) {
-            if (!bvh4_descend(V, sr, INFINITY, stk, sp, c, nn)) {
-                fin = true;
-            } else if (bvh4_leaf_hit(V, o, d, INFINITY, c, nn)) {
-                fin = hit = true;
-            } else if (!bvh4_pop(stk, sp, c, nn)) {
-                fin = true;
-            }
-            if (fin) busy = false;
-        }
-        if (__ballot(fin)) ao_finish<true>(S, W, 1u, fin, false, hit, (uint64_t)call, o, d);
-        if (__ballot(busy) == 0 && p_next >= p_end) break;
+        ao_finish<true>(S, W, 1u, live, false, hit, (uint64_t)__float_as_uint(r0.w), v3(r0.x, r0.y, r0.z),
+                        v3(r1.x, r1.y, r1.z));
     }
 }
 
@@ -2230,16 +1653,6 @@ __global__ void ao_audit_finish_kernel(const DevScene S, const DevWork W, const 
     if (aud[1] != aud[2]) out[3]++;
 }
 
-// RT580_LATE_REREAD=0: the 8-wave late pass without the re-read (its round-4 form)
-static int late_reread() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_LATE_REREAD");
-        v = e ? atoi(e) : 1;
-    }
-    return v;
-}
-
 static bool ao_verify_on() {
     static int v = -1;
     if (v < 0) {
@@ -2280,156 +1693,6 @@ static const AuditBuf* audit_for(const DevWork& W) {
 }
 #endif
 
-// RT580_LATE_WPE=8 (A/B): ao_late_kernel built for 8 waves/SIMD (64 VGPRs, spills)
-// instead of 6
-static int late_wpe() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_LATE_WPE");
-        v = e ? atoi(e) : 6;
-    }
-    return v;
-}
-
-static int ao_split() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_SPLIT");
-        v = e ? atoi(e) : 1;
-    }
-    return v;
-}
-
-// RT580_NEAR_WAVE=1 (A/B): the wave-cooperative near traversal
-// (bvh_any_near_wave, VARIANT 8192) for AO and shadow rays instead of the
-// per-lane bvh_any. Measured on 100k 1080p: AO 139 ms vs 85 ms per lane (the
-// union of 64 hemisphere directions' paths is far longer than one path),
-// shadow passes 14.5 vs 13.9 ms of trace. Off by default.
-static bool near_wave() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_NEAR_WAVE");
-        v = e ? atoi(e) : 0;
-    }
-    return v != 0;
-}
-
-// The first 16 traversal-stack entries of ao_trace_kernel in LDS
-// (RT580_TRACE_LDS=0: all in scratch). cornell10k AO 91.7 -> 84.9 ms,
-// field100k 1080p 72.7 -> 67.8 ms.
-static int trace_lds() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_TRACE_LDS");
-        v = e ? atoi(e) : 1;
-    }
-    return v;
-}
-
-static int ao_sort() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_SORT");
-        // 3: blocks of 2048 samples by 16 x 16 direction cells. AO field100k
-        // 1080p 53.9 -> 49.3 ms, cornell10k 80.1 -> 77.9 ms (0: unsorted;
-        // 1: 1024 / 8 x 8 50.6 / 79.4; 2: 2048 / 8 x 8 49.4; 4096 samples
-        // lose occupancy: 59.1 / 88.4; round 3, 2048 / 32 x 32 cells: 4
-        // waves/SIMD, north-star frame 41.8 -> 46.6 ms)
-        v = e ? atoi(e) : 3;
-    }
-    return v;
-}
-
-// RT580_AO_BUDGET: leaf visits per AO ray in ao_trace_kernel before the ray is
-// left to ao_late_kernel (0: no budget). 100k 1080p frame / Cornell frame:
-// 0: 56.3 / 87.5 ms, 2: 58.4 / 81.6, 4: 54.7 / 79.0, 8: 55.2 / 84.6.
-// RT580_SMALL_TRACE_WPE: occupancy target of the small-scene trace kernel (0: none, A/B 5, 6)
-static int small_trace_wpe() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_SMALL_TRACE_WPE");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
-// RT580_TRACE_SPEC: the trace levels' near walks in speculative form, bit 0
-// the closest-hit phase, bit 1 the shadow rays. Default 2 (kernel trace,
-// profiles/r05/ab/trace_spec.txt: the shadow pass 283.5 -> 271.9 us per launch
-// on the north-star frame, 451 -> 404 us on Cornell; the closest-hit form is
-// slower, 392 -> 526 / 480 -> 617 us -- its speculative descents run with the
-// bound of before the held leaf's test, which is what prunes most of the tree)
-static int trace_spec() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_TRACE_SPEC");
-        v = e ? atoi(e) : 2;
-    }
-    return v;
-}
-
-// RT580_AO_SPEC: the AO walks in speculative while-while form, bit 0 the
-// budgeted trace pass, bit 1 the late pass, bit 2 two held leaves, bits 3-4 the
-// trace's block shape (A/B: 8 x 8 cells, 1024-sample blocks) (default the first two: north-star frame
-// 37.5 -> 34.3 ms, Cornell 59.6 -> 54.7 ms; profiles/r05/ab/spec*)
-static int ao_spec() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_SPEC");
-        v = e ? atoi(e) : 3;
-    }
-    return v;
-}
-
-// RT580_AO_REFILL: persistent-lane forms, bit 0 the AO trace (ao_trace_refill_kernel),
-// bit 1 the late pass (ao_late_refill_kernel)
-static int ao_refill() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_REFILL");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
-static int ao_budget() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_BUDGET");
-        v = e ? atoi(e) : 4;
-    }
-    return v;
-}
-
-// RT580_AO_BUDGET2=1 (A/B): ao_late_kernel itself stops after 16 leaf visits and
-// a third launch finishes the rest
-static int ao_budget2() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_BUDGET2");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
-static int trace_wpe() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_TRACE_WPE");
-        v = e ? atoi(e) : 6;  // cornell10k AO: 8 (spills) 117 ms, 6: 97 ms, 4: 102 ms
-    }
-    return v;
-}
-
-static int near_wpe() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_NEAR_WPE");
-        v = e ? atoi(e) : 8;
-    }
-    return v;
-}
-
 // ---------------------------------------------------------------- far-hit pass
 // Direction-grid candidates (rt_bvh.h build_dir_grid) of a lane whose origin is
 // within grid_r: the "always" entries, then its cell's list. When every grid
@@ -2468,100 +1731,6 @@ __device__ int g_cell_skip;
 #define RT_CELL_STAT(k, v) ((void)0)
 #define RT_FAR_STAT(k, v) ((void)0)
 #endif
-
-template <bool CLOSEST, int U = 1>
-__device__ __forceinline__ bool far_grid_lane(const DevScene& S, bool gl, rv3 o, rv3 d, const FarRay& fr, Hit& h,
-                                              bool& found, FarTri* tile) {
-    const BvhView& V = S.bv;
-    bool hit = false;
-    const uint32_t cell = gl ? grid_cell(d, V.grid_log2) : 0u;
-    auto test = [&](bool on, const FarTri& ft) {
-        if (!(on && !(CLOSEST ? false : hit))) return;
-        if (!far_candidate(ft, fr, o, d)) return;
-        if (!CLOSEST) RT_FAR_STAT(7, 1);
-        const rt_prim P = load_prim_scalar(S.prims, (int)__builtin_amdgcn_readfirstlane(ft.id));
-        if (CLOSEST) {
-            float t, a, b, g;
-            if (tri_test<true, true>(P, o, d, t, a, b, g, found ? h.t : INFINITY) && lex_better(t, (int)ft.id, found, h)) {
-                found = true;
-                hit = true;
-                h.t = t; h.a = a; h.b = b; h.g = g; h.prim = (int)ft.id;
-            }
-        } else if (prim_test_any(P, o, d)) {
-            hit = true;
-        }
-    };
-    for (int q = 0; q < V.n_always; q++) test(gl, load_far_tri(V.far_tris, (int)V.grid_always[q]));
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t glm = __ballot(gl);
-    uint32_t c0 = 0;
-    bool uniform = false;
-    if (glm) {
-        c0 = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)cell, __ffsll((unsigned long long)glm) - 1));
-        uniform = __ballot(gl && cell != c0) == 0;
-    }
-#ifdef RT580_DIAGNOSTICS
-    if (!CLOSEST && glm && lane == (uint32_t)(__ffsll((unsigned long long)glm) - 1)) RT_FAR_STAT(uniform ? 2 : 3, 1);
-    if (!CLOSEST && gl) {
-        const uint32_t len = V.grid_start[cell + 1] - V.grid_start[cell];
-        RT_FAR_STAT(4, len);
-        uint32_t mx = len;
-        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
-        if (lane == (uint32_t)(__ffsll((unsigned long long)glm) - 1)) RT_FAR_STAT(5, uniform ? (mx + 63) / 64 : (mx + U - 1) / U);
-    }
-#endif
-    if (uniform) {
-        const bool mine = gl;
-        const uint32_t b = V.grid_start[c0], e = V.grid_start[c0 + 1];
-        for (uint32_t t0 = b; t0 < e; t0 += 64) {
-            if (!CLOSEST && __ballot(mine && !hit) == 0) break;
-            // the previous tile's reads are done before it is overwritten
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (t0 + lane < e) tile[lane] = V.far_tris[V.grid_items[t0 + lane]];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const uint32_t m = e - t0 < 64u ? e - t0 : 64u;
-            for (uint32_t j = 0; j < m; j++) {
-                if (!CLOSEST && (j & 7u) == 0 && __ballot(mine && !hit) == 0) break;
-                test(mine, tile[j]);
-            }
-        }
-    } else if (gl) {
-        // U candidates per step: their list entries, then their planes, in
-        // flight together (the lane's loads are a dependent chain otherwise)
-        const uint32_t b = V.grid_start[cell], e = V.grid_start[cell + 1];
-        for (uint32_t k0 = b; k0 < e && (CLOSEST || !hit); k0 += U) {
-          uint32_t idx[U];
-#pragma unroll
-          for (int u = 0; u < U; u++) idx[u] = k0 + u < e ? V.grid_items[k0 + u] : 0u;
-          FarTri fts[U];
-#pragma unroll
-          for (int u = 0; u < U; u++) fts[u] = V.far_tris[idx[u]];
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            if (k0 + u >= e || !(CLOSEST || !hit)) continue;
-            const FarTri& ft = fts[u];
-            if (!far_candidate(ft, fr, o, d)) continue;
-            if (!CLOSEST) RT_FAR_STAT(7, 1);
-            const rt_prim P = S.prims[ft.id];
-            if (CLOSEST) {
-                float t, a, bb, g;
-                if (tri_test<true, true>(P, o, d, t, a, bb, g, found ? h.t : INFINITY) && lex_better(t, (int)ft.id, found, h)) {
-                    found = true;
-                    hit = true;
-                    h.t = t; h.a = a; h.b = bb; h.g = g; h.prim = (int)ft.id;
-                }
-            } else if (prim_test_any(P, o, d)) {
-                hit = true;
-            }
-          }
-        }
-    }
-    return hit;
-}
 
 // The queued AO rays, sorted by direction key, 64 per wave: the wave walks the
 // plane tree once for all its lanes (a node is entered if any live lane may
@@ -2745,7 +1914,7 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t nwork = W.far_seg_n[1];
     const uint32_t stride = gridDim.x * (TB / 64);
-    uint32_t w = xcd_block(blockIdx.x, gridDim.x) * (TB / 64) + wave;
+    uint32_t w = blockIdx.x * (TB / 64) + wave;
     if (w >= nwork) return;
     for (;;) {
         const CellItem cur = cell_item(V, W.far_work[w]);
@@ -2900,7 +2069,7 @@ far_cell_closest_kernel(DevScene S, DevWork W) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t nwork = W.far_seg_n[1];
     const uint32_t stride = gridDim.x * (TB / 64);
-    for (uint32_t w = xcd_block(blockIdx.x, gridDim.x) * (TB / 64) + wave; w < nwork; w += stride) {
+    for (uint32_t w = blockIdx.x * (TB / 64) + wave; w < nwork; w += stride) {
         const CellItem cur = cell_item(V, W.far_work[w]);
         if (cur.skip) continue;  // no candidate: no far hit in this cell
         uint32_t q, gi;
@@ -2996,76 +2165,6 @@ far_cell_closest_kernel(DevScene S, DevWork W) {
                 W.hit4[node] = make_float4(t, ba, bb, bg);
                 W.hit_prim[node] = id;
             }
-        }
-    }
-}
-
-template <int U = 1>
-__global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(FAR_ANY_WPE)))
-far_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
-    if (frame_poisoned(W)) return;
-    __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
-    __shared__ FarTri ftile[TB / 64][64];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t stride = gridDim.x * TB;
-    for (uint32_t base = (blockIdx.x * (TB / 64) + wave) * 64u; base < n; base += stride) {
-        const uint32_t i = base + lane;
-        bool live = i < n;
-        rv3 o = v3(0, 0, 0), d = v3(1, 0, 0);
-        uint32_t call = 0;
-        if (live) {
-            const uint32_t r = W.far_vals_alt[i];
-            const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
-            o = v3(a.x, a.y, a.z);
-            call = __float_as_uint(a.w);
-            d = v3(b.x, b.y, b.z);
-        }
-        const FarRay fr = far_ray(S.bv, o);
-        bool hit = false;
-        {
-            const bool gl = live && grid_origin(S.bv, o);
-            RT_FAR_STAT(0, live ? 1 : 0);
-            RT_FAR_STAT(1, gl ? 1 : 0);
-            RT_FAR_STAT(6, live && !gl ? 1 : 0);
-            Hit hd;
-            bool fd = false;
-            if (far_grid_lane<false, U>(S, gl, o, d, fr, hd, fd, ftile[wave])) hit = true;
-            if (gl) live = false;  // done: the tree walk below serves the other lanes
-        }
-        if (far_tree_any_wave(S, live, o, d, fr, stk[wave])) hit = true;
-        if (hit) any_hit_out(W, flag, call);
-        RT_FAR_STAT(8, hit ? 1 : 0);
-    }
-}
-
-// Per-lane variants (each lane walks its own path): better than the wave union
-// when the queue is too sparse for sorted waves to share a direction.
-__global__ void __launch_bounds__(TB) far_any_lane_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
-    if (frame_poisoned(W)) return;
-    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
-        const uint32_t r = W.far_vals_alt[i];
-        const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
-        if (far_any(S.bv, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z))) any_hit_out(W, flag, __float_as_uint(a.w));
-    }
-}
-
-__global__ void __launch_bounds__(TB) far_closest_lane_kernel(DevScene S, DevWork W, uint32_t n) {
-    if (frame_poisoned(W)) return;
-    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
-        const uint32_t r = W.far_vals_alt[i];
-        const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
-        const uint32_t node = __float_as_uint(a.w);
-        const float4 hv = W.hit4[node];
-        Hit h;
-        h.prim = W.hit_prim[node];
-        h.t = hv.x; h.a = hv.y; h.b = hv.z; h.g = hv.w;
-        const bool found = h.prim >= 0;
-        const int prev = h.prim;
-        const float prev_t = h.t;
-        if (far_closest(S.bv, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), h, found) &&
-            (h.prim != prev || __float_as_uint(h.t) != __float_as_uint(prev_t))) {
-            W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
-            W.hit_prim[node] = h.prim;
         }
     }
 }
@@ -3397,54 +2496,15 @@ __global__ void __launch_bounds__(TB) far_brute_any_split_kernel(DevScene S, Dev
     }
 }
 
-// RT580_BRUTE_SPLIT bits: 1 = the closest-hit brute scans split across waves
-// (far_brute_split_kernel), 2 = the any-hit ones (far_brute_any_split_kernel).
-static int brute_split() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_BRUTE_SPLIT");
-        v = e ? atoi(e) : 3;
-    }
-    return v;
-}
-
-// The trace levels' closest-hit far pass (RT580_FAR_CLOSEST_U): 0 cell-major
-// (far_cell_closest_kernel), else far_closest_kernel with that many list entries
-// in flight per lane (1, 2, 4).
-static int far_closest_u() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_FAR_CLOSEST_U");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
 // Largest slice of the scene one wave scans in the split any-hit brute scan.
 constexpr uint32_t kBruteSlice = 4096;
 
-// Waves a split brute scan aims at (ray groups x slices): RT580_BRUTE_WAVES.
-// North-star frame, 8192 vs 32768 over three boxes: 38.22 / 38.69 / 36.69 vs
-// 39.27 / 39.04 / 37.40 ms; the 8-way share 7.56 vs 7.59 (profiles/r04/ab/bw*,
-// kn2_*): fewer, longer waves per launch.
-static uint32_t brute_waves() {
-    static long v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_BRUTE_WAVES");
-        v = e ? atol(e) : 8192;
-    }
-    return (uint32_t)v;
-}
-
-// Far-origin rays per wave of the split brute scans (RT580_BRUTE_RAYS 1, 4, 8).
-static int brute_rays() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_BRUTE_RAYS");
-        v = e ? atoi(e) : 8;
-    }
-    return v;
-}
+// Waves a split brute scan aims at (ray groups x slices). North-star frame,
+// 8192 vs 32768 over three boxes: 38.22 / 38.69 / 36.69 vs 39.27 / 39.04 /
+// 37.40 ms; the 8-way share 7.56 vs 7.59 (profiles/r04/ab/bw*, kn2_*): fewer,
+// longer waves per launch. Far-origin rays per wave of the split scans: 8.
+constexpr uint32_t kBruteWaves = 8192;
+constexpr int kBruteRays = 8;
 
 static int grid_for(uint64_t items, int cap);
 
@@ -3453,14 +2513,13 @@ static int grid_for(uint64_t items, int cap);
 static hipError_t launch_brute_any(const DevScene& S, const DevWork& W, uint32_t first, uint32_t nb, uint8_t* flag,
                                    hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    if (brute_split() & 2) {
+    {
         // the sort's input keys are free now: one claim word per ray
         uint32_t* done = W.far_keys;
         hipError_t e = hipMemsetAsync(done, 0, (size_t)nb * 4, s);
         if (e != hipSuccess) return e;
-        const int R = brute_rays();
-        const uint32_t ng = (nb + (uint32_t)R - 1) / (uint32_t)R;
-        uint32_t splits = brute_waves() / ng;
+        const uint32_t ng = (nb + (uint32_t)kBruteRays - 1) / (uint32_t)kBruteRays;
+        uint32_t splits = kBruteWaves / ng;
         splits = splits < 1u ? 1u : (splits > 256u ? 256u : splits);
         // slices of at most kBruteSlice records: a ray no record accepts is
         // scanned in parallel slices even when the queue is long (the AO chunks
@@ -3468,75 +2527,10 @@ static hipError_t launch_brute_any(const DevScene& S, const DevWork& W, uint32_t
         // skip their later slices through done[])
         splits = std::max(splits, ((uint32_t)S.n_prims + kBruteSlice - 1) / kBruteSlice);
         const dim3 grid(grid_for((uint64_t)ng * splits * 64, 16384));
-        if (R == 8)
-            hipLaunchKernelGGL(far_brute_any_split_kernel<8>, grid, dim3(TB), 0, s, S, W, first, nb, splits, done, flag);
-        else if (R == 4)
-            hipLaunchKernelGGL(far_brute_any_split_kernel<4>, grid, dim3(TB), 0, s, S, W, first, nb, splits, done, flag);
-        else
-            hipLaunchKernelGGL(far_brute_any_split_kernel<1>, grid, dim3(TB), 0, s, S, W, first, nb, splits, done, flag);
-    } else {
-        hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s, S, W, first,
-                           first + nb, 0, (int)S.bv.n_far, 1, flag);
+        hipLaunchKernelGGL(far_brute_any_split_kernel<kBruteRays>, grid, dim3(TB), 0, s, S, W, first, nb, splits, done,
+                           flag);
     }
     return hipGetLastError();
-}
-
-// Far-pass flavour for a queue of nq rays: 4 = cell-major segments (any-hit
-// passes), 1 = wave union per 64 sorted rays, 2 = per lane, 3 = scan.
-// RT580_FAR_MODE overrides (A/B only; the closest-hit passes use 1 for 4).
-static int far_mode(uint32_t nq) {
-    static int forced = -1;
-    if (forced < 0) {
-        const char* e = getenv("RT580_FAR_MODE");
-        forced = e ? atoi(e) : 4;
-    }
-    if (forced >= 1 && forced <= 4) return forced;
-    return 4;
-}
-
-// Queued tree rays of a BVH trace level (sorted by direction key): the far part
-// of bvh_closest, merged into the provisional hit with the same lexicographic
-// rule; wave-cooperative like far_any_kernel.
-// U: list entries in flight per lane in the per-lane walk of a non-uniform
-// wave (far_grid_lane): the kernel's time is its slowest lane's walk of its
-// cell's list (up to ~320 entries at 100k triangles), one dependent chain of
-// entry -> plane -> record per step.
-template <int U>
-__global__ void __launch_bounds__(TB) far_closest_kernel(DevScene S, DevWork W, uint32_t n) {
-    if (frame_poisoned(W)) return;
-    __shared__ int32_t stk[TB / 64][RT_BVH_STACK];
-    __shared__ FarTri ftile[TB / 64][64];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t stride = gridDim.x * TB;
-    for (uint32_t base = (blockIdx.x * (TB / 64) + wave) * 64u; base < n; base += stride) {
-        const uint32_t i = base + lane;
-        const bool live = i < n;
-        rv3 o = v3(0, 0, 0), d = v3(1, 0, 0);
-        uint32_t node = 0;
-        Hit h;
-        h.t = 0; h.a = h.b = h.g = 0; h.prim = -1;
-        bool found = false;
-        if (live) {
-            const uint32_t r = W.far_vals_alt[i];
-            const float4 a = W.far_rays[2 * (size_t)r], b = W.far_rays[2 * (size_t)r + 1];
-            o = v3(a.x, a.y, a.z);
-            node = __float_as_uint(a.w);
-            d = v3(b.x, b.y, b.z);
-            const float4 hv = W.hit4[node];
-            h.prim = W.hit_prim[node];
-            found = h.prim >= 0;
-            h.t = hv.x; h.a = hv.y; h.b = hv.z; h.g = hv.w;
-        }
-        const FarRay fr = far_ray(S.bv, o);
-        bool changed = false;
-        const bool gl = live && grid_origin(S.bv, o);
-        if (far_grid_lane<true, U>(S, gl, o, d, fr, h, found, ftile[wave])) changed = true;
-        if (far_tree_closest_wave(S, live && !gl, o, d, fr, h, found, stk[wave])) changed = true;
-        if (changed) {
-            W.hit4[node] = make_float4(h.t, h.a, h.b, h.g);
-            W.hit_prim[node] = h.prim;
-        }
-    }
 }
 
 // Same kernel with the register budget capped for 8 waves per SIMD (SGPR <= 80
@@ -3551,12 +2545,6 @@ ao_kernel_occ8(DevScene S, DevFrame F, DevWork W, const uint64_t* call_lo, const
 }
 
 // ---------------------------------------------------------------- resolve
-struct RFrame {
-    rpix local, refl;
-    float kr, kt, ks, ktm;
-    int node;
-    int stage;  // 1: reflection child pending, 2: refraction child pending
-};
 
 __device__ __forceinline__ rpix node_local(const DevScene& S, const DevFrame& F, const DevWork& W, const NodeRec& nd,
                                            const rt_material& m, uint32_t node) {
@@ -3575,62 +2563,6 @@ __device__ __forceinline__ rpix node_local(const DevScene& S, const DevFrame& F,
     return local;
 }
 
-__global__ void __launch_bounds__(TB) resolve_kernel(DevScene S, DevFrame F, DevWork W, int16_t* __restrict__ fb) {
-    if (S.use_bvh && frame_poisoned(W)) return;
-    const uint32_t npix = (uint32_t)F.n_rows * (uint32_t)F.width;
-    const uint32_t p = blockIdx.x * TB + threadIdx.x;
-    if (p >= npix) return;
-    RFrame st[RT_MAX_DEPTH + 1];
-    int lvl = 0;
-    int cur = (int)p;
-    rpix ret;
-    for (;;) {
-        const NodeRec nd = W.nodes[cur];
-        const int flags = nd.local_b_flags >> 16;
-        bool descended = false;
-        if (!(flags & RT_NODE_HIT)) {
-            ret = px(254, 64, 205);  // BG_COLOR (Raytracer.h:597)
-        } else {
-            const rt_material m = S.mats[nd.shape];
-            const rpix local = node_local(S, F, W, nd, m, (uint32_t)cur);
-            if (flags & RT_NODE_LEAF) {
-                ret = px_clamp(local);
-            } else {
-                RFrame& f = st[lvl];
-                f.local = local;
-                f.refl = px(0, 0, 0);
-                f.kr = nd.kr; f.kt = nd.kt; f.ks = m.ks; f.ktm = m.kt;
-                f.node = cur;
-                const int4 tp = W.topo[cur];
-                if (tp.x >= 0) {
-                    f.stage = 1; cur = tp.x; lvl++; descended = true;
-                } else if (tp.y >= 0) {
-                    f.stage = 2; cur = tp.y; lvl++; descended = true;
-                } else {
-                    ret = combine(local, px(0, 0, 0), px(0, 0, 0), f.kr, f.kt, f.ks, f.ktm);
-                }
-            }
-        }
-        if (descended) continue;
-        bool resumed = false;
-        while (lvl > 0) {
-            RFrame& pf = st[lvl - 1];
-            if (pf.stage == 1) {
-                pf.refl = ret;
-                const int c1 = W.topo[pf.node].y;
-                if (c1 >= 0) { pf.stage = 2; cur = c1; resumed = true; break; }
-                ret = combine(pf.local, pf.refl, px(0, 0, 0), pf.kr, pf.kt, pf.ks, pf.ktm);
-            } else {
-                ret = combine(pf.local, pf.refl, ret, pf.kr, pf.kt, pf.ks, pf.ktm);
-            }
-            lvl--;
-        }
-        if (!resumed) break;
-    }
-    fb[(size_t)p * 3 + 0] = (int16_t)ret.r;
-    fb[(size_t)p * 3 + 1] = (int16_t)ret.g;
-    fb[(size_t)p * 3 + 2] = (int16_t)ret.b;
-}
 
 // Level-by-level form of the same blend: one launch per recursion level, from
 // the deepest up. A node's value (Raycast's return) is combined from its own
@@ -3728,32 +2660,7 @@ static int grid_for(uint64_t items, int cap) {
 
 // Workgroups of a recursion level > 0 (trace and resolve; grid-stride over the
 // level's count, which only the device knows): RT580_DEEP_GRID for A/B.
-static int deep_grid() {
-    static int g = -1;
-    if (g < 0) {
-        const char* e = getenv("RT580_DEEP_GRID");
-        g = e ? atoi(e) : 512;  // 4096 / 1024 / 512: config 2 1.562 / 1.561 / 1.550 ms, its 8-way share 0.324 / 0.323 / 0.319
-        if (g < 64 || g > 65536) g = 512;
-    }
-    return g;
-}
-
-// Candidates in flight per lane in far_any_kernel's per-lane list walk
-// (RT580_FAR_U = 1, 2, 4).
-static void launch_far_any(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s) {
-    static int u = -1;
-    if (u < 0) {
-        const char* e = getenv("RT580_FAR_U");
-        u = e ? atoi(e) : 2;  // field1m frame 2252 (1) -> 2207 ms (2); 4 spills (2402)
-    }
-    if (u == 4)
-        hipLaunchKernelGGL(far_any_kernel<4>, dim3(grid_for(n, 16384)), dim3(TB), 0, s, S, W, n, flag);
-    else if (u == 2)
-        hipLaunchKernelGGL(far_any_kernel<2>, dim3(grid_for(n, 16384)), dim3(TB), 0, s, S, W, n, flag);
-    else
-        hipLaunchKernelGGL(far_any_kernel<1>, dim3(grid_for(n, 16384)), dim3(TB), 0, s, S, W, n, flag);
-}
-
+constexpr int kDeepGrid = 512;  // 4096 / 1024 / 512: config 2 1.562 / 1.561 / 1.550 ms, its 8-way share 0.324 / 0.323 / 0.319
 
 // RT580_PROGRESS=1: a stderr line per trace level / AO chunk of the BVH path
 // (those already synchronize), so multi-minute frames show progress.
@@ -3853,16 +2760,6 @@ static hipError_t read_counts(const uint32_t* dev, int n, uint32_t* out, hipStre
             g_cs->where.push_back(g_where);
         }
     return e;
-}
-
-// RT580_SMALL_SORT (default 1): queues of <= 4096 rays sorted by one workgroup
-static bool small_sort_on() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_SMALL_SORT");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
 }
 
 // Queues of at most kSmallSort rays: one workgroup sorts them in LDS (one
@@ -4021,7 +2918,7 @@ __global__ void __launch_bounds__(kSmallSortThreads) small_cells_kernel(DevScene
 // far_cell_any_kernel. One host read (the segment count).
 static hipError_t launch_far_cells(const DevScene& S, const DevWork& W, uint32_t n, uint8_t* flag, hipStream_t s,
                                    bool closest = false) {
-    if (n <= kSmallSort && small_sort_on()) {  // segments and work items in one workgroup
+    if (n <= kSmallSort) {  // segments and work items in one workgroup
         RT_STEP("far queue small segments");
         hipLaunchKernelGGL(small_cells_kernel, dim3(1), dim3(kSmallSortThreads), 0, s, S, W, n);
         RT_STEP("far cell pass");
@@ -4114,22 +3011,15 @@ __global__ void __launch_bounds__(TB) gamma_u8_wide_kernel(const int16_t* __rest
     }
 }
 
-// RT580_D2H_BLOCKS: workgroups of the kernels that write mapped host memory.
-// Their waves wait on the host link (~55 GB/s), so a few suffice to keep it
-// busy; a full grid would hold most of the chip's wave slots for the whole
-// transfer, away from the other frames' kernels.
-int d2h_blocks() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_D2H_BLOCKS");
-        v = e ? atoi(e) : 64;
-    }
-    return v;
-}
+// Workgroups of the kernels that write mapped host memory. Their waves wait on
+// the host link (~55 GB/s), so a few suffice to keep it busy; a full grid would
+// hold most of the chip's wave slots for the whole transfer, away from the other
+// frames' kernels (16 to 4096 workgroups: no difference in the step).
+constexpr int kD2HBlocks = 64;
 
 hipError_t launch_gamma_u8_wide(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s) {
     const uint64_t n16 = n / 16;
-    if (n16) hipLaunchKernelGGL(gamma_u8_wide_kernel, dim3(grid_for(n16, d2h_blocks())), dim3(TB), 0, s, fb, n16, out);
+    if (n16) hipLaunchKernelGGL(gamma_u8_wide_kernel, dim3(grid_for(n16, kD2HBlocks)), dim3(TB), 0, s, fb, n16, out);
     if (n > n16 * 16)
         hipLaunchKernelGGL(gamma_u8_kernel, dim3(1), dim3(TB), 0, s, fb + n16 * 16, n - n16 * 16, out + n16 * 16);
     return hipGetLastError();
@@ -4319,7 +3209,7 @@ hipError_t launch_deinterleave_u8(const uint8_t* tiles, int world, int n_max, in
     const uint64_t n = (uint64_t)width * 3 * height;
     if (n == 0) return hipSuccess;
     if ((width * 3) % 16 == 0 && ((uintptr_t)tiles | (uintptr_t)out) % 16 == 0)
-        hipLaunchKernelGGL(deinterleave_u8_wide_kernel, dim3(grid_for(n / 16, d2h_blocks())), dim3(256), 0, s,
+        hipLaunchKernelGGL(deinterleave_u8_wide_kernel, dim3(grid_for(n / 16, kD2HBlocks)), dim3(256), 0, s,
                            (const uint4*)tiles, world, n_max, width * 3 / 16, height, (uint4*)out);
     else
         hipLaunchKernelGGL(deinterleave_kernel<uint8_t>, dim3(grid_for(n, 16384)), dim3(256), 0, s, tiles, world,
@@ -4338,9 +3228,6 @@ hipError_t upload_minstd_table(hipStream_t s) {
         x = (x * 16807ull) % 2147483647ull;
     }
     hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_minstd_j1), j1, sizeof j1, 0, hipMemcpyHostToDevice, s);
-    static uint32_t xcd = 0u;  // (the same for every context)
-    if (const char* v = getenv("RT580_XCD_ORDER")) xcd = (uint32_t)atoi(v);
-    if (e == hipSuccess) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xcd_order), &xcd, 4, 0, hipMemcpyHostToDevice, s);
     return e;
 }
 
@@ -4409,12 +3296,7 @@ void kernel_timer_release() {
 // 4 at L = 10, 11); plane-tree keys then group by their top direction bits
 // only -- grouping, never a result (RT580_SORT_BITS=0: every bit, A/B).
 static int sort_begin_bit(const DevScene& S) {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_SORT_BITS");
-        v = e ? atoi(e) : 1;
-    }
-    if (!v || S.bv.grid_log2 <= 0) return 0;
+    if (S.bv.grid_log2 <= 0) return 0;
     const int b = 24 - 2 * S.bv.grid_log2;
     return b > 0 ? b : 0;
 }
@@ -4436,7 +3318,7 @@ static hipError_t sort_far_queue(const DevScene& S, const DevWork& W, hipStream_
     if (one_dir && nb == nq)  // every key RT_KEY_BRUTE: already grouped; the brute pass reads the sorted values
         return hipMemcpyAsync(W.far_vals_alt, W.far_vals, (size_t)nq * 4, hipMemcpyDeviceToDevice, s);
     const int b0 = one_dir ? 24 : sort_begin_bit(S);
-    if (nq <= kSmallSort && small_sort_on()) {
+    if (nq <= kSmallSort) {
         RT_STEP("far queue small sort");
         hipLaunchKernelGGL(small_sort_kernel, dim3(1), dim3(kSmallSortThreads), 0, s, W.far_keys, W.far_vals, nq, b0,
                            RT_DIR_KEY_BITS, W.far_keys_alt, W.far_vals_alt);
@@ -4456,16 +3338,6 @@ __global__ void frame_init_kernel(DevWork W) {
         *W.needed = 0;
         *W.aofix_count = 0;
     }
-}
-
-// Small brute-force scenes: scalar-load trace kernel (RT580_TRACE_SCALAR=0: LDS tile, A/B only).
-static bool trace_scalar() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_TRACE_SCALAR");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
 }
 
 hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
@@ -4496,34 +3368,26 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                 const int grid = grid_for(c1 - c0, 1 << 20);
                 if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
                 RT_STEP("trace near phase");
-                if (trace_spec() & 1)
-                    hipLaunchKernelGGL((trace_kernel<true, 1, false, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
-                else
-                    hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
+                hipLaunchKernelGGL((trace_kernel<true, 1>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 uint32_t nq = 0, nb = 0;
                 if ((e = sort_far_queue(S, W, s, nq, nb)) != hipSuccess) return e;
                 if (nb) {
                     RT_STEP("trace brute scan");
-                    if ((brute_split() & 1) && (uint64_t)nb * 2 <= W.far_cap) {
+                    if ((uint64_t)nb * 2 <= W.far_cap) {
                         // the sort's input keys are free now: 64-bit minima per brute ray
                         unsigned long long* best = reinterpret_cast<unsigned long long*>(W.far_keys);
                         if ((e = hipMemsetAsync(best, 0xff, (size_t)nb * 8, s)) != hipSuccess) return e;
-                        const int R = brute_rays();
-                        const uint32_t ng = (nb + (uint32_t)R - 1) / (uint32_t)R;
-                        uint32_t splits = brute_waves() / ng;
+                        const uint32_t ng = (nb + (uint32_t)kBruteRays - 1) / (uint32_t)kBruteRays;
+                        uint32_t splits = kBruteWaves / ng;
                         splits = splits < 1u ? 1u : (splits > 512u ? 512u : splits);
                         const dim3 grid(grid_for((uint64_t)ng * splits * 64, 16384));
-                        if (R == 8)
-                            hipLaunchKernelGGL(far_brute_split_kernel<8>, grid, dim3(TB), 0, s, S, W, nq - nb, nb, splits, best);
-                        else if (R == 4)
-                            hipLaunchKernelGGL(far_brute_split_kernel<4>, grid, dim3(TB), 0, s, S, W, nq - nb, nb, splits, best);
-                        else
-                            hipLaunchKernelGGL(far_brute_split_kernel<1>, grid, dim3(TB), 0, s, S, W, nq - nb, nb, splits, best);
+                        hipLaunchKernelGGL(far_brute_split_kernel<kBruteRays>, grid, dim3(TB), 0, s, S, W, nq - nb, nb,
+                                           splits, best);
                         if ((e = hipGetLastError()) != hipSuccess) return e;
                         hipLaunchKernelGGL(far_brute_merge_kernel, dim3(grid_for(nb, 4096)), dim3(TB), 0, s, S, W,
                                            nq - nb, nb, (const unsigned long long*)best);
-                    } else {
+                    } else {  // (no room for the minima in the free keys: one wave per ray over every record)
                         hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nb * 64, 16384)), dim3(TB), 0, s,
                                            S, W, nq - nb, nq, 1, (int)S.bv.n_far, 1, (uint8_t*)nullptr);
                     }
@@ -4545,24 +3409,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
 #endif
                 if (nq) {
                     RT_STEP("trace far pass");
-                    const int fm = far_mode(nq);
-                    if (fm == 4 && far_closest_u() == 0) {
-                        if ((e = launch_far_cells(S, W, nq, nullptr, s, /*closest=*/true)) != hipSuccess) return e;
-                    } else if (fm == 1 || fm == 4) {
-                        const int u = far_closest_u();
-                        if (u == 4)
-                            hipLaunchKernelGGL(far_closest_kernel<4>, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
-                        else if (u == 2)
-                            hipLaunchKernelGGL(far_closest_kernel<2>, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
-                        else
-                            hipLaunchKernelGGL(far_closest_kernel<1>, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
-                    }
-                    else if (fm == 2)
-                        hipLaunchKernelGGL(far_closest_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq);
-                    else
-                        hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nq * 64, 16384)), dim3(TB), 0, s, S,
-                                           W, 0u, nq, 1, (int)S.bv.n_far, 0, (uint8_t*)nullptr);
-                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                    if ((e = launch_far_cells(S, W, nq, nullptr, s, /*closest=*/true)) != hipSuccess) return e;
                 }
                 // shadow rays of the directional lights: near any-hit, then the
                 // sorted far pass (brute scan for far-origin rays), like AO rays
@@ -4571,12 +3418,8 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         const int li = S.shadow_light[dl];
                         if ((e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
                         RT_STEP("trace shadow near pass");
-                        if (trace_spec() & 2)
-                            hipLaunchKernelGGL((trace_kernel<true, 3, false, true>), dim3(grid), dim3(TB), 0, s, S, F, W,
-                                               level, c0, c1, li, dl, near_wave() ? 1 : 0);
-                        else
-                            hipLaunchKernelGGL((trace_kernel<true, 3>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1,
-                                               li, dl, near_wave() ? 1 : 0);
+                        hipLaunchKernelGGL((trace_kernel<true, 3>), dim3(grid), dim3(TB), 0, s, S, F, W, level, c0, c1,
+                                           li, dl);
                         if ((e = hipGetLastError()) != hipSuccess) return e;
                         uint32_t sq = 0, sb = 0;
                         if ((e = sort_far_queue(S, W, s, sq, sb, /*one_dir=*/true)) != hipSuccess) return e;
@@ -4588,12 +3431,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         }
                         if (sq) {
                             RT_STEP("trace shadow far pass");
-                            if (far_mode(sq) == 4) {
-                                if ((e = launch_far_cells(S, W, sq, flags, s)) != hipSuccess) return e;
-                            } else {
-                                launch_far_any(S, W, sq, flags, s);
-                            }
-                            if ((e = hipGetLastError()) != hipSuccess) return e;
+                            if ((e = launch_far_cells(S, W, sq, flags, s)) != hipSuccess) return e;
                         }
                     }
                 }
@@ -4605,18 +3443,10 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
             continue;
         }
         // level 0 has exactly npix rays; deeper levels read their count on the device
-        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, deep_grid());
+        const int grid = level == 0 ? grid_for(npix, 1 << 20) : grid_for(2 * npix, kDeepGrid);
         if (S.use_bvh) hipLaunchKernelGGL((trace_kernel<true, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
-        else if (S.n_prims <= TILE && trace_scalar())
-        {
-            const int sw = small_trace_wpe();
-            if (sw == 5)
-                hipLaunchKernelGGL((trace_kernel<false, 0, true, false, 5>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
-            else if (sw == 6)
-                hipLaunchKernelGGL((trace_kernel<false, 0, true, false, 6>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
-            else
-                hipLaunchKernelGGL((trace_kernel<false, 0, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
-        }
+        else if (S.n_prims <= TILE)  // small scenes: wave-uniform scalar scene loads
+            hipLaunchKernelGGL((trace_kernel<false, 0, true>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
         else hipLaunchKernelGGL((trace_kernel<false, 0>), dim3(grid), dim3(TB), 0, s, S, F, W, level, 0u, ~0u);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
@@ -4648,33 +3478,9 @@ size_t far_sort_tmp_bytes(uint32_t cap) {
     return std::max(bytes, std::max(rle, scan));
 }
 
-static int ao_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_AO_VARIANT");
-        // scalar scene, 8 waves/SIMD, fast sincos/normalize, sign rejects, two samples per lane
-        // (config 2: 1.519 / 1.539 vs 1.586 / 1.582 ms per frame, profiles/r05/ab/spl_*.json)
-        v = e ? atoi(e) : (4 | 8 | 16 | 1024 | 2048 | 4096 | 32768);
-    }
-    return v;
-}
-
-// Workgroups of the grid-stride small-scene AO launch (RT580_AO_GRID for A/B;
-// 16384 = 64 per CU. Config 2 after the table sincos, 100 frames: 8192 84.4 / 83.5,
-// 16384 84.8 / 85.2, 32768 84.9 / 84.8 Grays/s; 2048-32768 within 2 % before it).
-static unsigned ao_grid() {
-    static int g = -1;
-    if (g < 0) {
-        const char* e = getenv("RT580_AO_GRID");
-        g = e ? atoi(e) : 16384;
-        if (g < 256 || g > (1 << 20)) g = 16384;
-    }
-    return (unsigned)g;
-}
-
 hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W, uint64_t b, uint64_t e,
                          hipStream_t s, const uint64_t* call_lo = nullptr, const uint64_t* call_hi = nullptr);
-hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v,
+hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s,
                            const uint64_t* call_lo = nullptr, const uint64_t* call_hi = nullptr);
 
 hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s) {
@@ -4691,21 +3497,20 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         if (e != hipSuccess) return e;
         const uint64_t calls = (uint64_t)W.far_count_host[4] | ((uint64_t)W.far_count_host[5] << 32);
         const uint64_t items = calls * (uint64_t)F.ao_samples;
-        const bool split = ao_split() != 0 && W.ao_rays && S.bv.nodes4 && !near_wave();
+        if (!W.ao_rays || !S.bv.nodes4) return hipErrorInvalidValue;  // (the shim sizes ao_rays for BVH frames)
         if (W.call_hint && S.bv.has_far && calls &&
             (e = hipMemsetAsync(W.call_hint, 0xff, calls * 4, s)) != hipSuccess)
             return e;
         uint64_t chunk = S.bv.has_far ? (uint64_t)W.far_cap : items;
-        if (split && chunk > (uint64_t)W.ao_cap) chunk = W.ao_cap;
+        if (chunk > (uint64_t)W.ao_cap) chunk = W.ao_cap;
         for (uint64_t b = 0; b < items; b += chunk) {
             const uint64_t e1 = b + chunk < items ? b + chunk : items;
             if (S.bv.has_far && (e = hipMemsetAsync(W.far_count, 0, 8, s)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(W.aofix_count, 0, 4, s)) != hipSuccess) return e;
-            const int wpe = near_wpe();
 #ifdef RT580_DIAGNOSTICS
             const uint32_t c_lo = (uint32_t)(b / (uint64_t)F.ao_samples);
             const uint32_t c_n = (uint32_t)((e1 - 1) / (uint64_t)F.ao_samples) + 1u - c_lo;
-            if (split && audit) {
+            if (audit) {
                 if ((e = hipMemcpyAsync(audit->before, W.occ + c_lo, (size_t)c_n * 4, hipMemcpyDeviceToDevice, s)) !=
                         hipSuccess ||
                     (e = hipMemsetAsync(audit->exp, 0, (size_t)c_n * 4, s)) != hipSuccess ||
@@ -4713,137 +3518,21 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
                     return e;
             }
 #endif
-            if (split) {
-                constexpr int V = 512 | 1024 | 2048 | 4096 | 16384;
-                if (wpe == 5)
-                    hipLaunchKernelGGL((ao_near_kernel_w<5, V>), dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
-                else if (wpe == 6)
-                    hipLaunchKernelGGL((ao_near_kernel_w<6, V>), dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
-                else
-                    hipLaunchKernelGGL((ao_near_kernel_w<8, V>), dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
-                if ((e = hipGetLastError()) != hipSuccess) return e;
-                kt_begin(s);
-                const int twpe = trace_wpe();
-                const int so = ao_sort();
-                if (twpe == 6 && trace_lds() && so == 1)  // (A/B) direction-sorted blocks of 1024 samples
-                    hipLaunchKernelGGL((ao_trace_kernel<6, 16, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
-                                       (uint32_t)F.ao_samples, e1 - b);
-                else if (twpe == 6 && trace_lds() && so == 2)  // 2048 samples, 8 x 8 cells
-                    hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
-                                       (uint32_t)F.ao_samples, e1 - b);
-                else if ((twpe == 7 || twpe == 8) && trace_lds() && so == 3 && ao_budget() == 4 && (ao_spec() & 1)) {
-                    // (A/B) the speculative budget-4 trace at 7 / 8 waves per SIMD (LDS stacks of
-                    // 12 / 8 entries so that the workgroups fit the LDS); the late pass as below
-                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
-                    const dim3 g(grid_for(e1 - b, 16384));
-                    if (twpe == 7)
-                        hipLaunchKernelGGL((ao_trace_kernel<7, 12, 8, 4, 4, 1>), g, dim3(TB), 0, s, S, W,
-                                           (uint32_t)F.ao_samples, e1 - b);
-                    else
-                        hipLaunchKernelGGL((ao_trace_kernel<8, 8, 8, 4, 4, 1>), g, dim3(TB), 0, s, S, W,
-                                           (uint32_t)F.ao_samples, e1 - b);
-                    if ((e = hipGetLastError()) != hipSuccess) return e;
-                    hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 0, 1, 1>), dim3(4096), dim3(TB), 0, s, S, W);
-                }
-                else if (twpe == 6 && trace_lds() && so == 3 && ao_budget() > 0) {  // + step budget, late pass
-                    if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
-                    const int bu = ao_budget();
-                    if ((ao_refill() & 1) && bu >= 3) {  // persistent lanes: budgets 4 (3-5), 8 (6-11), 16 (12+)
-                        const dim3 g(grid_for(e1 - b, 16384));
-                        if (bu <= 5)
-                            hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 4>), g, dim3(TB), 0, s, S, W, e1 - b);
-                        else if (bu <= 11)
-                            hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 8>), g, dim3(TB), 0, s, S, W, e1 - b);
-                        else
-                            hipLaunchKernelGGL((ao_trace_refill_kernel<6, 16, 8, 4, 16>), g, dim3(TB), 0, s, S, W, e1 - b);
-                    }
-                    else if ((ao_spec() & 1) && bu >= 3) {  // budgets 3, 4, 6 (5-6), 8 (7+)
-                        const dim3 g(grid_for(e1 - b, 16384));
-                        const uint32_t ns = (uint32_t)F.ao_samples;
-                        if (bu == 4 && (ao_spec() & 4))
-                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4, 2>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
-                        else if (bu == 4 && (ao_spec() & 8))  // (A/B) 8 x 8 direction cells
-                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 3, 4, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
-                        else if (bu == 4 && (ao_spec() & 16))  // (A/B) blocks of 1024 samples
-                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 4, 4, 4, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
-                        else if (bu == 3)
-                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 3, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
-                        else if (bu <= 4)
-                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
-                        else if (bu <= 6)
-                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 6, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
-                        else
-                            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 8, 1>), g, dim3(TB), 0, s, S, W, ns, e1 - b);
-                    }
-                    else if (bu <= 2)
-                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 2>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
-                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    else if (bu == 3)
-                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 3>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
-                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    else if (bu == 5 || bu == 6)
-                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 6>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
-                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    else if (bu <= 4)
-                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
-                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    else
-                        hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 8>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0,
-                                           s, S, W, (uint32_t)F.ao_samples, e1 - b);
-                    if ((e = hipGetLastError()) != hipSuccess) return e;
-                    if (ao_budget2() > 0) {
-                        hipLaunchKernelGGL((ao_late_kernel<6, 16, 16, 0>), dim3(4096), dim3(TB), 0, s, S, W);
-                        hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 1>), dim3(1024), dim3(TB), 0, s, S, W);
-                    } else if ((ao_refill() & 2) && late_wpe() == 6) {
-                        hipLaunchKernelGGL((ao_late_refill_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
-                    } else {
-#ifdef RT580_DIAGNOSTICS
-                        if (late_wpe() == 8 && late_reread() == 0)
-                            hipLaunchKernelGGL((ao_late_kernel<8, 16, 0, 0, 0>), dim3(4096), dim3(TB), 0, s, S, W);
-                        else
-#endif
-                        if (late_wpe() == 8)
-                            hipLaunchKernelGGL((ao_late_kernel<8, 16>), dim3(4096), dim3(TB), 0, s, S, W);
-                        else if ((ao_spec() & 6) == 6)
-                            hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 0, 1, 2>), dim3(4096), dim3(TB), 0, s, S, W);
-                        else if (ao_spec() & 2)
-                            hipLaunchKernelGGL((ao_late_kernel<6, 16, 0, 0, 1, 1>), dim3(4096), dim3(TB), 0, s, S, W);
-                        else
-                            hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
-                    }
-                } else if (twpe == 6 && trace_lds() && so == 3)  // 2048 samples, 16 x 16 cells (default)
-                    hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S,
-                                       W, (uint32_t)F.ao_samples, e1 - b);
-                else if (twpe == 6 && trace_lds())  // 16-entry LDS stacks (default)
-                    hipLaunchKernelGGL((ao_trace_kernel<6, 16>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
-                                       (uint32_t)F.ao_samples, e1 - b);
-                else if (twpe == 4)
-                    hipLaunchKernelGGL(ao_trace_kernel<4>, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
-                                       (uint32_t)F.ao_samples, e1 - b);
-                else if (twpe == 8)
-                    hipLaunchKernelGGL(ao_trace_kernel<8>, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
-                                       (uint32_t)F.ao_samples, e1 - b);
-                else
-                    hipLaunchKernelGGL(ao_trace_kernel<6>, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
-                                       (uint32_t)F.ao_samples, e1 - b);
-            } else {
+            // the samples' rays (32-byte records), then the budgeted near any-hit in
+            // speculative form (ao_trace_kernel) and the late pass for the rays
+            // out of budget (ao_late_kernel), timed together (kt_*)
+            constexpr int V = 512 | 1024 | 2048 | 4096 | 16384;
+            hipLaunchKernelGGL((ao_near_kernel_w<8, V>), dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
             kt_begin(s);
-            if (near_wave())
-                hipLaunchKernelGGL((ao_near_kernel_w<8, 512 | 1024 | 2048 | 4096 | 8192>), dim3(grid_for(e1 - b, 8192)),
-                                   dim3(TB), 0, s, S, F, W, b, e1);
-            else if (wpe == 5)
-                hipLaunchKernelGGL(ao_near_kernel_w<5>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
-            else if (wpe == 6)
-                hipLaunchKernelGGL(ao_near_kernel_w<6>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
-            else if (wpe == 8)
-                hipLaunchKernelGGL(ao_near_kernel_w<8>, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
-            else
-                hipLaunchKernelGGL(ao_near_kernel, dim3(grid_for(e1 - b, 8192)), dim3(TB), 0, s, S, F, W, b, e1);
-            }
+            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
+                               e1 - b);
+            hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
             kt_end(s, e1 - b);
             if ((e = hipGetLastError()) != hipSuccess) return e;
 #ifdef RT580_DIAGNOSTICS
-            if (split && audit) {  // (before the fix-up pass adds to the queue and the counts)
+            if (audit) {  // (before the fix-up pass adds to the queue and the counts)
                 hipLaunchKernelGGL(ao_audit_expect_kernel, dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W, e1 - b,
                                    c_lo, audit->exp, audit->aud, g_verify_out);
                 hipLaunchKernelGGL(ao_audit_compare_kernel, dim3(4096), dim3(TB), 0, s, S, W, c_lo, c_n,
@@ -4875,17 +3564,7 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             }
 #endif
             if (nq == 0) continue;
-            const int fm = far_mode(nq);
-            if (fm == 4) {
-                if ((e = launch_far_cells(S, W, nq, (uint8_t*)nullptr, s)) != hipSuccess) return e;
-            } else if (fm == 1)
-                launch_far_any(S, W, nq, (uint8_t*)nullptr, s);
-            else if (fm == 2)
-                hipLaunchKernelGGL(far_any_lane_kernel, dim3(grid_for(nq, 16384)), dim3(TB), 0, s, S, W, nq,
-                                   (uint8_t*)nullptr);
-            else
-                hipLaunchKernelGGL(far_scan_kernel, dim3(grid_for((uint64_t)nq * 64, 16384)), dim3(TB), 0, s, S, W,
-                                   0u, nq, 0, (int)S.bv.n_far, 0, (uint8_t*)nullptr);
+            if ((e = launch_far_cells(S, W, nq, (uint8_t*)nullptr, s)) != hipSuccess) return e;
 #ifdef RT580_DIAGNOSTICS
             {
                 unsigned long long st[9];
@@ -4907,16 +3586,15 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
         }
         return hipSuccess;
     }
-    const int v = ao_variant();  // (frame_init_kernel zeroed W.aofix_count)
-    kt_begin(s);
-    const hipError_t e = launch_ao_small(S, F, W, s, v);
+    kt_begin(s);  // (frame_init_kernel zeroed W.aofix_count)
+    const hipError_t e = launch_ao_small(S, F, W, s);
     kt_end(s, 0);  // one launch per frame: its AO rays are the frame's (no host sync here)
-    if (e != hipSuccess || !(v & 4096)) return e;
+    if (e != hipSuccess) return e;
     return launch_ao_fix(S, F, W, 0, ~0ull, s);
 }
 
 bool ao_calls_supported(const DevScene& S, const DevFrame& F) {
-    return !S.use_bvh && F.ao_enabled && S.n_ambient > 0 && (ao_variant() & (16 | 4096)) == (16 | 4096);
+    return !S.use_bvh && F.ao_enabled && S.n_ambient > 0;
 }
 
 hipError_t launch_ao_calls(const DevScene& S, const DevFrame& F, const DevWork& W, const uint64_t* call_lo,
@@ -4926,7 +3604,7 @@ hipError_t launch_ao_calls(const DevScene& S, const DevFrame& F, const DevWork& 
     // a fresh fix-up queue for this range (frame_init_kernel zeroed it for the first)
     hipError_t e = hipMemsetAsync(W.aofix_count, 0, 4, s);
     if (e != hipSuccess) return e;
-    if ((e = launch_ao_small(S, F, W, s, ao_variant(), call_lo, call_hi)) != hipSuccess) return e;
+    if ((e = launch_ao_small(S, F, W, s, call_lo, call_hi)) != hipSuccess) return e;
     return launch_ao_fix(S, F, W, 0, ~0ull, s, call_lo, call_hi);
 }
 
@@ -4940,60 +3618,22 @@ hipError_t launch_ao_fix(const DevScene& S, const DevFrame& F, const DevWork& W,
     return hipGetLastError();
 }
 
-hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s, int v,
+// Small-scene AO (brute force): the wave-uniform scalar scene loop, sign-decided
+// rejections, the fast sincos / unit-vector sequences with the exact fix-up
+// queue, two samples per lane, 8 waves per SIMD (ao_kernel_occ8; config 2:
+// 1.519 / 1.539 vs 1.586 / 1.582 ms per frame for one sample per lane,
+// profiles/r05/ab/spl_*.json). 16384 workgroups (64 per CU; 8192 / 32768
+// within 1 %).
+hipError_t launch_ao_small(const DevScene& S, const DevFrame& F, const DevWork& W, hipStream_t s,
                            const uint64_t* call_lo, const uint64_t* call_hi) {
-    if (v & 16) {
-        switch (v & ~16) {
-#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel_occ8<v>, dim3(ao_grid()), dim3(TB), 0, s, S, F, W, call_lo, call_hi); break;
-            RT_AO_CASE(1) RT_AO_CASE(9) RT_AO_CASE(8) RT_AO_CASE(1032) RT_AO_CASE(2056) RT_AO_CASE(3080)
-            RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(5128) RT_AO_CASE(7180) RT_AO_CASE(7182)
-            RT_AO_CASE(32768 | 7180)
-#undef RT_AO_CASE
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
-    if (v >= 32) {  // A/B variants; 32/64 (timing ablations with wrong output) only in diagnostic builds
-        switch (v) {
-#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
-#ifdef RT580_DIAGNOSTICS
-            RT_AO_CASE(41) RT_AO_CASE(73) RT_AO_CASE(105) RT_AO_CASE(137) RT_AO_CASE(233)
-#endif
-            RT_AO_CASE(1032) RT_AO_CASE(3080) RT_AO_CASE(3084) RT_AO_CASE(7176) RT_AO_CASE(7180) RT_AO_CASE(7182)
-            RT_AO_CASE(32768 | 7180)
-#undef RT_AO_CASE
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
-    switch (v) {
-#define RT_AO_CASE(v) case v: hipLaunchKernelGGL(ao_kernel<v>, dim3(8192), dim3(TB), 0, s, S, F, W); break;
-        RT_AO_CASE(0) RT_AO_CASE(1) RT_AO_CASE(2) RT_AO_CASE(3)
-        RT_AO_CASE(4) RT_AO_CASE(5) RT_AO_CASE(6) RT_AO_CASE(7)
-        RT_AO_CASE(8) RT_AO_CASE(9) RT_AO_CASE(10) RT_AO_CASE(11)
-        RT_AO_CASE(12) RT_AO_CASE(13) RT_AO_CASE(14) RT_AO_CASE(15)
-#undef RT_AO_CASE
-    }
+    constexpr int V = 4 | 8 | 1024 | 2048 | 4096 | 32768;
+    hipLaunchKernelGGL(ao_kernel_occ8<V>, dim3(16384), dim3(TB), 0, s, S, F, W, call_lo, call_hi);
     return hipGetLastError();
-}
-
-// RT580_RESOLVE=0: the per-pixel stack form (A/B only).
-static bool resolve_by_level() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("RT580_RESOLVE");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
 }
 
 hipError_t launch_resolve(const DevScene& S, const DevFrame& F, const DevWork& W, int16_t* fb, hipStream_t s) {
     const uint64_t npix = (uint64_t)F.n_rows * F.width;
     if (npix == 0) return hipSuccess;
-    if (!resolve_by_level()) {
-        hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)((npix + TB - 1) / TB)), dim3(TB), 0, s, S, F, W, fb);
-        return hipGetLastError();
-    }
     return launch_resolve_range(S, F, W, fb, 0, (uint32_t)npix, s);
 }
 
@@ -5001,7 +3641,7 @@ hipError_t launch_resolve_range(const DevScene& S, const DevFrame& F, const DevW
                                 uint32_t p_hi, hipStream_t s) {
     const uint64_t npix = (uint64_t)F.n_rows * F.width;
     for (int level = F.depth; level >= 0; level--) {
-        const int grid = level == 0 ? grid_for(p_hi - p_lo, 1 << 20) : grid_for(2 * npix, deep_grid());
+        const int grid = level == 0 ? grid_for(p_hi - p_lo, 1 << 20) : grid_for(2 * npix, kDeepGrid);
         hipLaunchKernelGGL(resolve_level_kernel, dim3(grid), dim3(TB), 0, s, S, F, W, level, fb, p_lo, p_hi);
     }
     return hipGetLastError();

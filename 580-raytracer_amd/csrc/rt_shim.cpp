@@ -101,7 +101,7 @@ struct State {
     static constexpr int kSlots = 4;
     Slot slot[kSlots];
     int nslots = 3;            // slots in use (RT580_SLOTS): frames in flight
-    int small_slots = 3;       // the same for whole small-scene frames (RT580_SMALL_SLOTS)
+    int small_slots = 3;       // the same for whole small-scene frames
     int cur = 0;               // slot of the frame being enqueued
     int last_slot = -1;        // slot of the previous frame call
     uint64_t frames = 0;       // frames begun
@@ -576,16 +576,6 @@ DevFrame dev_frame(const rt_render_params* p, int row_begin, int row_step, int n
     return f;
 }
 
-// RT580_AO_RESUME=0 (A/B): late AO rays start their walk over in ao_late_kernel.
-bool ao_resume() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("RT580_AO_RESUME");
-        v = e ? std::atoi(e) : 1;
-    }
-    return v != 0;
-}
-
 DevWork dev_work() {
     DevWork w;
     w.nodes = (NodeRec*)SL.nodes.p;
@@ -608,11 +598,6 @@ DevWork dev_work() {
     w.occ = (uint32_t*)SL.occ.p;
     w.mt_stream = (const uint32_t*)SL.mt_stream.p;
     w.mt_base = SL.mt_base;
-    static const uint32_t refill_min = [] {
-        const char* e = std::getenv("RT580_AO_REFILL_MIN");
-        return e ? (uint32_t)std::atoi(e) : 32u;
-    }();
-    w.refill_min = refill_min;
     w.node_cap = g.node_cap;
     w.call_cap = g.call_cap;
     w.far_rays = (float4*)SL.far_rays.p;
@@ -633,7 +618,7 @@ DevWork dev_work() {
     w.ao_rays = w.ao_cap ? (float4*)SL.ao_rays.p : nullptr;
     w.ao_late = w.ao_cap ? (uint32_t*)SL.ao_late.p : nullptr;
     w.ao_late_count = w.ao_cap ? (uint32_t*)SL.ao_late_count.p : nullptr;
-    w.ao_state_cap = w.ao_cap && ao_resume() ? w.ao_cap / 16 : 0u;
+    w.ao_state_cap = w.ao_cap ? w.ao_cap / 16 : 0u;
     w.ao_state = w.ao_state_cap ? (uint32_t*)SL.ao_state.p : nullptr;
     const bool split = g.bvh_ok && !g.bvh.far_nodes.empty();
     w.hit4 = split ? (float4*)SL.hit4.p : nullptr;
@@ -643,14 +628,7 @@ DevWork dev_work() {
                                                                                                       : nullptr;
     w.aofix_items = (uint64_t*)SL.aofix_items.p;
     w.aofix_count = (uint32_t*)SL.aofix_count.p;
-    {   // RT580_CALL_HINT=0 (A/B): no per-call acceptor hints
-        static int hint = -1;
-        if (hint < 0) {
-            const char* e = std::getenv("RT580_CALL_HINT");
-            hint = e ? std::atoi(e) : 1;
-        }
-        w.call_hint = hint ? (uint32_t*)SL.call_hint.p : nullptr;
-    }
+    w.call_hint = (uint32_t*)SL.call_hint.p;  // per-call acceptor hints of the brute any-hit scans
     w.aofix_cap = (uint32_t)(SL.aofix_items.bytes / 8);
     w.poison = (const uint32_t*)SL.bad.p;
     return w;
@@ -734,7 +712,7 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     g.frame_fc = 0;
     if (g.bvh_ok && SL.ao_cap < ac) {  // ray records of the split AO pass (ao_trace_kernel)
         if (ensure(SL.ao_rays, (size_t)ac * 32) || ensure(SL.ao_late, (size_t)ac * 4) || ensure(SL.ao_late_count, 64) ||
-            (ao_resume() && ensure(SL.ao_state, 2 * (size_t)(ac / 16) * kLateWords * 4)))
+            ensure(SL.ao_state, (size_t)(ac / 16) * kLateWords * 4))
             return RT_FAILURE;
         SL.ao_cap = ac;
     }
@@ -949,16 +927,9 @@ int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global
 }
 
 // The frame's phase boundaries for rt_gpu_last_stats (ms_count, ms_scan,
-// ms_render). RT580_PHASE_EVENTS=0 (A/B): only the frame's start and end are
-// recorded -- each event between two kernels of a stream costs that stream a
-// few microseconds of idle.
+// ms_render). (Recording only the frame's start and end instead: no difference
+// measured, profiles/r05/ab.)
 static hipError_t phase_mark(int e, hipStream_t s) {
-    static int on = -1;
-    if (on < 0) {
-        const char* v = std::getenv("RT580_PHASE_EVENTS");
-        on = v ? std::atoi(v) : 1;
-    }
-    if (!on && !g.profiling) return hipSuccess;
     return hipEventRecord(g.ev[e], s);
 }
 
@@ -1118,8 +1089,7 @@ int rt_gpu_init(int device) {
         g.pipeline = !(e && std::atoi(e) == 0);
         const char* ns = std::getenv("RT580_SLOTS");  // frames in flight (2-4)
         g.nslots = ns ? std::atoi(ns) : 3;
-        const char* ss = std::getenv("RT580_SMALL_SLOTS");
-        g.small_slots = std::min(ss ? std::atoi(ss) : 3, g.nslots);
+        g.small_slots = g.nslots;
     }
     if (const char* e = std::getenv("RT580_CHUNK_LOG2")) {
         char* end = nullptr;
@@ -1204,14 +1174,12 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         // far-search direction grid: 2048^2 cells (field100k: 19.4 candidates
         // per far-pass ray against 33.7 at 1024^2; 139M list entries, 5.6 s host
         // build; config 5's 1M triangles: its row sample 1,370 -> 1,227 ms, 12 s
-        // build; RT580_GRID_LOG2: other sizes, 0 = plane tree only)
-        int glog2 = 11;
-        if (const char* e = std::getenv("RT580_GRID_LOG2")) glog2 = std::atoi(e);
-        if (g.bvh_ok && glog2 > 0 && glog2 <= 12) build_dir_grid(s->prims, g.bvh, glog2);
+        // build)
+        constexpr int glog2 = 11;
+        if (g.bvh_ok) build_dir_grid(s->prims, g.bvh, glog2);
         if (g.bvh_ok && grid_coarse_px() > 0) coarsen_dir_grid(g.bvh);
-        // the 4-wide form for the any-hit queries (AO, shadows); RT580_BVH4=0: binary only
-        const char* b4 = std::getenv("RT580_BVH4");
-        if (g.bvh_ok && !(b4 && std::atoi(b4) == 0)) collapse_bvh4(g.bvh);
+        // the 4-wide form for the near queries (AO, shadows, trace levels)
+        if (g.bvh_ok) collapse_bvh4(g.bvh);
         if (g.bvh_ok &&
             (upload_vec(g.bvh_nodes, g.bvh.nodes, "the BVH nodes") ||
              upload_vec(g.bvh_nodes4, g.bvh.nodes4q, "the 4-wide BVH nodes") ||
@@ -1473,12 +1441,8 @@ static int enqueue_split(const rt_render_params* p, int16_t* fb_out, hipStream_t
         uint64_t tot = 0, tail = 0;
         for (uint32_t v : rc) tot += v;
         int r = H;
-        static long pct = -1;  // RT580_LAT_SPLIT_PCT: the second part's share of the AO calls
-        if (pct < 0) {
-            const char* e = std::getenv("RT580_LAT_SPLIT_PCT");
-            pct = e ? std::atol(e) : 20;
-        }
-        while (r > 1 && (tail < (tot * (uint64_t)pct + 99) / 100 || r > H - 1)) tail += rc[(size_t)--r];
+        constexpr uint64_t pct = 20;  // the second part's share of the AO calls
+        while (r > 1 && (tail < (tot * pct + 99) / 100 || r > H - 1)) tail += rc[(size_t)--r];
         g.lat_params = *p;
         g.lat_gen = g.scene_gen;
         g.lat_row = r;

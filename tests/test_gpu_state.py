@@ -460,17 +460,15 @@ def test_render_async_frames_land_in_registered_buffers():
 
 
 
-@pytest.mark.parametrize("late_wpe,refill,spec", [("6", "0", "0"), ("8", "0", "0"), ("6", "3", "0"), ("6", "0", "3"), ("6", "0", "7")])
-def test_ao_audit_of_the_product_trace_and_late_passes(tmp_path, late_wpe, refill, spec):
+def test_ao_audit_of_the_product_trace_and_late_passes(tmp_path):
     """Diagnostic build, RT580_AO_VERIFY=1 (rt_kernels.hip ao_audit_*): on the
     north-star frame, every near-query AO ray is answered again by the
     unbudgeted query, and the occlusion counts and far queue that implies are
     compared with what ao_trace_kernel / ao_late_kernel wrote -- their code is
-    the product's (the audit adds kernels only). Both builds of the late pass:
-    the 64-VGPR one (RT580_LATE_WPE=8) queued origins not their own before the
-    ray record was re-read after the traversal (round 5); and the trace pass's
-    persistent-lane form (RT580_AO_REFILL=1) and its speculative while-while
-    form (RT580_AO_SPEC=1)."""
+    the product's (the audit adds kernels only): the budgeted speculative walk,
+    the saved walks resumed by the late pass, and the late pass's re-read ray
+    record (round 5: a 64-VGPR build of it, since removed, queued origins not
+    their own when the origin stayed live across the walk)."""
     import json
     import os
     import subprocess
@@ -478,8 +476,7 @@ def test_ao_audit_of_the_product_trace_and_late_passes(tmp_path, late_wpe, refil
     diag = os.path.join(helpers.REPO, "580-raytracer_amd", "lib580rt_diag.so")
     if not os.path.exists(diag):
         pytest.skip("diagnostic build absent (make diag)")
-    env = dict(os.environ, RT580_LIB=diag, RT580_AO_VERIFY="1", RT580_LATE_WPE=late_wpe, RT580_AO_REFILL=refill,
-               RT580_AO_SPEC=spec)
+    env = dict(os.environ, RT580_LIB=diag, RT580_AO_VERIFY="1")
     r = subprocess.run([sys.executable, os.path.join(helpers.REPO, "tools", "ao_verify.py"), "field100k_1080p", "2"],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -10,7 +10,7 @@ and the occlusion counts and far queue that implies against what the product's
 ao_trace_kernel / ao_late_kernel wrote (their code is untouched by the audit).
 
     RT580_LIB=580-raytracer_amd/lib580rt_diag.so RT580_AO_VERIFY=1 \\
-        [RT580_LATE_WPE=8] python tools/ao_verify.py [workload] [frames] [--small WxH]
+        python tools/ao_verify.py [workload] [frames] [--small WxH]
 
 Prints one JSON line: frame hashes, whether they agree, replay errors, the
 verification totals and the first wrong rays.
@@ -71,7 +71,7 @@ def main():
     head = b"P6\n%d %d\n255\n" % (W, H)  # the PPM as FlushFrameBufferToPPM writes it (bench.py frame_check)
     hashes = [helpers.sha256(head + o.cpu().numpy().tobytes()) if o is not None else None for o in outs]
     res = {"workload": name, "width": W, "height": H, "frames": frames,
-           "late_wpe": os.environ.get("RT580_LATE_WPE", "6"), "hashes": hashes,
+           "hashes": hashes,
            "frames_agree": len(set(h for h in hashes if h)) <= 1, "replay_errors": errors}
     if hasattr(lib, "rt580_diag_ao_verify"):
         v = np.zeros(64, dtype=np.uint64)
