@@ -1277,6 +1277,9 @@ static HostRange* host_range_ready(const void* host, size_t bytes) {
     HostRange* hr = host_range(host, bytes);
     if (!hr) return nullptr;
     if (hr->copied && hr->copied_device != g.device) {
+        // a copy from the other device may still be in flight: it completes
+        // before the range changes hands (frames land in call order)
+        if (hipEventSynchronize(hr->copied) != hipSuccess) return nullptr;
         (void)hipEventDestroy(hr->copied);
         hr->copied = nullptr;
     }
@@ -1599,6 +1602,9 @@ int rt_gpu_host_unregister(void* host_ptr) {
     RT_ENTRY("rt_gpu_host_unregister");
     for (size_t i = 0; i < g_host_ranges.size(); i++)
         if (g_host_ranges[i].p == (const char*)host_ptr) {
+            // the range's last write (possibly on a caller-supplied stream,
+            // rt_gpu_deinterleave_ppm), then every context's streams
+            if (g_host_ranges[i].copied) (void)hipEventSynchronize(g_host_ranges[i].copied);
             for (int k = 0; k < kMaxCtx; k++)  // no copy into it may still be in flight
                 if (g_ctx[k].inited) {
                     const int cur = g_cur;
@@ -1899,6 +1905,7 @@ namespace {
 void destroy_comms();
 void release_multi();
 void release_multi_ctx(int k);
+int rank_teardown();
 
 void shutdown_ctx() {
     if (!g.inited) return;
@@ -1954,6 +1961,8 @@ extern "C" {
 void rt_gpu_shutdown(void) {
     RT_ENTRY("rt_gpu_shutdown");
     const int cur = g_cur;
+    if (g_ctx[0].inited) (void)hipSetDevice(g_ctx[0].device);
+    (void)rank_teardown();
     release_multi();
     for (int k = kMaxCtx - 1; k >= 0; k--) {
         g_cur = k;
@@ -1981,6 +1990,8 @@ struct Rccl {
     decltype(&ncclGroupStart) GroupStart = nullptr;
     decltype(&ncclGroupEnd) GroupEnd = nullptr;
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;  // the one-process-per-GPU path (rt_gpu_rank_*)
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
 } g_rccl;
 
 bool rccl_load() {
@@ -2000,9 +2011,12 @@ bool rccl_load() {
     RT_RCCL_SYM(GroupStart);
     RT_RCCL_SYM(GroupEnd);
     RT_RCCL_SYM(GetErrorString);
+    RT_RCCL_SYM(GetUniqueId);
+    RT_RCCL_SYM(CommInitRank);
 #undef RT_RCCL_SYM
     if (!g_rccl.CommInitAll || !g_rccl.CommDestroy || !g_rccl.AllGather || !g_rccl.Send || !g_rccl.Recv ||
-        !g_rccl.GroupStart || !g_rccl.GroupEnd || !g_rccl.GetErrorString) {
+        !g_rccl.GroupStart || !g_rccl.GroupEnd || !g_rccl.GetErrorString || !g_rccl.GetUniqueId ||
+        !g_rccl.CommInitRank) {
         dlclose(g_rccl.h);
         g_rccl.h = nullptr;
         return false;
@@ -2377,6 +2391,158 @@ int multi_frame_async(const rt_render_params* p, uint8_t* ppm_host, int n, const
     return ordered_d2h(hr, ppm_host, g_multi.a_frame8[r].p, body, g.stream);
 }
 
+// ---------------------------------------------------------------- one process per GPU
+// The rank's side of a world of processes, one GPU each (rt_gpu_rank_*): the
+// library owns the world's RCCL communicator and runs the rank's frame loop --
+// count, all-gather, shade, gather -- with no host wait and no Python in it.
+//
+// Ordering. Every collective of the rank runs on one stream (xs), in the order
+// the calls enqueue them, and every rank makes the same calls: the
+// communicator sees one sequence per rank, the same on all ranks, so no two
+// collectives can wait on each other across ranks. A frame's gather is
+// enqueued by the NEXT frame call, after that frame's all-gather:
+//   xs: allgather(k) | wait shaded(k-1), gather(k-1), PPM(k-1) | allgather(k+1) | ...
+// so frame k+1's shading waits only for frame k-1's (two frames' AO phases run
+// together, as frames do on one GPU), never for frame k's. Buffers come from a
+// ring of three sets; frame k+3 starts after frame k's gather (g.stream waits
+// its xs event), which is after every read of frame k's set.
+struct RankLoop {
+    bool on = false;
+    int world = 0, rank = 0, device = -1;
+    ncclComm_t comm = nullptr;
+    hipStream_t xs = nullptr;
+    static constexpr int kRing = 3;
+    int ring = 0;
+    DevBuf rc[kRing], gat[kRing], base[kRing], t8[kRing], root8[kRing];
+    hipEvent_t counted[kRing] = {}, gathered[kRing] = {}, shaded[kRing] = {}, done[kRing] = {};
+    bool done_valid[kRing] = {};
+    // the frame whose tiles are still to be gathered (enqueued by the next call)
+    bool pending = false;
+    int pend_r = 0;
+    rt_render_params pend_p{};
+    uint8_t* pend_host = nullptr;
+} g_rank;
+
+int rank_teardown() {
+    int st = RT_SUCCESS;
+    if (g_rank.xs && hipStreamSynchronize(g_rank.xs) != hipSuccess) st = RT_FAILURE;
+    if (g_rank.comm) (void)g_rccl.CommDestroy(g_rank.comm);
+    g_rank.comm = nullptr;
+    for (int r = 0; r < RankLoop::kRing; r++) {
+        for (DevBuf* b : {&g_rank.rc[r], &g_rank.gat[r], &g_rank.base[r], &g_rank.t8[r], &g_rank.root8[r]}) release(*b);
+        for (hipEvent_t* e : {&g_rank.counted[r], &g_rank.gathered[r], &g_rank.shaded[r], &g_rank.done[r]}) {
+            if (*e) (void)hipEventDestroy(*e);
+            *e = nullptr;
+        }
+        g_rank.done_valid[r] = false;
+    }
+    if (g_rank.xs) (void)hipStreamDestroy(g_rank.xs);
+    g_rank.xs = nullptr;
+    g_rank.on = false;
+    g_rank.pending = false;
+    return st;
+}
+
+// The gather of the pending frame's u8 tiles to rank 0 and, on rank 0, its PPM
+// body into the host range; on xs, after that frame's shading.
+int rank_gather_pending() {
+    if (!g_rank.pending) return RT_SUCCESS;
+    g_rank.pending = false;
+    const rt_render_params* p = &g_rank.pend_p;
+    const int r = g_rank.pend_r, n = g_rank.world, H = p->height, W = p->width;
+    const int n_max = (H + n - 1) / n;
+    const size_t t8 = (size_t)n_max * W * 3, body = (size_t)H * W * 3;
+    hipStream_t xs = g_rank.xs;
+    HIP_TRY(hipStreamWaitEvent(xs, g_rank.shaded[r], 0));
+    if (g_rank.rank == 0) {
+        HIP_TRY(hipMemcpyAsync(g_rank.root8[r].p, g_rank.t8[r].p, t8, hipMemcpyDeviceToDevice, xs));
+        if (n > 1) {
+            RCCL_TRY(g_rccl.GroupStart());
+            for (int k = 1; k < n; k++)
+                RCCL_TRY(g_rccl.Recv((char*)g_rank.root8[r].p + (size_t)k * t8, t8, ncclUint8, k, g_rank.comm, xs));
+            RCCL_TRY(g_rccl.GroupEnd());
+        }
+        HostRange* hr = host_range_ready(g_rank.pend_host, body);
+        if (!hr) return fail("rt_gpu_render_rank_async: the buffer is not a registered range of %zu bytes", body);
+        HIP_TRY(hipStreamWaitEvent(xs, hr->copied, 0));
+        if (uint8_t* dst = (uint8_t*)mapped(hr, g_rank.pend_host)) {  // straight into the host range
+            HIP_TRY(launch_deinterleave_u8((const uint8_t*)g_rank.root8[r].p, n, n_max, W, H, dst, xs));
+        } else {
+            if (ensure(g.ppm_stage, body)) return RT_FAILURE;
+            HIP_TRY(launch_deinterleave_u8((const uint8_t*)g_rank.root8[r].p, n, n_max, W, H,
+                                           (uint8_t*)g.ppm_stage.p, xs));
+            HIP_TRY(hipMemcpyAsync(g_rank.pend_host, g.ppm_stage.p, body, hipMemcpyDeviceToHost, xs));
+        }
+        HIP_TRY(hipEventRecord(hr->copied, xs));
+    } else {
+        RCCL_TRY(g_rccl.Send(g_rank.t8[r].p, t8, ncclUint8, 0, g_rank.comm, xs));
+    }
+    HIP_TRY(hipEventRecord(g_rank.done[r], xs));
+    g_rank.done_valid[r] = true;
+    return RT_SUCCESS;
+}
+
+int rank_frame(const rt_render_params* p, uint8_t* ppm_host) {
+    if (!g_rank.on) return fail("rt_gpu_render_rank_async: rt_gpu_rank_init not called");
+    if (check_params(p)) return RT_FAILURE;
+    if (p->row_begin != 0 || p->row_step != 1 || p->row_end != p->height)
+        return fail("rt_gpu_render_rank_async renders whole frames (row_begin 0, row_step 1, row_end height)");
+    if (g.device != g_rank.device) return fail("rt_gpu_render_rank_async: the communicator's device changed");
+    const int n = g_rank.world, rank = g_rank.rank, H = p->height, W = p->width;
+    const int n_max = (H + n - 1) / n;
+    const size_t t8 = (size_t)n_max * W * 3, body = (size_t)H * W * 3;
+    if (rank == 0 && !host_range(ppm_host, body))
+        return fail("rt_gpu_render_rank_async: rank 0's buffer is not a registered range of %zu bytes", body);
+    HIP_TRY(hipSetDevice(g.device));
+    const int r = g_rank.ring;
+    g_rank.ring = (r + 1) % RankLoop::kRing;
+    // the ring set's last frame has been gathered (every read of the set is before that)
+    if (g_rank.pending && g_rank.pend_r == r && rank_gather_pending()) return RT_FAILURE;
+    if (g_rank.done_valid[r]) HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.done[r], 0));
+    if (ensure(g_rank.rc[r], (size_t)n_max * 4) || ensure(g_rank.gat[r], (size_t)n * n_max * 4) ||
+        ensure(g_rank.base[r], (size_t)n_max * 8) || ensure(g_rank.t8[r], t8) ||
+        (rank == 0 && ensure(g_rank.root8[r], t8 * n)))
+        return RT_FAILURE;
+    rt_render_params pk = *p;
+    pk.row_begin = rank;
+    pk.row_step = n;
+    pk.row_end = H;
+    // phase 1: this rank's rows traced, their AO calls counted (padding rows count 0)
+    HIP_TRY(hipMemsetAsync(g_rank.rc[r].p, 0, (size_t)n_max * 4, g.stream));
+    if (rt_gpu_count_rows(&pk, (uint32_t*)g_rank.rc[r].p)) return RT_FAILURE;
+    // the exchange: every rank's per-row counts (H int32 in all)
+    HIP_TRY(hipEventRecord(g_rank.counted[r], g.stream));
+    HIP_TRY(hipStreamWaitEvent(g_rank.xs, g_rank.counted[r], 0));
+    RCCL_TRY(g_rccl.AllGather(g_rank.rc[r].p, g_rank.gat[r].p, (size_t)n_max, ncclInt32, g_rank.comm, g_rank.xs));
+    HIP_TRY(hipEventRecord(g_rank.gathered[r], g_rank.xs));
+    HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.gathered[r], 0));
+    // phase 2: RNG bases of this rank's rows, shading, the rows' PPM bytes
+    if (rt_gpu_row_bases((const int32_t*)g_rank.gat[r].p, n, n_max, H, rank, (uint64_t*)g_rank.base[r].p))
+        return RT_FAILURE;
+    if (!g.split_ready || std::memcmp(&g.split_params, &pk, sizeof pk) != 0)
+        return fail("rt_gpu_render_rank_async: the count pass did not complete");
+    g.split_ready = false;
+    if (slot_wait_user()) return RT_FAILURE;  // the row bases were produced on the caller's stream
+    const size_t nv = (size_t)n_selected_rows(&pk) * W * 3;
+    if (ensure(SL.fb, nv * 2)) return RT_FAILURE;  // the slot's own int16 rows
+    if (shade_rows(&pk, pk.row_begin, pk.row_step, n_selected_rows(&pk), (const uint64_t*)g_rank.base[r].p,
+                   (int16_t*)SL.fb.p))
+        return RT_FAILURE;
+    HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, nv, (uint8_t*)g_rank.t8[r].p, fs()));
+    // the slot's end without the caller's stream waiting for it: the gather (on
+    // xs, next call) waits for `shaded`, the caller's stream goes on
+    if (post_replay_check()) return RT_FAILURE;
+    if (g.pipeline) HIP_TRY(hipEventRecord(SL.done, fs()));
+    HIP_TRY(hipEventRecord(g_rank.shaded[r], fs()));
+    // the previous frame's gather, after this frame's all-gather on xs
+    if (rank_gather_pending()) return RT_FAILURE;
+    g_rank.pending = true;
+    g_rank.pend_r = r;
+    g_rank.pend_p = *p;
+    g_rank.pend_host = ppm_host;
+    return RT_SUCCESS;
+}
+
 }  // namespace
 
 extern "C" int rt_gpu_render_multi_async(const rt_render_params* p, uint8_t* ppm_body_host, int n_devices,
@@ -2396,6 +2562,65 @@ extern "C" int rt_gpu_render_multi(const rt_render_params* p, int16_t* fb_out, i
     g_cur = 0;
     if (g.inited) (void)hipSetDevice(g.device);
     return st;
+}
+
+extern "C" int rt_gpu_rank_unique_id(void* id_out, uint64_t id_bytes) {
+    RT_ENTRY("rt_gpu_rank_unique_id");
+    if (!id_out || id_bytes < sizeof(ncclUniqueId)) return fail("rt_gpu_rank_unique_id: need %zu bytes", sizeof(ncclUniqueId));
+    if (!rccl_load()) return fail("rt_gpu_rank_unique_id: librccl.so.1 could not be loaded");
+    ncclUniqueId id;
+    RCCL_TRY(g_rccl.GetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof id);
+    return RT_SUCCESS;
+}
+
+extern "C" int rt_gpu_rank_init(const void* id, uint64_t id_bytes, int world, int rank) {
+    RT_WORK("rt_gpu_rank_init");
+    if (g_cur != 0) return fail("re-entered");
+    if (!id || id_bytes < sizeof(ncclUniqueId)) return fail("rt_gpu_rank_init: need a %zu-byte id", sizeof(ncclUniqueId));
+    if (world < 1 || rank < 0 || rank >= world) return fail("rt_gpu_rank_init: bad world %d / rank %d", world, rank);
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (!rccl_load()) return fail("rt_gpu_rank_init: librccl.so.1 could not be loaded");
+    if (g_rank.on && rank_teardown()) return fail("rt_gpu_rank_init: the previous communicator's work failed");
+    HIP_TRY(hipSetDevice(g.device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    RCCL_TRY(g_rccl.CommInitRank(&g_rank.comm, world, uid, rank));
+    HIP_TRY(hipStreamCreateWithFlags(&g_rank.xs, hipStreamNonBlocking));
+    for (int r = 0; r < RankLoop::kRing; r++)
+        for (hipEvent_t* e : {&g_rank.counted[r], &g_rank.gathered[r], &g_rank.shaded[r], &g_rank.done[r]})
+            HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    g_rank.world = world;
+    g_rank.rank = rank;
+    g_rank.device = g.device;
+    g_rank.ring = 0;
+    g_rank.on = true;
+    return RT_SUCCESS;
+}
+
+extern "C" int rt_gpu_render_rank_async(const rt_render_params* p, uint8_t* ppm_body_host) {
+    RT_WORK("rt_gpu_render_rank_async");
+    if (g_cur != 0) return fail("re-entered");
+    return rank_frame(p, ppm_body_host);
+}
+
+extern "C" int rt_gpu_rank_finish(void) {
+    RT_WORK("rt_gpu_rank_finish");
+    if (!g_rank.on) return fail("rt_gpu_rank_finish: rt_gpu_rank_init not called");
+    HIP_TRY(hipSetDevice(g.device));
+    if (rank_gather_pending()) return RT_FAILURE;
+    // the caller's stream (and rt_gpu_synchronize) sees the exchange's end
+    const int last = (g_rank.ring + RankLoop::kRing - 1) % RankLoop::kRing;
+    if (g_rank.done_valid[last]) HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.done[last], 0));
+    return RT_SUCCESS;
+}
+
+extern "C" int rt_gpu_rank_shutdown(void) {
+    RT_ENTRY("rt_gpu_rank_shutdown");
+    if (!g_rank.on) return RT_SUCCESS;
+    (void)hipSetDevice(g_rank.device);
+    if (rank_teardown()) return fail("rt_gpu_rank_shutdown: the exchange stream reported an error");
+    return RT_SUCCESS;
 }
 
 extern "C" int rt_gpu_device_count(void) {

@@ -79,6 +79,11 @@ SIGNATURES = [
                                                 ctypes.c_void_p, ctypes.c_void_p]),
     ("rt_gpu_shade_rows_ppm", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p]),
+    ("rt_gpu_rank_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    ("rt_gpu_rank_init", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),
+    ("rt_gpu_render_rank_async", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
+    ("rt_gpu_rank_finish", ctypes.c_int, []),
+    ("rt_gpu_rank_shutdown", ctypes.c_int, []),
     ("rt_gpu_device_count", ctypes.c_int, []),
     ("rt_gpu_gamma_u8", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     ("rt_gpu_row_bases", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -16,10 +16,12 @@ Backends: GpuRows (lib580rt.so through the C ABI, device tensors) and, for the
 CPU tests of this logic with gloo, OracleRows in tests/.
 
 render_frame() is the plain one-frame form. DistFrame is the steady-state form
-used by bench.py: persistent buffers, all_gather_into_tensor, the row-base scan
-as one kernel (rt_gpu_row_bases), and a double-buffered asynchronous gather of
-frame N that overlaps frame N+1's kernels (rank 0 de-interleaves frame N after
-frame N+1 is queued; finish() completes the last one).
+over torch.distributed (any backend, the gloo CPU tests included): persistent
+buffers, all_gather_into_tensor, the row-base scan as one kernel
+(rt_gpu_row_bases), and a double-buffered asynchronous gather of frame N that
+overlaps frame N+1's kernels. NativeRankFrame is bench.py's multi-rank step over
+RCCL: the same exchange run by the library itself (rt_gpu_render_rank_async),
+with the communicator and the frame loop native.
 """
 import ctypes
 
@@ -235,95 +237,79 @@ class DistFrame:
         return self.last_host
 
     def close(self):
-        """Unregister rank 0's host buffers (after finish())."""
+        """Complete what is in flight, then unregister rank 0's host buffers."""
+        if self.pending is not None or any(w is not None for w in self.work):
+            self.finish()
         for _, buf in self._reg:
             self.lib.rt_gpu_host_unregister(buf.ctypes.data)
         self._reg = []
 
 
-class PipelinedDistFrame:
-    """DistFrame's u8 steady state with each frame's AO phase left running (the
-    GPU backend over RCCL; bench.py's multi-rank step). In DistFrame the compute
-    stream waits for frame N's AO phase before frame N+1's count exchange, so
-    consecutive AO phases cannot overlap; here rt_gpu_shade_rows_ppm puts that
-    wait on an exchange stream instead: the tiles' gather (on a process group of
-    its own -- a second communicator, whose collectives never queue behind the
-    next frame's count exchange) and rank 0's write of the PPM body into
-    registered host memory (rt_gpu_deinterleave_ppm) run there, while the
-    compute stream goes on with the next frame. A ring of R buffer sets; a set
-    is reused once its frame's gather (and write) is done. The library's stream
-    must be torch's current stream (rt_gpu_set_stream)."""
+class NativeRankFrame:
+    """The steady-state multi-rank frame driven by the library (bench.py's
+    multi-rank step; rt_gpu_rank_* in include/rt580.h): the library owns the
+    world's RCCL communicator (ncclCommInitRank from an id rank 0 makes and
+    this class broadcasts over `dist`) and runs the rank's frame loop itself --
+    count, all-gather, shading, the PPM bytes of its rows, the gather to rank 0
+    and rank 0's write of the PPM body into registered host memory -- every
+    collective on one library stream in the same order on every rank, a frame's
+    gather queued by the next frame's call so that two frames' AO phases overlap.
+    No per-frame Python, torch or event work beyond one ctypes call. Rank 0 keeps
+    a ring of R page-locked host frames (frame k lands in buffer k mod R)."""
 
     R = 3
+    ID_BYTES = 128  # NCCL_UNIQUE_ID_BYTES
 
-    def __init__(self, backend, dist, torch, height, width, rank, world, device):
+    def __init__(self, rt580, params, dist, torch, height, width, rank, world, device):
         import numpy as np
-        self.b, self.dist, self.t = backend, dist, torch
-        self.lib, self.rt580 = backend.lib, backend.rt580
-        self.h, self.w, self.rank, self.world, self.device = height, width, rank, world, device
-        self.n_max = n_max_rows(height, world)
-        tile = self.n_max * width * 3
-        R = self.R
-        self.cnt = [torch.zeros(self.n_max, dtype=torch.int32, device=device) for _ in range(R)]
-        self.gathered = [torch.empty(world * self.n_max, dtype=torch.int32, device=device) for _ in range(R)]
-        self.base = [torch.empty(self.n_max, dtype=torch.int64, device=device) for _ in range(R)]
-        self.fb8 = [torch.empty(tile, dtype=torch.uint8, device=device) for _ in range(R)]
-        self.tiles = [torch.empty(world * tile, dtype=torch.uint8, device=device) for _ in range(R)] \
-            if rank == 0 else None
-        self.x = torch.cuda.Stream(device)
-        self.pg = dist.new_group(list(range(world)))
-        self.done = [None] * R  # event on the exchange stream: set k free again
+        self.rt580, self.lib, self.t = rt580, rt580.load(), torch
+        self.params = rt580.RenderParams.from_buffer_copy(params)
+        self.h, self.w, self.rank, self.world = height, width, rank, world
+        uid = torch.zeros(self.ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            rt580.check(self.lib.rt_gpu_rank_unique_id(uid.data_ptr(), self.ID_BYTES), "rt_gpu_rank_unique_id")
+        on_dev = dist.get_backend() != "gloo"
+        u = uid.to(device) if on_dev else uid
+        dist.broadcast(u, src=0)
+        uid = u.cpu() if on_dev else u
+        rt580.check(self.lib.rt_gpu_rank_init(uid.data_ptr(), self.ID_BYTES, world, rank), "rt_gpu_rank_init")
         self._reg = []
         if rank == 0:
             span = (height * width * 3 + 4095) // 4096 * 4096
-            for _ in range(R):
+            for _ in range(self.R):
                 raw = np.zeros(span + 4096, dtype=np.uint8)
                 off = (-raw.ctypes.data) % 4096
                 buf = raw[off:off + span]
-                self.rt580.check(self.lib.rt_gpu_host_register(buf.ctypes.data, span), "rt_gpu_host_register")
+                rt580.check(self.lib.rt_gpu_host_register(buf.ctypes.data, span), "rt_gpu_host_register")
                 self._reg.append((raw, buf))
         self.i = 0
-        self.last_host = None
+        self.last = None
 
     def render(self):
-        t, k = self.t, self.i
-        ctypes_ = ctypes
-        cur = t.cuda.current_stream(self.device)
-        if self.done[k] is not None:  # set k's previous frame: gathered (and written) before its buffers are reused
-            cur.wait_event(self.done[k])
-        pc = self.b._p(self.rank, self.world)
-        self.rt580.check(self.lib.rt_gpu_count_rows(ctypes_.byref(pc), self.cnt[k].data_ptr()), "rt_gpu_count_rows")
-        self.dist.all_gather_into_tensor(self.gathered[k], self.cnt[k])
-        self.b.row_bases(self.gathered[k], self.rank, self.world, self.base[k])
-        self.rt580.check(self.lib.rt_gpu_shade_rows_ppm(ctypes_.byref(pc), self.base[k].data_ptr(),
-                                                        self.fb8[k].data_ptr(), ctypes_.c_void_p(self.x.cuda_stream)),
-                         "rt_gpu_shade_rows_ppm")
-        with t.cuda.stream(self.x):
-            if self.rank == 0:
-                work = self.dist.gather(self.fb8[k], gather_list=list(self.tiles[k].chunk(self.world)), dst=0,
-                                        group=self.pg, async_op=True)
-                work.wait()  # the exchange stream waits for the gather
-                buf = self._reg[k][1]
-                self.rt580.check(self.lib.rt_gpu_deinterleave_ppm(
-                    self.tiles[k].data_ptr(), self.world, self.n_max, self.w, self.h, buf.ctypes.data,
-                    ctypes_.c_void_p(self.x.cuda_stream)), "rt_gpu_deinterleave_ppm")
-                self.last_host = t.from_numpy(buf[:self.h * self.w * 3]).view(self.h, self.w, 3)
-            else:
-                work = self.dist.gather(self.fb8[k], dst=0, group=self.pg, async_op=True)
-                work.wait()
-            ev = t.cuda.Event()
-            ev.record(self.x)
-            self.done[k] = ev
-        self.i = (k + 1) % self.R
+        host = self._reg[self.i][1].ctypes.data if self.rank == 0 else None
+        self.rt580.check(self.lib.rt_gpu_render_rank_async(ctypes.byref(self.params), host),
+                         "rt_gpu_render_rank_async")
+        self.last = self.i
+        self.i = (self.i + 1) % self.R
+
+    def frame(self, k):
+        """Rank 0: host buffer k of the ring as an (H, W, 3) uint8 array (after finish())."""
+        return self._reg[k][1][:self.h * self.w * 3].reshape(self.h, self.w, 3)
 
     def finish(self):
         """Complete every frame in flight; rank 0: the last frame's PPM body
         (H, W, 3) uint8 in page-locked host memory."""
+        self.rt580.check(self.lib.rt_gpu_rank_finish(), "rt_gpu_rank_finish")
         self.rt580.check(self.lib.rt_gpu_synchronize(), "rt_gpu_synchronize")
-        self.t.cuda.synchronize(self.device)
-        return self.last_host if self.rank == 0 else None
+        if self.rank != 0 or self.last is None:
+            return None
+        return self.t.from_numpy(self.frame(self.last))
 
     def close(self):
+        """The communicator and rank 0's host buffers (every frame complete first)."""
+        self.lib.rt_gpu_rank_finish()
+        self.lib.rt_gpu_synchronize()
+        self.lib.rt_gpu_rank_shutdown()
         for _, buf in self._reg:
             self.lib.rt_gpu_host_unregister(buf.ctypes.data)
         self._reg = []

@@ -25,9 +25,10 @@ Parallel modes (the row split of SURVEY §8e, byte-identical frames for every N)
     overlap the next frame's kernels). N above the visible devices is an
     error; --rehearse runs the same split on device 0 N times (device copies
     instead of RCCL) to rehearse it on a one-GPU box.
-  * under torch.distributed.run: one process per GPU (rt580_dist.DistFrame:
-    RCCL all-gather of the counts, async gather of the u8 tiles to rank 0).
-    --gpus must equal WORLD_SIZE.
+  * under torch.distributed.run: one process per GPU (rt580_dist.NativeRankFrame:
+    the library's rank loop, rt_gpu_render_rank_async -- RCCL all-gather of the
+    counts, the u8 tiles gathered to rank 0, frames in flight; --backend gloo:
+    rt580_dist.DistFrame over torch.distributed). --gpus must equal WORLD_SIZE.
 
 Rank 0 prints ONE JSON line on stdout: metric, value = whole-job Mrays/s,
 ms_per_step, roofline of the AO ray kernel, cpu_baseline (N = 1), the frame
@@ -184,7 +185,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     if ctx.dist_on:
         backend = dist_mod.GpuRows(rt580, params, torch, ctx.device)
         if ctx.args.backend == "nccl":
-            dframe = dist_mod.PipelinedDistFrame(backend, ctx.dist, torch, H, W, ctx.rank, ctx.world, ctx.device)
+            dframe = dist_mod.NativeRankFrame(rt580, params, ctx.dist, torch, H, W, ctx.rank, ctx.world, ctx.device)
     import numpy as np
     if ctx.multi:
         devs = (ctypes.c_int * ctx.multi)(*ctx.devices)
@@ -350,8 +351,8 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
                  % ("rt_gpu_render_multi_async (tiles mapped to bytes on their devices, gathered and de-interleaved "
                     "on device 0)" if ctx.multi else "rt_gpu_render_async_ppm", RING) if not ctx.dist_on else
                  "one frame on every rank; rank 0 gathers the u8 tiles and writes the PPM body into page-locked host "
-                 "memory (rt580_dist.PipelinedDistFrame: each frame's gather and write on an exchange stream, the "
-                 "next frame's count exchange and AO phase going ahead)"),
+                 "memory (rt580_dist.NativeRankFrame: the library's own rank loop, rt_gpu_render_rank_async -- "
+                 "count, RCCL all-gather, shading, the previous frame's gather, on one communicator)"),
         "step_kind": step_kind,
         "scene_upload_s": round(upload_s, 3),
         "host_enqueue_ms_per_step": round(host_s / steps * 1e3, 4),

@@ -241,6 +241,28 @@ int rt_gpu_deinterleave_ppm(const uint8_t* tiles, int world, int n_max, int widt
  * wait for it. NULL done_stream: the caller's stream waits, as rt_gpu_shade_rows. */
 int rt_gpu_shade_rows_ppm(const rt_render_params* params, const uint64_t* row_base_device, uint8_t* tile_u8_device,
                           void* done_stream);
+/* One process per GPU, driven by the library (the reference's row
+ * loop, Raytracer.cpp:921-932, split by interleaved rows over `world` ranks).
+ * rt_gpu_rank_unique_id: rank 0 makes the communicator's id (id_bytes >= 128,
+ * ncclGetUniqueId), which the launcher hands to every rank (e.g. a
+ * torch.distributed broadcast); rt_gpu_rank_init then joins this process's
+ * device (rt_gpu_init's) to the world's RCCL communicator (ncclCommInitRank),
+ * owned by the library. rt_gpu_render_rank_async queues one whole frame
+ * (params: row_begin 0, row_step 1, row_end height) on every rank: this rank's
+ * rows (rank, rank + world, ...), the count all-gather, the shading and the PPM
+ * bytes of its rows, and the previous frame's gather of the u8 row tiles to
+ * rank 0, which writes that frame's PPM body into its ppm_body_host (a
+ * registered range of height x width x 3 bytes; other ranks pass NULL), in call
+ * order. Every collective of the rank runs on one library stream, in the same
+ * order on every rank; a frame's gather is queued by the next call (or
+ * rt_gpu_rank_finish), so two frames' shading overlap. Every rank makes the same
+ * sequence of calls. Complete after rt_gpu_rank_finish + rt_gpu_synchronize.
+ * rt_gpu_rank_shutdown destroys the communicator (rt_gpu_shutdown does too). */
+int rt_gpu_rank_unique_id(void* id_out, uint64_t id_bytes);
+int rt_gpu_rank_init(const void* id, uint64_t id_bytes, int world, int rank);
+int rt_gpu_render_rank_async(const rt_render_params* params, uint8_t* ppm_body_host);
+int rt_gpu_rank_finish(void);
+int rt_gpu_rank_shutdown(void);
 /* Visible HIP devices (0 without a GPU). */
 int rt_gpu_device_count(void);
 /* FlushFrameBufferToPPM's pixel mapping on the device (Raytracer.cpp:812-818):

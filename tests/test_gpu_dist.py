@@ -1,5 +1,6 @@
-"""bench.py's multi-rank path on the real device over RCCL, with one rank
-(the GPU box has one MI355X): DistFrame = rt_gpu_count_rows, RCCL
+"""The multi-rank paths on the real device over RCCL, with one rank (SURVEY
+§8e; the GPU box has one MI355X): NativeRankFrame (bench.py's step: the
+library's own rank loop) and DistFrame = rt_gpu_count_rows, RCCL
 all_gather_into_tensor of the per-row AO counts, the row-base kernel,
 rt_gpu_shade_rows, u8 gamma on the device, an asynchronous RCCL gather of the
 row tiles, de-interleave. Frames are queued back to back, so consecutive frames
@@ -75,29 +76,62 @@ def test_dist_frame_rccl_one_rank_matches_reference(rccl_one_rank, u8):
     rt.close()
 
 
-def test_pipelined_dist_frame_rccl_one_rank_matches_reference(rccl_one_rank):
-    """PipelinedDistFrame (bench.py's multi-rank step): each frame's gather and
-    rank 0's host write on the exchange stream and a second communicator, the
-    next frame's count exchange and AO phase going ahead -- frames one at a
-    time, then six queued back to back (two turns of the buffer ring): the PPM
-    body equals the reference's 1080p render."""
+def test_native_rank_frame_rccl_one_rank_matches_reference(rccl_one_rank):
+    """NativeRankFrame (bench.py's multi-rank step): the library's own rank loop
+    (rt_gpu_rank_init from a broadcast RCCL id, rt_gpu_render_rank_async:
+    count, all-gather, shading, the previous frame's gather and rank 0's PPM
+    write, every collective on one library stream) -- frames one at a time, then
+    seven queued back to back (two turns of the buffer ring and one more): every
+    host buffer of the ring holds the reference's 1080p render."""
     torch, dist, device, rt580, lib = rccl_one_rank
     w, h = 1920, 1080
     want = next(e for e in helpers.golden_entries(False) if e["name"] == "config2_1080p_d4_ao64")["sha256"]
     rt, params = _setup(rt580, lib, w, h)
     dm = helpers.rt580_dist()
-    df = dm.PipelinedDistFrame(dm.GpuRows(rt580, params, torch, device), dist, torch, h, w, 0, 1, device)
+    df = dm.NativeRankFrame(rt580, params, dist, torch, h, w, 0, 1, device)
 
     def sha(frame):
-        return helpers.sha256(b"P6\n%d %d\n255\n" % (w, h) + frame.numpy().tobytes())
+        return helpers.sha256(b"P6\n%d %d\n255\n" % (w, h) + frame.tobytes())
 
     try:
         for _ in range(2):
             df.render()
-            assert sha(df.finish()) == want
+            assert sha(df.finish().numpy()) == want
+        for _ in range(7):
+            df.render()
+        df.finish()
+        for k in range(df.R):
+            assert sha(df.frame(k)) == want, "ring buffer %d" % k
+    finally:
+        df.close()
+    rt.close()
+
+
+def test_native_rank_frame_bvh_scene_matches_oracle(rccl_one_rank):
+    """The rank loop on a BVH scene (replayed count schedules, frames in
+    flight): the Cornell box at depth 3, AO 8, against the oracle."""
+    import numpy as np
+    torch, dist, device, rt580, lib = rccl_one_rank
+    w, h = 96, 54
+    root = helpers.synthetic_root("cornell10k")
+    rt = rt580.Raytracer(w, h, root)
+    assert rt.LoadSceneJSON("cornell10k.json") == 0
+    rt.set_depth(3)
+    rt.set_ao(8, True)
+    assert rt.InitializeRenderer() == 0
+    params = rt.render_params()
+    scene = rt.scene()
+    rt580.check(lib.rt_gpu_upload_scene(ctypes.byref(scene)), "rt_gpu_upload_scene")
+    ref, _ = helpers.oracle_render("cornell10k.json", w, h, 3, 8, True, root=root)
+    want = rt580.gamma_lut()[ref.astype(np.int64)].astype(np.uint8)
+    dm = helpers.rt580_dist()
+    df = dm.NativeRankFrame(rt580, params, dist, torch, h, w, 0, 1, device)
+    try:
         for _ in range(6):
             df.render()
-        assert sha(df.finish()) == want
+        df.finish()
+        for k in range(df.R):
+            assert np.array_equal(df.frame(k), want), "ring buffer %d" % k
     finally:
         df.close()
     rt.close()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Host cost of one frame call on a tiny frame (GPU work negligible): the
 plain single-GPU step (rt_gpu_render_async_ppm) vs the per-process
-multi-GPU step (rt580_dist.PipelinedDistFrame, one rank over RCCL). Prints
+multi-GPU step (rt580_dist.NativeRankFrame, one rank over RCCL). Prints
 one JSON line: microseconds of host time per frame for each (mean of N)."""
 import ctypes
 import json
@@ -58,7 +58,7 @@ def main():
     res["plain_us_per_frame_total"] = round((t2 - t0) / n * 1e6, 1)
     lib.rt_gpu_host_unregister(buf.ctypes.data)
     dm = helpers.rt580_dist()
-    df = dm.PipelinedDistFrame(dm.GpuRows(rt580, params, torch, dev), dist, torch, h, w, 0, 1, dev)
+    df = dm.NativeRankFrame(rt580, params, dist, torch, h, w, 0, 1, dev)
     for _ in range(20):
         df.render()
     df.finish()
