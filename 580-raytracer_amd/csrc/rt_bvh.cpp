@@ -521,14 +521,21 @@ namespace rt580 {
 // and inside the triangle's angle at v0 widened by ~zeta_j.
 // A direction d within chord rho of a cell centre c satisfies each condition
 // only if c does with rho|N| (resp. rho|E||N|) added to the bound; cell radii
-// come from the octahedral decode's Lipschitz bound (<= sqrt6 per map unit:
-// sqrt2 for the unnormalised vector, sqrt3 for normalising it, |v| >= 1/sqrt3)
-// times the cell's half diagonal, plus 1e-6 map units for the device's float
-// cell computation. A quadtree over the map lists every triangle in every cell
+// come from the octahedral decode's Lipschitz bound (<= 3 per map unit: sqrt3
+// for the unnormalised vector -- (a, b, 1 - |a| - |b|) moves by
+// sqrt(da^2 + db^2 + (da +- db)^2) <= sqrt3 |(da, db)|, the folded half alike --
+// and sqrt3 for normalising it, |v|_2 >= |v|_1 / sqrt3 = 1 / sqrt3) times the
+// cell's half diagonal, plus 1e-6 map units for the device's float cell
+// computation. (Rounds 2-5 used sqrt6, taking sqrt2 for the first factor: a
+// quadtree node whose centre was 2.6 half diagonals from a direction inside it
+// was pruned, and the north-star frame lost 34 far hits -- tools/pixel_tree_check.cpp,
+// DESIGN.md "Full-frame parity".) A quadtree over the map lists every triangle in every cell
 // its patch can reach; the device tests far_candidate + the full reference
 // test on the listed triangles only.
 
 namespace {
+
+constexpr double kOctLipschitz = 3.0 * (1.0 + 1e-9);  // chord per map unit (above), with the doubles' rounding
 
 void oct_decode(double a, double b, double out[3]) {
     double x = a, y = b;
@@ -591,6 +598,14 @@ bool grid_reach(const GridTri& g, const double c[3], double rho) {
 
 }  // namespace
 
+void oct_node_centre(int level, int i, int j, double out[3]) {
+    const double side = 2.0 / (double)(1 << level);
+    oct_decode(-1.0 + (i + 0.5) * side, -1.0 + (j + 0.5) * side, out);
+}
+
+// node radius (chord) of a map square of side 2/2^level, centre decoded
+double oct_node_radius(int level) { return kOctLipschitz * (std::sqrt(0.5) * 2.0 / (double)(1 << level) + 1e-6); }
+
 void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells) {
     const auto t0 = std::chrono::steady_clock::now();
     out.grid_log2 = 0;
@@ -609,8 +624,7 @@ void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells) {
         ok[k] = prims[ft.id].area > 0.0f && grid_tri(prims[ft.id], ft, R, S, gt[k]);
         if (!ok[k]) out.grid_always.push_back((uint32_t)k);
     }
-    // node radius (chord) of a map square of side 2/2^level, centre decoded
-    auto rho_of = [](int level) { return std::sqrt(6.0) * (std::sqrt(0.5) * 2.0 / (double)(1 << level) + 1e-6); };
+    auto rho_of = [](int level) { return oct_node_radius(level); };
     unsigned nt = std::thread::hardware_concurrency();
     if (nt < 1) nt = 1;
     if (nt > 16) nt = 16;
@@ -631,9 +645,8 @@ void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells) {
             while (!stk.empty()) {
                 const Node nd = stk.back();
                 stk.pop_back();
-                const double side = 2.0 / (double)(1 << nd.level);
                 double c[3];
-                oct_decode(-1.0 + (nd.i + 0.5) * side, -1.0 + (nd.j + 0.5) * side, c);
+                oct_node_centre(nd.level, nd.i, nd.j, c);
                 if (!grid_reach(g, c, rho_of(nd.level))) continue;
                 if (nd.level == L) {
                     const size_t cell = (size_t)nd.i * M + nd.j;

@@ -152,6 +152,12 @@ void collapse_bvh4(BvhBuild& out);
 // Build the far-search direction grid over out.far_tris (after build_bvh; the
 // query side is rt_isect.h grid_cell / far_any / far_closest).
 void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells);
+// The grid's geometry, for its checks (tests/native/octgrid_check.cpp): the unit
+// direction at the centre of quadtree node (i, j) of `level` (2^level nodes per
+// map axis), and the chord radius the build assumes every direction whose
+// cell lies in that node to be within.
+void oct_node_centre(int level, int i, int j, double out[3]);
+double oct_node_radius(int level);
 
 // out.grid2_* from out.grid_* (after build_dir_grid): coarse cell (i, j) lists
 // the sorted union of fine cells (2i + a, 2j + b). grid_cell(d, L - 1) is

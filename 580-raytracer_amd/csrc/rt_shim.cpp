@@ -2421,6 +2421,10 @@ struct RankLoop {
     int pend_r = 0;
     rt_render_params pend_p{};
     uint8_t* pend_host = nullptr;
+    // rt580_rank_rehearse: rank `rank` of `world` on one GPU, no communicator --
+    // the all-gather copies a precomputed gathered count vector, the gather
+    // moves nothing (rank 0 writes its own rows only); for timing one rank's share
+    const int32_t* rehearse_gathered = nullptr;
 } g_rank;
 
 int rank_teardown() {
@@ -2456,7 +2460,7 @@ int rank_gather_pending() {
     HIP_TRY(hipStreamWaitEvent(xs, g_rank.shaded[r], 0));
     if (g_rank.rank == 0) {
         HIP_TRY(hipMemcpyAsync(g_rank.root8[r].p, g_rank.t8[r].p, t8, hipMemcpyDeviceToDevice, xs));
-        if (n > 1) {
+        if (n > 1 && g_rank.comm) {
             RCCL_TRY(g_rccl.GroupStart());
             for (int k = 1; k < n; k++)
                 RCCL_TRY(g_rccl.Recv((char*)g_rank.root8[r].p + (size_t)k * t8, t8, ncclUint8, k, g_rank.comm, xs));
@@ -2474,7 +2478,7 @@ int rank_gather_pending() {
             HIP_TRY(hipMemcpyAsync(g_rank.pend_host, g.ppm_stage.p, body, hipMemcpyDeviceToHost, xs));
         }
         HIP_TRY(hipEventRecord(hr->copied, xs));
-    } else {
+    } else if (g_rank.comm) {
         RCCL_TRY(g_rccl.Send(g_rank.t8[r].p, t8, ncclUint8, 0, g_rank.comm, xs));
     }
     HIP_TRY(hipEventRecord(g_rank.done[r], xs));
@@ -2513,7 +2517,11 @@ int rank_frame(const rt_render_params* p, uint8_t* ppm_host) {
     // the exchange: every rank's per-row counts (H int32 in all)
     HIP_TRY(hipEventRecord(g_rank.counted[r], g.stream));
     HIP_TRY(hipStreamWaitEvent(g_rank.xs, g_rank.counted[r], 0));
-    RCCL_TRY(g_rccl.AllGather(g_rank.rc[r].p, g_rank.gat[r].p, (size_t)n_max, ncclInt32, g_rank.comm, g_rank.xs));
+    if (g_rank.comm)
+        RCCL_TRY(g_rccl.AllGather(g_rank.rc[r].p, g_rank.gat[r].p, (size_t)n_max, ncclInt32, g_rank.comm, g_rank.xs));
+    else  // rehearsal: the world's counts as precomputed, this rank's own rows included
+        HIP_TRY(hipMemcpyAsync(g_rank.gat[r].p, g_rank.rehearse_gathered, (size_t)n * n_max * 4,
+                               hipMemcpyDeviceToDevice, g_rank.xs));
     HIP_TRY(hipEventRecord(g_rank.gathered[r], g_rank.xs));
     HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.gathered[r], 0));
     // phase 2: RNG bases of this rank's rows, shading, the rows' PPM bytes
@@ -2594,6 +2602,27 @@ extern "C" int rt_gpu_rank_init(const void* id, uint64_t id_bytes, int world, in
     g_rank.rank = rank;
     g_rank.device = g.device;
     g_rank.ring = 0;
+    g_rank.rehearse_gathered = nullptr;
+    g_rank.on = true;
+    return RT_SUCCESS;
+}
+
+extern "C" int rt580_rank_rehearse(int world, int rank, const int32_t* gathered_device) {
+    RT_WORK("rt580_rank_rehearse");
+    if (g_cur != 0) return fail("re-entered");
+    if (world < 1 || rank < 0 || rank >= world || !gathered_device) return fail("rt580_rank_rehearse: bad arguments");
+    if (!g.inited) return fail("rt_gpu_init not called");
+    if (g_rank.on && rank_teardown()) return fail("rt580_rank_rehearse: the previous communicator's work failed");
+    HIP_TRY(hipSetDevice(g.device));
+    HIP_TRY(hipStreamCreateWithFlags(&g_rank.xs, hipStreamNonBlocking));
+    for (int r = 0; r < RankLoop::kRing; r++)
+        for (hipEvent_t* e : {&g_rank.counted[r], &g_rank.gathered[r], &g_rank.shaded[r], &g_rank.done[r]})
+            HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    g_rank.world = world;
+    g_rank.rank = rank;
+    g_rank.device = g.device;
+    g_rank.ring = 0;
+    g_rank.rehearse_gathered = gathered_device;
     g_rank.on = true;
     return RT_SUCCESS;
 }

@@ -84,6 +84,7 @@ SIGNATURES = [
     ("rt_gpu_render_rank_async", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
     ("rt_gpu_rank_finish", ctypes.c_int, []),
     ("rt_gpu_rank_shutdown", ctypes.c_int, []),
+    ("rt580_rank_rehearse", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("rt_gpu_device_count", ctypes.c_int, []),
     ("rt_gpu_gamma_u8", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     ("rt_gpu_row_bases", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

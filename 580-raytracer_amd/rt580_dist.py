@@ -260,19 +260,26 @@ class NativeRankFrame:
     R = 3
     ID_BYTES = 128  # NCCL_UNIQUE_ID_BYTES
 
-    def __init__(self, rt580, params, dist, torch, height, width, rank, world, device):
+    def __init__(self, rt580, params, dist, torch, height, width, rank, world, device, rehearse_gathered=None):
+        """rehearse_gathered (dist None): rank `rank` of `world` on this one GPU
+        without a communicator, the world's per-row counts given (int32 device
+        tensor [world * n_max]; rt580_rank_rehearse) -- one rank's share timed."""
         import numpy as np
         self.rt580, self.lib, self.t = rt580, rt580.load(), torch
         self.params = rt580.RenderParams.from_buffer_copy(params)
         self.h, self.w, self.rank, self.world = height, width, rank, world
-        uid = torch.zeros(self.ID_BYTES, dtype=torch.uint8)
-        if rank == 0:
-            rt580.check(self.lib.rt_gpu_rank_unique_id(uid.data_ptr(), self.ID_BYTES), "rt_gpu_rank_unique_id")
-        on_dev = dist.get_backend() != "gloo"
-        u = uid.to(device) if on_dev else uid
-        dist.broadcast(u, src=0)
-        uid = u.cpu() if on_dev else u
-        rt580.check(self.lib.rt_gpu_rank_init(uid.data_ptr(), self.ID_BYTES, world, rank), "rt_gpu_rank_init")
+        if rehearse_gathered is not None:
+            self._gathered = rehearse_gathered
+            rt580.check(self.lib.rt580_rank_rehearse(world, rank, rehearse_gathered.data_ptr()), "rt580_rank_rehearse")
+        else:
+            uid = torch.zeros(self.ID_BYTES, dtype=torch.uint8)
+            if rank == 0:
+                rt580.check(self.lib.rt_gpu_rank_unique_id(uid.data_ptr(), self.ID_BYTES), "rt_gpu_rank_unique_id")
+            on_dev = dist.get_backend() != "gloo"
+            u = uid.to(device) if on_dev else uid
+            dist.broadcast(u, src=0)
+            uid = u.cpu() if on_dev else u
+            rt580.check(self.lib.rt_gpu_rank_init(uid.data_ptr(), self.ID_BYTES, world, rank), "rt_gpu_rank_init")
         self._reg = []
         if rank == 0:
             span = (height * width * 3 + 4095) // 4096 * 4096

@@ -205,11 +205,7 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
     step_i = [0]
 
     def step():
-        if K > 1:
-            rows.count(R, K)
-            rows.shade(R, K, sample_base)
-            return None
-        if ctx.dist_on:
+        if K > 1 or ctx.dist_on:
             if dframe is not None:
                 dframe.render()
                 return None
@@ -234,17 +230,23 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
         return dframe.finish() if dframe is not None else None
 
     # rank r's exact share of a K-way interleaved split (--row-sample K
-    # --row-rank r, one GPU): RNG bases from a full-frame count, untimed
+    # --row-rank r, one GPU): the rank loop of the multi-rank step
+    # (rt_gpu_render_rank_async) rehearsed as rank r of K without a
+    # communicator -- the world's per-row counts from an untimed full-frame
+    # count pass, no gather traffic (rt580_rank_rehearse)
     K, R = ctx.row_sample, ctx.row_rank
-    sample_base = None
     if K > 1:
-        rows = helpers.rt580_dist().GpuRows(rt580, params, torch, ctx.device)
+        dm = helpers.rt580_dist()
+        rows = dm.GpuRows(rt580, params, torch, ctx.device)
         log("%s: row sample %d/%d: full-frame count pass" % (name, R, K))
-        cnt = rows.count(0, 1)[:H].to(torch.int64)
-        base = torch.cumsum(cnt, 0) - cnt
-        n_loc = helpers.rt580_dist().n_local_rows(H, R, K)
-        sample_base = torch.zeros(helpers.rt580_dist().n_max_rows(H, K), dtype=torch.int64, device=ctx.device)
-        sample_base[:n_loc] = base[R::K][:n_loc]
+        cnt = rows.count(0, 1)[:H]
+        torch.cuda.synchronize()
+        n_max = dm.n_max_rows(H, K)
+        gathered = torch.zeros(K * n_max, dtype=torch.int32, device=ctx.device)
+        for k in range(K):
+            part = cnt[k::K]
+            gathered[k * n_max:k * n_max + part.numel()] = part
+        dframe = dm.NativeRankFrame(rt580, params, None, torch, H, W, R, K, ctx.device, rehearse_gathered=gathered)
 
     # a split frame (N > 1 in this process): the frame's rays, and the frame to
     # compare with, from one untimed single-device render (rt_gpu_last_stats

@@ -263,6 +263,11 @@ int rt_gpu_rank_init(const void* id, uint64_t id_bytes, int world, int rank);
 int rt_gpu_render_rank_async(const rt_render_params* params, uint8_t* ppm_body_host);
 int rt_gpu_rank_finish(void);
 int rt_gpu_rank_shutdown(void);
+/* Bench/test hook: rank `rank` of `world` rehearsed on this one GPU without a
+ * communicator (the world's per-row counts precomputed in gathered_device,
+ * int32[world][n_max]; the gather moves nothing, rank 0 writes its own rows):
+ * rt_gpu_render_rank_async then times exactly one rank's share of the loop. */
+int rt580_rank_rehearse(int world, int rank, const int32_t* gathered_device);
 /* Visible HIP devices (0 without a GPU). */
 int rt_gpu_device_count(void);
 /* FlushFrameBufferToPPM's pixel mapping on the device (Raytracer.cpp:812-818):

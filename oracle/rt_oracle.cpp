@@ -1224,6 +1224,21 @@ extern "C" int oracle_count_rows(const char* root, const char* scene, int w, int
     return 0;
 }
 
+// AO calls of the pixels (x0 + k, y), k < n -> out[k] (parity hunts: which
+// pixel of a row holds a differing count).
+extern "C" int oracle_count_pixels(const char* root, const char* scene, int w, int h, int depth, int ao_n, int ao_on,
+                                   int y, int x0, int n, uint32_t* out) {
+    Loaded L;
+    int st = load_all(L, root, scene, w, h, depth, ao_n, ao_on);
+    if (st) return st;
+    for (int k = 0; k < n; k++) {
+        Counters c;
+        L.tr.raycast(generate_ray(L.cam, x0 + k, y), depth, nullptr, c, true);
+        out[k] = (uint32_t)c.ao_calls;
+    }
+    return 0;
+}
+
 // Shade the same rows given each row's absolute first AO-call index (minstd_rand0).
 extern "C" int oracle_shade_rows(const char* root, const char* scene, int w, int h, int depth, int ao_n,
                                  int ao_on, int row_begin, int row_step, int n_rows, const uint64_t* row_base,

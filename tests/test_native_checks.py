@@ -102,6 +102,18 @@ def test_bvh_queries_equal_brute_force(scene, rays, far):
         assert "differ_without_far_search=0 " not in out, out
 
 
+def test_direction_grid_node_radius_covers_every_direction():
+    """rt_bvh.cpp build_dir_grid prunes a quadtree node when a triangle's far-hit
+    patch cannot come within the node's chord radius of its centre: every
+    direction whose device cell lies in the node must be within that radius, at
+    every level. The true bound is 3 half diagonals (observed 2.98); rounds 2-5
+    assumed sqrt6 = 2.45 and the north-star frame lost 34 far hits."""
+    exe = _build("octgrid_check", [os.path.join(CSRC, "rt_bvh.cpp"), os.path.join(CSRC, "rt_scene.cpp")])
+    out = _run(exe, "2000000")
+    worst = float(out.split("worst_chord_per_half_diagonal=")[1].split()[0])
+    assert worst > 2.9, out  # the sampling reaches the bound's tight region
+
+
 def test_mt19937_block_jump_ahead_equals_the_engine():
     """rt_mt.h: the window W_J reached by the polynomial jump (x^(J-1) mod phi,
     phi from Berlekamp-Massey) yields std::mt19937's draws J, J+1, ... after
