@@ -74,6 +74,8 @@ CPU_BUDGET_S = 15.0  # one core, per workload (the all-cores leg renders the sam
 # pixel grows with triangles, depth and AO samples)
 CHECK_PIXELS = {"config2": 10240, "cornell10k": 10240, "field100k_1080p": 10240, "field100k": 4096, "field1m": 256}
 CHECK_SEGMENTS = 16
+# workloads whose whole frame the oracle rendered once (tests/golden/make_fullframe.py)
+FULLFRAME_KEYS = {"field100k_1080p": "north_star", "cornell10k": "config3"}
 
 
 def env_int(k, d):
@@ -452,6 +454,14 @@ def frame_check(ctx, name, frame_np, single, W, H, check):
         want = next(e for e in helpers.golden_entries(False) if e["name"] == "config2_1080p_d4_ao64")["sha256"]
         res["reference_sha256"] = want
         res["matches_reference"] = res["sha256"] == want
+    # the whole frame against the oracle's full render (tests/golden/fullframe.json)
+    ff = os.path.join(REPO, "tests", "golden", "fullframe.json")
+    key = FULLFRAME_KEYS.get(name)
+    if check and key and os.path.exists(ff):
+        want = json.load(open(ff)).get(key, {}).get("sha256")
+        if want:
+            res["oracle_full_frame_sha256"] = want
+            res["matches_oracle_full_frame"] = res["sha256"] == want
     if single is not None and (ctx.multi or ctx.dist_on):
         ref = rt580.gamma_lut()[single.astype(np.int64)] if frame_np.dtype == np.uint8 else single
         res["matches_single_gpu"] = bool(np.array_equal(frame_np.reshape(-1), ref.reshape(-1)))
@@ -670,8 +680,8 @@ def compact(rec):
     fc, rf, cb = rec.get("frame_check", {}), rec.get("roofline", {}), rec.get("cpu_baseline") or {}
     return {"value": rec["value"], "unit": rec["unit"], "ms_per_step": rec["ms_per_step"], "steps": rec["steps"],
             "rays_per_frame": rec["config"]["rays_per_frame"], "workload": rec["config"]["workload"],
-            "frame_check": {k: fc[k] for k in ("matches_reference", "matches_oracle_rows", "pixels_checked",
-                                               "matches_single_gpu") if k in fc},
+            "frame_check": {k: fc[k] for k in ("matches_reference", "matches_oracle_full_frame", "matches_oracle_rows",
+                                               "pixels_checked", "matches_single_gpu") if k in fc},
             "roofline": {k: rf.get(k) for k in ("kernel", "frac", "achieved", "launch_ms", "live_frac",
                                                 "isolated_over_rocprof", "profile")},
             "render_call_ms": rec.get("render_call_ms"),

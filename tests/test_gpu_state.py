@@ -484,5 +484,6 @@ def test_ao_audit_of_the_product_trace_and_late_passes(tmp_path):
     v = res["verify"]
     assert v["ok"] and v["entries_unexplained"] == 0 and v["rays_checked"] > 2e8, v
     assert res["frames_agree"] and not res["replay_errors"], res
-    # the frame the bench's oracle frame check pins (profiles/r04/bench_final.json north_star)
-    assert res["hashes"][0] == "42f02c04df52fe3694345c940b4fe94bbfeefec47a04617c7c82508d4d06c24f", res["hashes"]
+    # the oracle's render of the whole frame (tests/golden/fullframe.json, make_fullframe.py)
+    want = json.load(open(os.path.join(helpers.REPO, "tests", "golden", "fullframe.json")))["north_star"]["sha256"]
+    assert res["hashes"][0] == want, res["hashes"]

@@ -32,7 +32,12 @@ for f in sys.argv[1:]:
     if ns:
         nfc = ns.get("frame_check", {})
         out += ["| ns", ns.get("value"), ns.get("ms_per_step"), "frac=%s" % ns.get("roofline", {}).get("frac"),
-                "rows_ok=%s px=%s" % (nfc.get("matches_oracle_rows"), nfc.get("pixels_checked"))]
+                "rows_ok=%s px=%s full=%s" % (nfc.get("matches_oracle_rows"), nfc.get("pixels_checked"),
+                                              nfc.get("matches_oracle_full_frame"))]
+    c3 = d.get("config3")
+    if c3:
+        out += ["| c3", c3.get("value"), c3.get("ms_per_step"),
+                "full=%s" % c3.get("frame_check", {}).get("matches_oracle_full_frame")]
     print(*out)
 PY
 }
