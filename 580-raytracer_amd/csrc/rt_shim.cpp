@@ -2401,21 +2401,27 @@ int multi_frame_async(const rt_render_params* p, uint8_t* ppm_host, int n, const
 // communicator sees one sequence per rank, the same on all ranks, so no two
 // collectives can wait on each other across ranks. A frame's gather is
 // enqueued by the NEXT frame call, after that frame's all-gather:
-//   xs: allgather(k) | wait shaded(k-1), gather(k-1), PPM(k-1) | allgather(k+1) | ...
+//   xs: allgather(k), bases(k) | wait shaded(k-1), gather(k-1) | allgather(k+1), bases(k+1) | ...
 // so frame k+1's shading waits only for frame k-1's (two frames' AO phases run
-// together, as frames do on one GPU), never for frame k's. Buffers come from a
-// ring of three sets; frame k+3 starts after frame k's gather (g.stream waits
-// its xs event), which is after every read of frame k's set.
+// together, as frames do on one GPU), never for frame k's. The frame's own
+// chain stays off the caller's stream: the slot stream traces and copies the
+// counts, xs exchanges them and scans the row bases, the slot stream shades.
+// Rank 0 writes each PPM body into host memory on a stream of its own (hs),
+// so the ~0.1 ms of the host link per 1080p frame never holds xs. Buffers come
+// from a ring of three sets, one per frame slot; frame k+3 starts after frame
+// k's gather (the caller's stream, which the slot waits on, waits its xs
+// event) and receives into root8 after frame k's host write (xs waits hs).
 struct RankLoop {
     bool on = false;
     int world = 0, rank = 0, device = -1;
     ncclComm_t comm = nullptr;
-    hipStream_t xs = nullptr;
+    hipStream_t xs = nullptr, hs = nullptr;
     static constexpr int kRing = 3;
     int ring = 0;
     DevBuf rc[kRing], gat[kRing], base[kRing], t8[kRing], root8[kRing];
-    hipEvent_t counted[kRing] = {}, gathered[kRing] = {}, shaded[kRing] = {}, done[kRing] = {};
-    bool done_valid[kRing] = {};
+    hipEvent_t counted[kRing] = {}, gathered[kRing] = {}, shaded[kRing] = {}, done[kRing] = {}, recvd[kRing] = {},
+               written[kRing] = {};
+    bool done_valid[kRing] = {}, written_valid[kRing] = {};
     // the frame whose tiles are still to be gathered (enqueued by the next call)
     bool pending = false;
     int pend_r = 0;
@@ -2425,30 +2431,53 @@ struct RankLoop {
     // the all-gather copies a precomputed gathered count vector, the gather
     // moves nothing (rank 0 writes its own rows only); for timing one rank's share
     const int32_t* rehearse_gathered = nullptr;
+    std::vector<hipEvent_t*> events() {
+        std::vector<hipEvent_t*> v;
+        for (int r = 0; r < kRing; r++)
+            for (hipEvent_t* e : {&counted[r], &gathered[r], &shaded[r], &done[r], &recvd[r], &written[r]}) v.push_back(e);
+        return v;
+    }
 } g_rank;
 
 int rank_teardown() {
     int st = RT_SUCCESS;
-    if (g_rank.xs && hipStreamSynchronize(g_rank.xs) != hipSuccess) st = RT_FAILURE;
+    for (hipStream_t s : {g_rank.xs, g_rank.hs})
+        if (s && hipStreamSynchronize(s) != hipSuccess) st = RT_FAILURE;
     if (g_rank.comm) (void)g_rccl.CommDestroy(g_rank.comm);
     g_rank.comm = nullptr;
     for (int r = 0; r < RankLoop::kRing; r++) {
         for (DevBuf* b : {&g_rank.rc[r], &g_rank.gat[r], &g_rank.base[r], &g_rank.t8[r], &g_rank.root8[r]}) release(*b);
-        for (hipEvent_t* e : {&g_rank.counted[r], &g_rank.gathered[r], &g_rank.shaded[r], &g_rank.done[r]}) {
-            if (*e) (void)hipEventDestroy(*e);
-            *e = nullptr;
-        }
-        g_rank.done_valid[r] = false;
+        g_rank.done_valid[r] = g_rank.written_valid[r] = false;
     }
-    if (g_rank.xs) (void)hipStreamDestroy(g_rank.xs);
-    g_rank.xs = nullptr;
+    for (hipEvent_t* e : g_rank.events()) {
+        if (*e) (void)hipEventDestroy(*e);
+        *e = nullptr;
+    }
+    for (hipStream_t* s : {&g_rank.xs, &g_rank.hs}) {
+        if (*s) (void)hipStreamDestroy(*s);
+        *s = nullptr;
+    }
     g_rank.on = false;
     g_rank.pending = false;
+    g_rank.rehearse_gathered = nullptr;
     return st;
 }
 
-// The gather of the pending frame's u8 tiles to rank 0 and, on rank 0, its PPM
-// body into the host range; on xs, after that frame's shading.
+// The streams and events of a rank (rt_gpu_rank_init, rt580_rank_rehearse).
+int rank_open(int world, int rank) {
+    HIP_TRY(hipStreamCreateWithFlags(&g_rank.xs, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&g_rank.hs, hipStreamNonBlocking));
+    for (hipEvent_t* e : g_rank.events()) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    g_rank.world = world;
+    g_rank.rank = rank;
+    g_rank.device = g.device;
+    g_rank.ring = 0;
+    g_rank.on = true;
+    return RT_SUCCESS;
+}
+
+// The gather of the pending frame's u8 tiles to rank 0 (on xs, after that
+// frame's shading) and, on rank 0, its PPM body into the host range (on hs).
 int rank_gather_pending() {
     if (!g_rank.pending) return RT_SUCCESS;
     g_rank.pending = false;
@@ -2456,9 +2485,10 @@ int rank_gather_pending() {
     const int r = g_rank.pend_r, n = g_rank.world, H = p->height, W = p->width;
     const int n_max = (H + n - 1) / n;
     const size_t t8 = (size_t)n_max * W * 3, body = (size_t)H * W * 3;
-    hipStream_t xs = g_rank.xs;
+    hipStream_t xs = g_rank.xs, hs = g_rank.hs;
     HIP_TRY(hipStreamWaitEvent(xs, g_rank.shaded[r], 0));
     if (g_rank.rank == 0) {
+        if (g_rank.written_valid[r]) HIP_TRY(hipStreamWaitEvent(xs, g_rank.written[r], 0));  // root8[r] read out
         HIP_TRY(hipMemcpyAsync(g_rank.root8[r].p, g_rank.t8[r].p, t8, hipMemcpyDeviceToDevice, xs));
         if (n > 1 && g_rank.comm) {
             RCCL_TRY(g_rccl.GroupStart());
@@ -2466,18 +2496,22 @@ int rank_gather_pending() {
                 RCCL_TRY(g_rccl.Recv((char*)g_rank.root8[r].p + (size_t)k * t8, t8, ncclUint8, k, g_rank.comm, xs));
             RCCL_TRY(g_rccl.GroupEnd());
         }
+        HIP_TRY(hipEventRecord(g_rank.recvd[r], xs));
         HostRange* hr = host_range_ready(g_rank.pend_host, body);
         if (!hr) return fail("rt_gpu_render_rank_async: the buffer is not a registered range of %zu bytes", body);
-        HIP_TRY(hipStreamWaitEvent(xs, hr->copied, 0));
+        HIP_TRY(hipStreamWaitEvent(hs, g_rank.recvd[r], 0));
+        HIP_TRY(hipStreamWaitEvent(hs, hr->copied, 0));
         if (uint8_t* dst = (uint8_t*)mapped(hr, g_rank.pend_host)) {  // straight into the host range
-            HIP_TRY(launch_deinterleave_u8((const uint8_t*)g_rank.root8[r].p, n, n_max, W, H, dst, xs));
+            HIP_TRY(launch_deinterleave_u8((const uint8_t*)g_rank.root8[r].p, n, n_max, W, H, dst, hs));
         } else {
             if (ensure(g.ppm_stage, body)) return RT_FAILURE;
             HIP_TRY(launch_deinterleave_u8((const uint8_t*)g_rank.root8[r].p, n, n_max, W, H,
-                                           (uint8_t*)g.ppm_stage.p, xs));
-            HIP_TRY(hipMemcpyAsync(g_rank.pend_host, g.ppm_stage.p, body, hipMemcpyDeviceToHost, xs));
+                                           (uint8_t*)g.ppm_stage.p, hs));
+            HIP_TRY(hipMemcpyAsync(g_rank.pend_host, g.ppm_stage.p, body, hipMemcpyDeviceToHost, hs));
         }
-        HIP_TRY(hipEventRecord(hr->copied, xs));
+        HIP_TRY(hipEventRecord(hr->copied, hs));
+        HIP_TRY(hipEventRecord(g_rank.written[r], hs));
+        g_rank.written_valid[r] = true;
     } else if (g_rank.comm) {
         RCCL_TRY(g_rccl.Send(g_rank.t8[r].p, t8, ncclUint8, 0, g_rank.comm, xs));
     }
@@ -2500,7 +2534,8 @@ int rank_frame(const rt_render_params* p, uint8_t* ppm_host) {
     HIP_TRY(hipSetDevice(g.device));
     const int r = g_rank.ring;
     g_rank.ring = (r + 1) % RankLoop::kRing;
-    // the ring set's last frame has been gathered (every read of the set is before that)
+    // the ring set's last frame has been gathered (every read of the set is
+    // before that); the caller's stream waits, and the slot begins after it
     if (g_rank.pending && g_rank.pend_r == r && rank_gather_pending()) return RT_FAILURE;
     if (g_rank.done_valid[r]) HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.done[r], 0));
     if (ensure(g_rank.rc[r], (size_t)n_max * 4) || ensure(g_rank.gat[r], (size_t)n * n_max * 4) ||
@@ -2511,30 +2546,39 @@ int rank_frame(const rt_render_params* p, uint8_t* ppm_host) {
     pk.row_begin = rank;
     pk.row_step = n;
     pk.row_end = H;
-    // phase 1: this rank's rows traced, their AO calls counted (padding rows count 0)
-    HIP_TRY(hipMemsetAsync(g_rank.rc[r].p, 0, (size_t)n_max * 4, g.stream));
-    if (rt_gpu_count_rows(&pk, (uint32_t*)g_rank.rc[r].p)) return RT_FAILURE;
-    // the exchange: every rank's per-row counts (H int32 in all)
-    HIP_TRY(hipEventRecord(g_rank.counted[r], g.stream));
+    const int n_rows = n_selected_rows(&pk);
+    // phase 1 on the frame's slot: this rank's rows traced, their AO calls
+    // counted (rt_gpu_count_rows' steps, the counts copied on the slot stream)
+    if (begin_slot(false, g.nslots)) return RT_FAILURE;
+    for (int attempt = 0; attempt < 4; attempt++) {
+        if (begin_frame()) return RT_FAILURE;
+        HIP_TRY(hipEventRecord(g.ev[EV_START], fs()));
+        if (trace_rows(&pk, pk.row_begin, pk.row_step, n_rows)) return RT_FAILURE;
+        bool retry = false;
+        if (check_capacity(&pk, retry)) return RT_FAILURE;
+        if (!retry) break;
+        if (attempt == 3) return fail("node capacity could not be sized");
+        if (g.profiling) g.prof_frames--;
+    }
+    HIP_TRY(hipMemsetAsync(g_rank.rc[r].p, 0, (size_t)n_max * 4, fs()));  // padding rows count 0
+    if (n_rows)
+        HIP_TRY(hipMemcpyAsync(g_rank.rc[r].p, SL.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToDevice, fs()));
+    // the exchange and the row bases on xs: every rank's per-row counts (H int32 in all)
+    HIP_TRY(hipEventRecord(g_rank.counted[r], fs()));
     HIP_TRY(hipStreamWaitEvent(g_rank.xs, g_rank.counted[r], 0));
     if (g_rank.comm)
         RCCL_TRY(g_rccl.AllGather(g_rank.rc[r].p, g_rank.gat[r].p, (size_t)n_max, ncclInt32, g_rank.comm, g_rank.xs));
     else  // rehearsal: the world's counts as precomputed, this rank's own rows included
         HIP_TRY(hipMemcpyAsync(g_rank.gat[r].p, g_rank.rehearse_gathered, (size_t)n * n_max * 4,
                                hipMemcpyDeviceToDevice, g_rank.xs));
+    HIP_TRY(launch_row_bases((const int32_t*)g_rank.gat[r].p, n, n_max, H, rank, (uint64_t*)g_rank.base[r].p,
+                             g_rank.xs));
     HIP_TRY(hipEventRecord(g_rank.gathered[r], g_rank.xs));
-    HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.gathered[r], 0));
-    // phase 2: RNG bases of this rank's rows, shading, the rows' PPM bytes
-    if (rt_gpu_row_bases((const int32_t*)g_rank.gat[r].p, n, n_max, H, rank, (uint64_t*)g_rank.base[r].p))
-        return RT_FAILURE;
-    if (!g.split_ready || std::memcmp(&g.split_params, &pk, sizeof pk) != 0)
-        return fail("rt_gpu_render_rank_async: the count pass did not complete");
-    g.split_ready = false;
-    if (slot_wait_user()) return RT_FAILURE;  // the row bases were produced on the caller's stream
-    const size_t nv = (size_t)n_selected_rows(&pk) * W * 3;
+    HIP_TRY(hipStreamWaitEvent(fs(), g_rank.gathered[r], 0));
+    // phase 2 on the slot: shading with those RNG bases, the rows' PPM bytes
+    const size_t nv = (size_t)n_rows * W * 3;
     if (ensure(SL.fb, nv * 2)) return RT_FAILURE;  // the slot's own int16 rows
-    if (shade_rows(&pk, pk.row_begin, pk.row_step, n_selected_rows(&pk), (const uint64_t*)g_rank.base[r].p,
-                   (int16_t*)SL.fb.p))
+    if (shade_rows(&pk, pk.row_begin, pk.row_step, n_rows, (const uint64_t*)g_rank.base[r].p, (int16_t*)SL.fb.p))
         return RT_FAILURE;
     HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, nv, (uint8_t*)g_rank.t8[r].p, fs()));
     // the slot's end without the caller's stream waiting for it: the gather (on
@@ -2594,17 +2638,7 @@ extern "C" int rt_gpu_rank_init(const void* id, uint64_t id_bytes, int world, in
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof uid);
     RCCL_TRY(g_rccl.CommInitRank(&g_rank.comm, world, uid, rank));
-    HIP_TRY(hipStreamCreateWithFlags(&g_rank.xs, hipStreamNonBlocking));
-    for (int r = 0; r < RankLoop::kRing; r++)
-        for (hipEvent_t* e : {&g_rank.counted[r], &g_rank.gathered[r], &g_rank.shaded[r], &g_rank.done[r]})
-            HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    g_rank.world = world;
-    g_rank.rank = rank;
-    g_rank.device = g.device;
-    g_rank.ring = 0;
-    g_rank.rehearse_gathered = nullptr;
-    g_rank.on = true;
-    return RT_SUCCESS;
+    return rank_open(world, rank);
 }
 
 extern "C" int rt580_rank_rehearse(int world, int rank, const int32_t* gathered_device) {
@@ -2614,16 +2648,8 @@ extern "C" int rt580_rank_rehearse(int world, int rank, const int32_t* gathered_
     if (!g.inited) return fail("rt_gpu_init not called");
     if (g_rank.on && rank_teardown()) return fail("rt580_rank_rehearse: the previous communicator's work failed");
     HIP_TRY(hipSetDevice(g.device));
-    HIP_TRY(hipStreamCreateWithFlags(&g_rank.xs, hipStreamNonBlocking));
-    for (int r = 0; r < RankLoop::kRing; r++)
-        for (hipEvent_t* e : {&g_rank.counted[r], &g_rank.gathered[r], &g_rank.shaded[r], &g_rank.done[r]})
-            HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    g_rank.world = world;
-    g_rank.rank = rank;
-    g_rank.device = g.device;
-    g_rank.ring = 0;
+    if (rank_open(world, rank)) return RT_FAILURE;
     g_rank.rehearse_gathered = gathered_device;
-    g_rank.on = true;
     return RT_SUCCESS;
 }
 
@@ -2638,9 +2664,10 @@ extern "C" int rt_gpu_rank_finish(void) {
     if (!g_rank.on) return fail("rt_gpu_rank_finish: rt_gpu_rank_init not called");
     HIP_TRY(hipSetDevice(g.device));
     if (rank_gather_pending()) return RT_FAILURE;
-    // the caller's stream (and rt_gpu_synchronize) sees the exchange's end
+    // the caller's stream sees the exchange's end and rank 0's last host write
     const int last = (g_rank.ring + RankLoop::kRing - 1) % RankLoop::kRing;
     if (g_rank.done_valid[last]) HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.done[last], 0));
+    if (g_rank.written_valid[last]) HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.written[last], 0));
     return RT_SUCCESS;
 }
 
