@@ -696,13 +696,11 @@ void build_dir_grid(const rt_prim* prims, BvhBuild& out, int log2_cells) {
     out.grid_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-namespace {
-
-// The grid of 2^(L-1) cells per axis from one of 2^L: coarse cell (i, j) lists
-// the sorted union of cells (2i + a, 2j + b).
-void coarsen_grid(const std::vector<uint32_t>& start, const std::vector<uint32_t>& items_in, int L,
-                  std::vector<uint32_t>& out_start, std::vector<uint32_t>& out_items) {
-    const int Mc = (1 << L) / 2;
+void coarsen_dir_grid(BvhBuild& out) {
+    out.grid2_start.clear();
+    out.grid2_items.clear();
+    if (out.grid_log2 < 2 || out.grid_start.empty()) return;
+    const int L = out.grid_log2, M = 1 << L, Mc = M / 2;
     const size_t nc = (size_t)Mc * Mc;
     unsigned nt = std::thread::hardware_concurrency();
     if (nt < 1) nt = 1;
@@ -721,7 +719,8 @@ void coarsen_grid(const std::vector<uint32_t>& start, const std::vector<uint32_t
                         for (int a = 0; a < 2; a++)
                             for (int b = 0; b < 2; b++) {
                                 const size_t c = ((size_t)(2 * ic + a) << L) | (size_t)(2 * jc + b);
-                                u.insert(u.end(), items_in.begin() + start[c], items_in.begin() + start[c + 1]);
+                                u.insert(u.end(), out.grid_items.begin() + out.grid_start[c],
+                                         out.grid_items.begin() + out.grid_start[c + 1]);
                             }
                         std::sort(u.begin(), u.end());
                         u.erase(std::unique(u.begin(), u.end()), u.end());
@@ -731,34 +730,20 @@ void coarsen_grid(const std::vector<uint32_t>& start, const std::vector<uint32_t
             });
         for (auto& t : th) t.join();
     }
-    out_start.assign(nc + 1, 0);
+    out.grid2_start.assign(nc + 1, 0);
     uint64_t total = 0;
     size_t c = 0;
     for (unsigned w = 0; w < nt; w++)
         for (uint32_t n : lens[w]) {
-            out_start[c++] = (uint32_t)total;
+            out.grid2_start[c++] = (uint32_t)total;
             total += n;
         }
-    out_start[nc] = (uint32_t)total;
-    out_items.clear();
-    out_items.reserve(total);
+    out.grid2_start[nc] = (uint32_t)total;
+    out.grid2_items.reserve(total);
     for (unsigned w = 0; w < nt; w++) {
-        out_items.insert(out_items.end(), items[w].begin(), items[w].end());
+        out.grid2_items.insert(out.grid2_items.end(), items[w].begin(), items[w].end());
         std::vector<uint32_t>().swap(items[w]);
     }
-}
-
-}  // namespace
-
-void coarsen_dir_grid(BvhBuild& out) {
-    out.grid2_start.clear();
-    out.grid2_items.clear();
-    out.grid4_start.clear();
-    out.grid4_items.clear();
-    if (out.grid_log2 < 2 || out.grid_start.empty()) return;
-    coarsen_grid(out.grid_start, out.grid_items, out.grid_log2, out.grid2_start, out.grid2_items);
-    if (out.grid_log2 >= 3)  // the quarter-resolution grid from the half-resolution one
-        coarsen_grid(out.grid2_start, out.grid2_items, out.grid_log2 - 1, out.grid4_start, out.grid4_items);
 }
 
 }  // namespace rt580

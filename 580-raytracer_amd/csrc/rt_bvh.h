@@ -140,8 +140,6 @@ struct BvhBuild {
     // a K-way split), whose cells would hold few rays each.
     std::vector<uint32_t> grid2_start;  // [(M/2)^2 + 1]
     std::vector<uint32_t> grid2_items;
-    std::vector<uint32_t> grid4_start;  // [(M/4)^2 + 1]: the quarter-resolution grid (coarsen_dir_grid)
-    std::vector<uint32_t> grid4_items;
 };
 
 // Build over prims[0..n). Returns false if there are no triangles or a tree
@@ -165,8 +163,7 @@ double oct_node_radius(int level);
 // the sorted union of fine cells (2i + a, 2j + b). grid_cell(d, L - 1) is
 // grid_cell(d, L)'s (i >> 1, j >> 1) (power-of-two scalings of one float), and
 // a direction of the coarse cell lies in one of its children, whose list is
-// conservative: so is the union. out.grid4_* alike from out.grid2_* (2^(L-2)
-// cells per axis).
+// conservative: so is the union.
 void coarsen_dir_grid(BvhBuild& out);
 
 // Render-time guard for the camera (float ranges only; the bounds hold for any origin).

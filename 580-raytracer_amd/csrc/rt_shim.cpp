@@ -89,12 +89,10 @@ struct State {
     // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
     DevBuf bvh_nodes, bvh_nodes4, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always, scan_prims;
     DevBuf grid2_start, grid2_items;  // the half-resolution grid (coarsen_dir_grid)
-    DevBuf grid4_start, grid4_items;  // the quarter-resolution grid
     BvhBuild bvh;
     bool bvh_ok = false;
     int grid_log2 = 0, grid_n_always = 0;  // far-search direction grid (uploaded; host copy dropped)
     bool grid2 = false;                    // grid2_* uploaded (log2 = grid_log2 - 1)
-    bool grid4 = false;                    // grid4_* uploaded (log2 = grid_log2 - 2)
     int accel = RT_ACCEL_AUTO;
     bool last_accel = false;
     uint64_t scene_gen = 0;
@@ -369,12 +367,11 @@ int check_params(const rt_render_params* p) {
     return RT_SUCCESS;
 }
 
-// Frames of fewer pixels than this use the half-resolution direction grid, and
-// of fewer than a quarter of it the quarter-resolution one: fewer rays per
-// cell there, and a cell's list is read once per chunk of its rays. North-star
-// frame's K-way row shares (rank 1), fine -> half: K = 2 22.45 -> 21.62 ms, 4:
-// 13.40 -> 12.32, 8: 8.66 -> 7.55; the whole frame (2.07M pixels) keeps the fine
-// grid (38.8 vs 39.1 ms). RT580_GRID_COARSE_PX (0: never).
+// Frames of fewer pixels than this use the half-resolution direction grid:
+// fewer rays per cell there, and a cell's list is read once per chunk of its
+// rays. North-star frame's K-way row shares (rank 1), fine -> coarse: K = 2
+// 22.45 -> 21.62 ms, 4: 13.40 -> 12.32, 8: 8.66 -> 7.55; the whole frame (2.07M
+// pixels) keeps the fine grid (38.8 vs 39.1 ms). RT580_GRID_COARSE_PX (0: never).
 long grid_coarse_px() {
     static long v = -1;
     if (v < 0) {
@@ -425,14 +422,12 @@ DevScene dev_scene(const rt_render_params* p, int n_rows) {
     }
 #endif
     v.scale = g.bvh.scale;
-    const long px = n_rows >= 0 ? (long)n_rows * p->width : -1;
-    const bool coarse = g.grid2 && px >= 0 && px < grid_coarse_px();
-    const bool quarter = coarse && g.grid4 && px < grid_coarse_px() / 4;
-    v.grid_start = (const uint32_t*)(quarter ? g.grid4_start.p : coarse ? g.grid2_start.p : g.grid_start.p);
-    v.grid_items = (const uint32_t*)(quarter ? g.grid4_items.p : coarse ? g.grid2_items.p : g.grid_items.p);
+    const bool coarse = g.grid2 && n_rows >= 0 && (long)n_rows * p->width < grid_coarse_px();
+    v.grid_start = (const uint32_t*)(coarse ? g.grid2_start.p : g.grid_start.p);
+    v.grid_items = (const uint32_t*)(coarse ? g.grid2_items.p : g.grid_items.p);
     v.grid_always = (const uint32_t*)g.grid_always.p;
     v.n_always = g.grid_n_always;
-    v.grid_log2 = quarter ? g.grid_log2 - 2 : coarse ? g.grid_log2 - 1 : g.grid_log2;
+    v.grid_log2 = coarse ? g.grid_log2 - 1 : g.grid_log2;
     v.grid_r = g.bvh.grid_r;
     return s;
 }
@@ -1026,7 +1021,7 @@ std::vector<DevBuf State::*> scene_bufs() {
     return {&State::prims, &State::shade, &State::mats, &State::lights, &State::bvh_nodes, &State::bvh_nodes4,
             &State::bvh_prims, &State::bvh_ids, &State::far_nodes, &State::far_tris, &State::brute,
             &State::grid_start, &State::grid_items, &State::grid_always, &State::scan_prims, &State::grid2_start,
-            &State::grid2_items, &State::grid4_start, &State::grid4_items};
+            &State::grid2_items};
 }
 
 // The scene of context `src` into the current context without building
@@ -1053,7 +1048,6 @@ int clone_scene(int src) {
     g.bvh_ok = c.bvh_ok;
     g.grid_log2 = c.grid_log2;
     g.grid2 = c.grid2;
-    g.grid4 = c.grid4;
     g.grid_n_always = c.grid_n_always;
     g.n_prims = c.n_prims;
     g.n_lights = c.n_lights;
@@ -1174,7 +1168,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
     g.bvh_ok = false;
     release(g.scan_prims);
     g.grid_log2 = g.grid_n_always = 0;
-    g.grid2 = g.grid4 = false;
+    g.grid2 = false;
     if (s->n_prims > 64) {
         g.bvh_ok = build_bvh(s->prims, s->n_prims, g.bvh);
         // far-search direction grid: 2048^2 cells (field100k: 19.4 candidates
@@ -1198,9 +1192,7 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
              upload_vec(g.grid_items, g.bvh.grid_items, "the direction-grid lists") ||
              upload_vec(g.grid_always, g.bvh.grid_always, "the direction-grid always-list") ||
              upload_vec(g.grid2_start, g.bvh.grid2_start, "the half-resolution grid offsets") ||
-             upload_vec(g.grid2_items, g.bvh.grid2_items, "the half-resolution grid lists") ||
-             upload_vec(g.grid4_start, g.bvh.grid4_start, "the quarter-resolution grid offsets") ||
-             upload_vec(g.grid4_items, g.bvh.grid4_items, "the quarter-resolution grid lists")))
+             upload_vec(g.grid2_items, g.bvh.grid2_items, "the half-resolution grid lists")))
             return RT_FAILURE;
         if (g.bvh_ok && !g.bvh.far_nodes.empty()) {
             // The any-hit scan order of far-origin rays (far_scan_kernel): a fixed
@@ -1216,7 +1208,6 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         }
         g.grid_log2 = g.bvh.grid_start.empty() ? 0 : g.bvh.grid_log2;
         g.grid2 = g.grid_log2 > 1 && !g.bvh.grid2_start.empty();
-        g.grid4 = g.grid2 && g.grid_log2 > 2 && !g.bvh.grid4_start.empty();
         g.grid_n_always = (int)g.bvh.grid_always.size();
         // the device needs only the arrays; keep the host copy small
         g.bvh.prims = std::vector<rt_prim>();
@@ -1229,8 +1220,6 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
         g.bvh.grid_always = std::vector<uint32_t>();
         g.bvh.grid2_start = std::vector<uint32_t>();
         g.bvh.grid2_items = std::vector<uint32_t>();
-        g.bvh.grid4_start = std::vector<uint32_t>();
-        g.bvh.grid4_items = std::vector<uint32_t>();
     }
     if (device_sync("at the end of the scene upload")) return RT_FAILURE;
     g.n_prims = s->n_prims;
@@ -1923,8 +1912,7 @@ void shutdown_ctx() {
     (void)hipSetDevice(g.device);
     if (sync_all() || device_sync("at shutdown"))
         std::fprintf(stderr, "rt_gpu: shutting down after a device error (%s)\n", g_err);
-    for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always, &g.grid2_start, &g.grid2_items, &g.grid4_start,
-                      &g.grid4_items})
+    for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always, &g.grid2_start, &g.grid2_items})
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute,
                       &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.ppm_stage})

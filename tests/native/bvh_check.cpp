@@ -125,19 +125,13 @@ int main(int argc, char** argv) {
     BvhView Vnear = V;  // control: without the far search some results must differ
     Vnear.has_far = 0;
     // the half-resolution grid of row-share frames (coarsen_dir_grid): same answers
-    BvhView Vc = V, Vq = V;  // and the quarter-resolution grid of smaller shares
+    BvhView Vc = V;
     if (use_grid && V.grid_log2 > 1) {
         coarsen_dir_grid(B);
         Vc.grid_start = B.grid2_start.data();
         Vc.grid_items = B.grid2_items.data();
         Vc.grid_log2 = V.grid_log2 - 1;
         std::printf("coarse grid log2=%d items=%zu\n", Vc.grid_log2, B.grid2_items.size());
-        if (!B.grid4_start.empty()) {
-            Vq.grid_start = B.grid4_start.data();
-            Vq.grid_items = B.grid4_items.data();
-            Vq.grid_log2 = V.grid_log2 - 2;
-            std::printf("quarter grid log2=%d items=%zu\n", Vq.grid_log2, B.grid4_items.size());
-        }
     }
     std::atomic<long> bad{0}, hits{0}, anyhits{0}, far_closest{0}, near_only_bad{0}, point_checks{0}, bad4{0};
 #ifdef RT_BVH_COUNT
@@ -256,10 +250,9 @@ int main(int argc, char** argv) {
                 if (same && cb)
                     same = hb.prim == hv.prim && fbits(hb.t) == fbits(hv.t) && fbits(hb.a) == fbits(hv.a) &&
                            fbits(hb.b) == fbits(hv.b) && fbits(hb.g) == fbits(hv.g);
-                for (const BvhView* Vx : {&Vc, &Vq}) {
-                    if (Vx->grid_log2 == V.grid_log2) continue;
+                if (Vc.grid_log2 != V.grid_log2) {
                     Hit hc;
-                    const bool cc = bvh_closest(*Vx, o, d, hc), ac = bvh_any(*Vx, o, d);
+                    const bool cc = bvh_closest(Vc, o, d, hc), ac = bvh_any(Vc, o, d);
                     if (cc != cv || ac != av ||
                         (cc && (hc.prim != hv.prim || fbits(hc.t) != fbits(hv.t) || fbits(hc.a) != fbits(hv.a) ||
                                 fbits(hc.b) != fbits(hv.b) || fbits(hc.g) != fbits(hv.g))))
