@@ -125,6 +125,7 @@ struct BvhView {
     const uint32_t* grid_start;
     const uint32_t* grid_items;
     const uint32_t* grid_always;
+    const uint32_t* grid_live;  // bit c: cell c's list is not empty (the far queues' filter, far_live)
     int n_always;
     int grid_log2;
     float grid_r;

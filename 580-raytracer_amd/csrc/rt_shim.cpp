@@ -89,6 +89,7 @@ struct State {
     // exact BVH (rt_bvh.h), built at upload for triangle scenes beyond one LDS tile
     DevBuf bvh_nodes, bvh_nodes4, bvh_prims, bvh_ids, far_nodes, far_tris, brute, grid_start, grid_items, grid_always, scan_prims;
     DevBuf grid2_start, grid2_items;  // the half-resolution grid (coarsen_dir_grid)
+    DevBuf grid_live, grid2_live;     // bitmaps of the grids' non-empty cells (far_live)
     BvhBuild bvh;
     bool bvh_ok = false;
     int grid_log2 = 0, grid_n_always = 0;  // far-search direction grid (uploaded; host copy dropped)
@@ -381,6 +382,14 @@ long grid_coarse_px() {
     return v;
 }
 
+// Bit c set: cell c of a grid (its list offsets `start`) lists a candidate.
+std::vector<uint32_t> live_bitmap(const std::vector<uint32_t>& start) {
+    std::vector<uint32_t> bits(start.empty() ? 0 : (start.size() - 1 + 31) / 32, 0u);
+    for (size_t c = 0; c + 1 < start.size(); c++)
+        if (start[c + 1] != start[c]) bits[c >> 5] |= 1u << (c & 31);
+    return bits;
+}
+
 // n_rows: the frame's rows (selects the direction grid; -1: the fine one).
 DevScene dev_scene(const rt_render_params* p, int n_rows) {
     DevScene s;
@@ -426,6 +435,7 @@ DevScene dev_scene(const rt_render_params* p, int n_rows) {
     v.grid_start = (const uint32_t*)(coarse ? g.grid2_start.p : g.grid_start.p);
     v.grid_items = (const uint32_t*)(coarse ? g.grid2_items.p : g.grid_items.p);
     v.grid_always = (const uint32_t*)g.grid_always.p;
+    v.grid_live = (const uint32_t*)(coarse ? g.grid2_live.p : g.grid_live.p);
     v.n_always = g.grid_n_always;
     v.grid_log2 = coarse ? g.grid_log2 - 1 : g.grid_log2;
     v.grid_r = g.bvh.grid_r;
@@ -1021,7 +1031,7 @@ std::vector<DevBuf State::*> scene_bufs() {
     return {&State::prims, &State::shade, &State::mats, &State::lights, &State::bvh_nodes, &State::bvh_nodes4,
             &State::bvh_prims, &State::bvh_ids, &State::far_nodes, &State::far_tris, &State::brute,
             &State::grid_start, &State::grid_items, &State::grid_always, &State::scan_prims, &State::grid2_start,
-            &State::grid2_items};
+            &State::grid2_items, &State::grid_live, &State::grid2_live};
 }
 
 // The scene of context `src` into the current context without building
@@ -1189,6 +1199,8 @@ int rt_gpu_upload_scene(const rt_scene_soa* s) {
              upload_vec(g.far_tris, g.bvh.far_tris, "the plane records") ||
              upload_vec(g.brute, g.bvh.brute, "the brute-force list") ||
              upload_vec(g.grid_start, g.bvh.grid_start, "the direction-grid offsets") ||
+             upload_vec(g.grid_live, live_bitmap(g.bvh.grid_start), "the direction-grid cell bitmap") ||
+             upload_vec(g.grid2_live, live_bitmap(g.bvh.grid2_start), "the half-resolution cell bitmap") ||
              upload_vec(g.grid_items, g.bvh.grid_items, "the direction-grid lists") ||
              upload_vec(g.grid_always, g.bvh.grid_always, "the direction-grid always-list") ||
              upload_vec(g.grid2_start, g.bvh.grid2_start, "the half-resolution grid offsets") ||
@@ -1912,7 +1924,8 @@ void shutdown_ctx() {
     (void)hipSetDevice(g.device);
     if (sync_all() || device_sync("at shutdown"))
         std::fprintf(stderr, "rt_gpu: shutting down after a device error (%s)\n", g_err);
-    for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always, &g.grid2_start, &g.grid2_items})
+    for (DevBuf* b : {&g.grid_start, &g.grid_items, &g.grid_always, &g.grid2_start, &g.grid2_items, &g.grid_live,
+                      &g.grid2_live})
         release(*b);
     for (DevBuf* b : {&g.bvh_nodes, &g.bvh_nodes4, &g.bvh_prims, &g.bvh_ids, &g.far_nodes, &g.far_tris, &g.brute,
                       &g.prims, &g.shade, &g.mats, &g.lights, &g.scan_prims, &g.ppm_stage})
