@@ -300,6 +300,22 @@ RTM_HD bool far_candidate(const FarTri& ft, const FarRay& r, rv3 o, rv3 d) {
     return t >= T;
 }
 
+// far_candidate without the division: a superset of it (every pair with
+// t >= T_j passes, and the few with 0.999 T_j <= t < T_j, or T_j <= 0, too).
+// For the cell kernels, which queue the passing pairs for the reference's full
+// test: a pair that then hits is a hit of the reference's own loop whatever its
+// t, and one with t < T_j was already found by the near walk (the same key), so
+// the any-hit flag and the closest key are unchanged. Saves the division that a
+// wave executes whenever any of its 64 pairs passes (about half its steps).
+RTM_HD bool far_candidate_filter(const FarTri& ft, const FarRay& r, rv3 o, rv3 d) {
+    const rv3 N = ld3(ft.n);
+    const float nd = v3_dot(N, d);
+    if (rt_lt_eps(fabsf(nd))) return false;
+    const float num = -(v3_dot(N, o) + ft.d);
+    const float T = far_T(r, ft.dhi);
+    return !(T > 0.0f) || (num * nd > 0.0f && fabsf(num) >= 0.999f * T * fabsf(nd));
+}
+
 // The far search of bvh_closest on its own (per ray): merges into h.
 RTM_HD bool far_closest(const BvhView& V, rv3 o, rv3 d, Hit& h, bool found) {
     if (dir_zero(d)) return found;

@@ -1861,6 +1861,10 @@ __device__ __forceinline__ CellItem cell_item(const BvhView& V, uint4 wd) {
     it.skip = !it.tree && V.n_always + (int)it.n_list == 0;  // no candidate: no far hit in this cell
     return it;
 }
+// lane j's value of x (j wave-uniform)
+__device__ __forceinline__ float lane_f32(float x, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j));
+}
 __device__ __forceinline__ int cell_lg(int lt) {
     return lt > 32 ? 6 : lt > 16 ? 5 : lt > 8 ? 4 : lt > 4 ? 3 : lt > 2 ? 2 : lt > 1 ? 1 : 0;
 }
@@ -1958,6 +1962,9 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 uint32_t qn = 0;  // queued (candidate, ray) pairs, wave-uniform
+                // this lane's ray, for the full chunks' register broadcasts
+                const float rR = far_ray(V, v3(a.x, a.y, a.z)).R;
+                uint64_t hitm = 0;  // rays flagged by the full tests so far (refreshed after each batch)
                 for (int kc = 0; kc < (CELL_SKIP(1) ? 0 : n_cand); kc += 64) {
                     const int lt = n_cand - kc < 64 ? n_cand - kc : 64;
                     const int lg = cell_lg(lt);
@@ -1967,6 +1974,40 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                     if (kc > 0 && has) {
                         const int k = kc + kk - V.n_always;
                         ft = V.far_tris[k < 0 ? V.grid_always[k + V.n_always] : V.grid_items[cur.lb + (uint32_t)k]];
+                    }
+                    if (lg == 6 && !CELL_SKIP(3)) {
+                        // 64 candidates, one ray a step: the ray is wave-uniform, read
+                        // from its lane's registers (7 readlanes) instead of LDS (two
+                        // b128 reads and the flag: the LDS pipe, not the VALU, bound
+                        // this loop), and rays already hit are skipped as a whole step.
+                        uint64_t todo = __ballot(live) & ~hitm;
+                        while (todo) {
+                            const int j = __builtin_ctzll(todo);
+                            todo &= todo - 1;
+                            FarRay fj;
+                            fj.R = lane_f32(rR, j);
+                            const rv3 oj = v3(lane_f32(a.x, j), lane_f32(a.y, j),
+                                              lane_f32(a.z, j));
+                            const rv3 dj = v3(lane_f32(b.x, j), lane_f32(b.y, j),
+                                              lane_f32(b.z, j));
+                            const bool fc = far_candidate_filter(ft, fj, oj, dj);
+                            RT_CELL_STAT(2, fc ? 1 : 0);
+                            const uint64_t m = __ballot(fc);
+                            if (m == 0) continue;
+                            if (fc) {
+                                const uint32_t slot = qn + (uint32_t)__popcll(m & lanemask_lt());
+                                pq_id[wave][slot] = ft.id;
+                                pq_j[wave][slot] = (uint8_t)j;
+                            }
+                            qn += (uint32_t)__popcll(m);
+                            if (qn >= 64u) {
+                                cell_full_tests(S, sray[wave], shit[wave], pq_id[wave], pq_j[wave], qn);
+                                qn = 0;
+                                hitm = __ballot(live && shit[wave][lane] != 0u);
+                                todo &= ~hitm;
+                            }
+                        }
+                        continue;
                     }
                     const uint32_t step = 64u >> lg;
                     for (uint32_t j0 = 0; j0 < nr; j0 += step) {
@@ -1980,7 +2021,7 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                                 if (aj.x == ft.n[0] && bj.w == ft.d) shit[wave][j] = 1u;
                                 continue;
                             }
-                            fc = far_candidate(ft, fj, v3(aj.x, aj.y, aj.z), v3(bj.x, bj.y, bj.z));
+                            fc = far_candidate_filter(ft, fj, v3(aj.x, aj.y, aj.z), v3(bj.x, bj.y, bj.z));
                         }
                         RT_CELL_STAT(2, fc ? 1 : 0);
                         // passing pairs are queued; their full tests run 64 at a time
@@ -1997,6 +2038,7 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                         if (qn >= 64u) {
                             cell_full_tests(S, sray[wave], shit[wave], pq_id[wave], pq_j[wave], qn);
                             qn = 0;
+                            hitm = __ballot(live && shit[wave][lane] != 0u);
                         }
                     }
                 }
@@ -2141,7 +2183,7 @@ far_cell_closest_kernel(DevScene S, DevWork W) {
                     const float4 aj = sray[wave][j][0], bj = sray[wave][j][1];
                     FarRay fj;
                     fj.R = bj.w;
-                    fc = far_candidate(ft, fj, v3(aj.x, aj.y, aj.z), v3(bj.x, bj.y, bj.z));
+                    fc = far_candidate_filter(ft, fj, v3(aj.x, aj.y, aj.z), v3(bj.x, bj.y, bj.z));
                 }
                 const uint64_t m = __ballot(fc);
                 if (m == 0) continue;

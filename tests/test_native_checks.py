@@ -114,6 +114,16 @@ def test_direction_grid_node_radius_covers_every_direction():
     assert worst > 2.9, out  # the sampling reaches the bound's tight region
 
 
+def test_far_candidate_filter_is_a_superset():
+    """The cell kernels test (ray, candidate) pairs with far_candidate_filter, which
+    drops far_candidate's division: every pair far_candidate passes must pass it
+    (the extra pairs only get the reference's own full test)."""
+    exe = _build("farcand_check", [os.path.join(CSRC, "rt_bvh.cpp"), os.path.join(CSRC, "rt_scene.cpp")])
+    out = _run(exe, "4000000")
+    n_exact = int(out.split("far_candidate=")[1].split()[0])
+    assert n_exact > 100000, out  # the placed pairs reach the t ~ T_j boundary
+
+
 def test_mt19937_block_jump_ahead_equals_the_engine():
     """rt_mt.h: the window W_J reached by the polynomial jump (x^(J-1) mod phi,
     phi from Berlekamp-Massey) yields std::mt19937's draws J, J+1, ... after
