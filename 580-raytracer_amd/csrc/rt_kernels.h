@@ -206,6 +206,10 @@ hipError_t upload_gamma_lut(const uint8_t* lut, hipStream_t s);
 hipError_t launch_gamma_u8(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
 // the same, 16 bytes per lane (out 16-byte aligned; e.g. mapped host memory)
 hipError_t launch_gamma_u8_wide(const int16_t* fb, uint64_t n, uint8_t* out, hipStream_t s);
+// rows row0, row0 + step, ... (n_rows packed int16 rows) as PPM bytes at their
+// places in a whole frame's body (a rank's rows straight into the shared host frame)
+hipError_t launch_gamma_rows_u8(const int16_t* fb, int n_rows, int width, int row0, int step, uint8_t* out,
+                                hipStream_t s);
 // mt19937 draws [lo, hi) of the serial stream into out[0, hi - lo): one
 // workgroup per checkpoint block k in [k0, k0 + nblk) (rt_mt.h: windows[j] =
 // W_{(k0 + j) kMtBlock}), each running the twist from its window.

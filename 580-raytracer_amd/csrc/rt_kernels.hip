@@ -3070,6 +3070,50 @@ hipError_t launch_gamma_u8_wide(const int16_t* fb, uint64_t n, uint8_t* out, hip
     return hipGetLastError();
 }
 
+// A rank's rows (rows row0, row0 + step, ... of the frame; n_rows int16 rows of
+// `width` pixels, packed) mapped to PPM bytes and stored at their places in the
+// whole frame's body `out` (mapped host memory shared by the ranks, or any
+// frame-sized buffer): each rank writes its own rows over its own host link,
+// no gather. 16 bytes per lane when a row is a whole number of them.
+__global__ void __launch_bounds__(TB) gamma_rows_u8_wide_kernel(const int16_t* __restrict__ fb, uint32_t row16,
+                                                                uint32_t n_rows, uint32_t row0, uint32_t step,
+                                                                uint8_t* __restrict__ out) {
+    __shared__ uint32_t lut[256];
+    for (int k = threadIdx.x; k < 256; k += TB) lut[k] = c_gamma_lut[k];
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(fb);
+    uint4* dst = reinterpret_cast<uint4*>(out);
+    const uint64_t total = (uint64_t)row16 * n_rows;
+    for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < total; i += (uint64_t)gridDim.x * TB) {
+        const uint64_t y = i / row16, e = i - y * row16;
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        dst[(row0 + y * step) * row16 + e] =
+            make_uint4(gamma4(lut, a.x, a.y), gamma4(lut, a.z, a.w), gamma4(lut, b.x, b.y), gamma4(lut, b.z, b.w));
+    }
+}
+__global__ void gamma_rows_u8_kernel(const int16_t* __restrict__ fb, uint32_t row_bytes, uint32_t n_rows,
+                                     uint32_t row0, uint32_t step, uint8_t* __restrict__ out) {
+    const uint64_t total = (uint64_t)row_bytes * n_rows;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t y = i / row_bytes, e = i - y * row_bytes;
+        const int v = fb[i];
+        out[(row0 + y * step) * row_bytes + e] = c_gamma_lut[v < 0 ? 0 : (v > 255 ? 255 : v)];
+    }
+}
+
+hipError_t launch_gamma_rows_u8(const int16_t* fb, int n_rows, int width, int row0, int step, uint8_t* out,
+                                hipStream_t s) {
+    const uint32_t rb = (uint32_t)width * 3u;
+    if (n_rows <= 0 || rb == 0) return hipSuccess;
+    if (rb % 16 == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)fb % 32) == 0)
+        hipLaunchKernelGGL(gamma_rows_u8_wide_kernel, dim3(grid_for((uint64_t)rb / 16 * n_rows, kD2HBlocks)), dim3(TB),
+                           0, s, fb, rb / 16, (uint32_t)n_rows, (uint32_t)row0, (uint32_t)step, out);
+    else
+        hipLaunchKernelGGL(gamma_rows_u8_kernel, dim3(grid_for((uint64_t)rb * n_rows, 8192)), dim3(TB), 0, s, fb, rb,
+                           (uint32_t)n_rows, (uint32_t)row0, (uint32_t)step, out);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- math self-test
 // The device-only fast sequences against the plain operations they replace:
 //  [0] rt_sqrt_nr vs sqrtf over EVERY float in [2^-96, +inf] and +0

@@ -2420,7 +2420,18 @@ int multi_frame_async(const rt_render_params* p, uint8_t* ppm_host, int n, const
 // chain stays off the caller's stream: the slot stream traces and copies the
 // counts, xs exchanges them and scans the row bases, the slot stream shades.
 // Rank 0 writes each PPM body into host memory on a stream of its own (hs),
-// so the ~0.1 ms of the host link per 1080p frame never holds xs. Buffers come
+// so the ~0.1 ms of the host link per 1080p frame never holds xs.
+//
+// Shared body (rt_gpu_rank_share_body, what NativeRankFrame sets on one node):
+// every rank's buffer is its own mapping of ONE host frame shared by the
+// processes; each rank's shading writes its rows' PPM bytes straight to their
+// places in it over its own host link (launch_gamma_rows_u8), and the frame's
+// "gather" is a 4-byte all-gather on xs after every rank's write: when it
+// completes on rank 0, every rank's rows have landed. No tile moves over xGMI
+// and rank 0's link carries 1/world of the frame instead of all of it (at
+// 8 ranks its whole-frame write, ~0.12 ms per 1080p frame, was the slowest
+// rank's extra). With one rank there is no exchange at all: the row bases are
+// scanned on the slot stream. Buffers come
 // from a ring of three sets, one per frame slot; frame k+3 starts after frame
 // k's gather (the caller's stream, which the slot waits on, waits its xs
 // event) and receives into root8 after frame k's host write (xs waits hs).
@@ -2431,7 +2442,8 @@ struct RankLoop {
     hipStream_t xs = nullptr, hs = nullptr;
     static constexpr int kRing = 3;
     int ring = 0;
-    DevBuf rc[kRing], gat[kRing], base[kRing], t8[kRing], root8[kRing];
+    DevBuf rc[kRing], gat[kRing], base[kRing], t8[kRing], root8[kRing], bar[kRing];
+    bool shared = false;  // rt_gpu_rank_share_body
     hipEvent_t counted[kRing] = {}, gathered[kRing] = {}, shaded[kRing] = {}, done[kRing] = {}, recvd[kRing] = {},
                written[kRing] = {};
     bool done_valid[kRing] = {}, written_valid[kRing] = {};
@@ -2459,7 +2471,9 @@ int rank_teardown() {
     if (g_rank.comm) (void)g_rccl.CommDestroy(g_rank.comm);
     g_rank.comm = nullptr;
     for (int r = 0; r < RankLoop::kRing; r++) {
-        for (DevBuf* b : {&g_rank.rc[r], &g_rank.gat[r], &g_rank.base[r], &g_rank.t8[r], &g_rank.root8[r]}) release(*b);
+        for (DevBuf* b : {&g_rank.rc[r], &g_rank.gat[r], &g_rank.base[r], &g_rank.t8[r], &g_rank.root8[r],
+                          &g_rank.bar[r]})
+            release(*b);
         g_rank.done_valid[r] = g_rank.written_valid[r] = false;
     }
     for (hipEvent_t* e : g_rank.events()) {
@@ -2472,6 +2486,7 @@ int rank_teardown() {
     }
     g_rank.on = false;
     g_rank.pending = false;
+    g_rank.shared = false;
     g_rank.rehearse_gathered = nullptr;
     return st;
 }
@@ -2500,6 +2515,20 @@ int rank_gather_pending() {
     const size_t t8 = (size_t)n_max * W * 3, body = (size_t)H * W * 3;
     hipStream_t xs = g_rank.xs, hs = g_rank.hs;
     HIP_TRY(hipStreamWaitEvent(xs, g_rank.shaded[r], 0));
+    if (g_rank.shared) {
+        // every rank's rows are in the shared frame once each rank's shading
+        // (and its host write) has ended: a 4-byte all-gather says so to all
+        if (n > 1 && g_rank.comm)
+            RCCL_TRY(g_rccl.AllGather((int32_t*)g_rank.bar[r].p + g_rank.rank, g_rank.bar[r].p, 1, ncclInt32,
+                                      g_rank.comm, xs));
+        HIP_TRY(hipEventRecord(g_rank.done[r], xs));
+        g_rank.done_valid[r] = true;
+        if (g_rank.rank == 0) {
+            HIP_TRY(hipEventRecord(g_rank.written[r], xs));
+            g_rank.written_valid[r] = true;
+        }
+        return RT_SUCCESS;
+    }
     if (g_rank.rank == 0) {
         if (g_rank.written_valid[r]) HIP_TRY(hipStreamWaitEvent(xs, g_rank.written[r], 0));  // root8[r] read out
         HIP_TRY(hipMemcpyAsync(g_rank.root8[r].p, g_rank.t8[r].p, t8, hipMemcpyDeviceToDevice, xs));
@@ -2542,8 +2571,10 @@ int rank_frame(const rt_render_params* p, uint8_t* ppm_host) {
     const int n = g_rank.world, rank = g_rank.rank, H = p->height, W = p->width;
     const int n_max = (H + n - 1) / n;
     const size_t t8 = (size_t)n_max * W * 3, body = (size_t)H * W * 3;
-    if (rank == 0 && !host_range(ppm_host, body))
-        return fail("rt_gpu_render_rank_async: rank 0's buffer is not a registered range of %zu bytes", body);
+    const bool sh = g_rank.shared;
+    if ((rank == 0 || sh) && !host_range(ppm_host, body))
+        return fail("rt_gpu_render_rank_async: %s buffer is not a registered range of %zu bytes",
+                    sh ? "the shared frame's" : "rank 0's", body);
     HIP_TRY(hipSetDevice(g.device));
     const int r = g_rank.ring;
     g_rank.ring = (r + 1) % RankLoop::kRing;
@@ -2553,7 +2584,7 @@ int rank_frame(const rt_render_params* p, uint8_t* ppm_host) {
     if (g_rank.done_valid[r]) HIP_TRY(hipStreamWaitEvent(g.stream, g_rank.done[r], 0));
     if (ensure(g_rank.rc[r], (size_t)n_max * 4) || ensure(g_rank.gat[r], (size_t)n * n_max * 4) ||
         ensure(g_rank.base[r], (size_t)n_max * 8) || ensure(g_rank.t8[r], t8) ||
-        (rank == 0 && ensure(g_rank.root8[r], t8 * n)))
+        (rank == 0 && !sh && ensure(g_rank.root8[r], t8 * n)) || (sh && ensure(g_rank.bar[r], (size_t)n * 4)))
         return RT_FAILURE;
     rt_render_params pk = *p;
     pk.row_begin = rank;
@@ -2576,24 +2607,44 @@ int rank_frame(const rt_render_params* p, uint8_t* ppm_host) {
     HIP_TRY(hipMemsetAsync(g_rank.rc[r].p, 0, (size_t)n_max * 4, fs()));  // padding rows count 0
     if (n_rows)
         HIP_TRY(hipMemcpyAsync(g_rank.rc[r].p, SL.row_calls.p, (size_t)n_rows * 4, hipMemcpyDeviceToDevice, fs()));
-    // the exchange and the row bases on xs: every rank's per-row counts (H int32 in all)
-    HIP_TRY(hipEventRecord(g_rank.counted[r], fs()));
-    HIP_TRY(hipStreamWaitEvent(g_rank.xs, g_rank.counted[r], 0));
-    if (g_rank.comm)
-        RCCL_TRY(g_rccl.AllGather(g_rank.rc[r].p, g_rank.gat[r].p, (size_t)n_max, ncclInt32, g_rank.comm, g_rank.xs));
-    else  // rehearsal: the world's counts as precomputed, this rank's own rows included
-        HIP_TRY(hipMemcpyAsync(g_rank.gat[r].p, g_rank.rehearse_gathered, (size_t)n * n_max * 4,
-                               hipMemcpyDeviceToDevice, g_rank.xs));
-    HIP_TRY(launch_row_bases((const int32_t*)g_rank.gat[r].p, n, n_max, H, rank, (uint64_t*)g_rank.base[r].p,
-                             g_rank.xs));
-    HIP_TRY(hipEventRecord(g_rank.gathered[r], g_rank.xs));
-    HIP_TRY(hipStreamWaitEvent(fs(), g_rank.gathered[r], 0));
+    if (n == 1) {  // one rank: its counts are the world's; the bases on the slot
+        HIP_TRY(launch_row_bases((const int32_t*)g_rank.rc[r].p, 1, n_max, H, 0, (uint64_t*)g_rank.base[r].p, fs()));
+    } else {
+        // the exchange and the row bases on xs: every rank's per-row counts (H int32 in all)
+        HIP_TRY(hipEventRecord(g_rank.counted[r], fs()));
+        HIP_TRY(hipStreamWaitEvent(g_rank.xs, g_rank.counted[r], 0));
+        if (g_rank.comm)
+            RCCL_TRY(g_rccl.AllGather(g_rank.rc[r].p, g_rank.gat[r].p, (size_t)n_max, ncclInt32, g_rank.comm,
+                                      g_rank.xs));
+        else  // rehearsal: the world's counts as precomputed, this rank's own rows included
+            HIP_TRY(hipMemcpyAsync(g_rank.gat[r].p, g_rank.rehearse_gathered, (size_t)n * n_max * 4,
+                                   hipMemcpyDeviceToDevice, g_rank.xs));
+        HIP_TRY(launch_row_bases((const int32_t*)g_rank.gat[r].p, n, n_max, H, rank, (uint64_t*)g_rank.base[r].p,
+                                 g_rank.xs));
+        HIP_TRY(hipEventRecord(g_rank.gathered[r], g_rank.xs));
+        HIP_TRY(hipStreamWaitEvent(fs(), g_rank.gathered[r], 0));
+    }
     // phase 2 on the slot: shading with those RNG bases, the rows' PPM bytes
     const size_t nv = (size_t)n_rows * W * 3;
     if (ensure(SL.fb, nv * 2)) return RT_FAILURE;  // the slot's own int16 rows
     if (shade_rows(&pk, pk.row_begin, pk.row_step, n_rows, (const uint64_t*)g_rank.base[r].p, (int16_t*)SL.fb.p))
         return RT_FAILURE;
-    HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, nv, (uint8_t*)g_rank.t8[r].p, fs()));
+    if (sh) {  // this rank's rows straight to their places in the shared frame
+        HostRange* hr = host_range_ready(ppm_host, body);
+        if (!hr) return fail("rt_gpu_render_rank_async: the shared frame's buffer is not registered");
+        HIP_TRY(hipStreamWaitEvent(fs(), hr->copied, 0));
+        if (uint8_t* dst = (uint8_t*)mapped(hr, ppm_host)) {
+            HIP_TRY(launch_gamma_rows_u8((const int16_t*)SL.fb.p, n_rows, W, rank, n, dst, fs()));
+        } else {  // (not device-mapped: the rows' bytes on the device, one strided copy)
+            HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, nv, (uint8_t*)g_rank.t8[r].p, fs()));
+            if (n_rows)
+                HIP_TRY(hipMemcpy2DAsync(ppm_host + (size_t)rank * W * 3, (size_t)n * W * 3, g_rank.t8[r].p,
+                                         (size_t)W * 3, (size_t)W * 3, (size_t)n_rows, hipMemcpyDeviceToHost, fs()));
+        }
+        HIP_TRY(hipEventRecord(hr->copied, fs()));
+    } else {
+        HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, nv, (uint8_t*)g_rank.t8[r].p, fs()));
+    }
     // the slot's end without the caller's stream waiting for it: the gather (on
     // xs, next call) waits for `shaded`, the caller's stream goes on
     if (post_replay_check()) return RT_FAILURE;
@@ -2663,6 +2714,15 @@ extern "C" int rt580_rank_rehearse(int world, int rank, const int32_t* gathered_
     HIP_TRY(hipSetDevice(g.device));
     if (rank_open(world, rank)) return RT_FAILURE;
     g_rank.rehearse_gathered = gathered_device;
+    return RT_SUCCESS;
+}
+
+extern "C" int rt_gpu_rank_share_body(int on) {
+    RT_ENTRY("rt_gpu_rank_share_body");
+    if (!g_rank.on) return fail("rt_gpu_rank_share_body: rt_gpu_rank_init not called");
+    if (g_rank.pending || g_rank.done_valid[0] || g_rank.done_valid[1] || g_rank.done_valid[2])
+        return fail("rt_gpu_rank_share_body: set before the first frame");
+    g_rank.shared = on != 0;
     return RT_SUCCESS;
 }
 

@@ -82,6 +82,7 @@ SIGNATURES = [
     ("rt_gpu_rank_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     ("rt_gpu_rank_init", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),
     ("rt_gpu_render_rank_async", ctypes.c_int, [ctypes.POINTER(RenderParams), ctypes.c_void_p]),
+    ("rt_gpu_rank_share_body", ctypes.c_int, [ctypes.c_int]),
     ("rt_gpu_rank_finish", ctypes.c_int, []),
     ("rt_gpu_rank_shutdown", ctypes.c_int, []),
     ("rt580_rank_rehearse", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),

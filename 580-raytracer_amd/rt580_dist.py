@@ -123,6 +123,23 @@ def render_frame(backend, dist, torch, height, width, rank, world, gather=True):
     return None
 
 
+def render_frame_shared(backend, dist, torch, height, width, rank, world, body, lut):
+    """The shared-body form of render_frame (what NativeRankFrame's library loop
+    does with rt_gpu_rank_share_body, restated over torch.distributed for the
+    gloo tests): each rank maps its rows to PPM bytes (`lut`, the writer's gamma
+    table) and stores them at their places in `body` -- its view (H, W, 3) uint8
+    of ONE frame shared by the ranks (SharedHostFrames) -- then a 4-byte
+    all-gather says every rank's rows have landed. Returns body on rank 0."""
+    import numpy as np
+    fb = render_frame(backend, dist, torch, height, width, rank, world, gather=False)
+    n = n_local_rows(height, rank, world)
+    rows = fb.cpu().numpy().reshape(-1, width, 3)[:n]
+    body[rank::world] = lut[np.clip(rows.astype(np.int64), 0, 255)]
+    flag = torch.ones(1, dtype=torch.int32)
+    dist.all_gather([torch.empty_like(flag) for _ in range(world)], flag)
+    return body if rank == 0 else None
+
+
 class DistFrame:
     """Steady-state multi-rank frames on the GPU backend over RCCL (see module doc).
     u8=True: each rank applies FlushFrameBufferToPPM's gamma mapping to its rows
@@ -245,55 +262,133 @@ class DistFrame:
         self._reg = []
 
 
+def _broadcast_bytes(dist, data, nbytes, device, src=0):
+    """`data` (bytes, on rank src) to every rank of `dist` as a uint8 tensor of
+    nbytes (a device tensor unless the backend is gloo)."""
+    import torch
+    t = torch.zeros(nbytes, dtype=torch.uint8)
+    if data is not None:
+        t[:len(data)] = torch.tensor(list(data), dtype=torch.uint8)
+    on_dev = dist.get_backend() != "gloo"
+    u = t.to(device) if on_dev else t
+    dist.broadcast(u, src=src)
+    return bytes((u.cpu() if on_dev else u).tolist())
+
+
+class SharedHostFrames:
+    """R frame bodies of `nbytes` each in ONE host mapping shared by the ranks
+    of this node (NativeRankFrame's shared body): rank 0 creates a /dev/shm
+    file and broadcasts its name over `dist`; every rank maps it; rank 0
+    unlinks it once all have (the mappings stay until close)."""
+
+    def __init__(self, dist, rank, nbytes, R, device=None):
+        import mmap
+        import os
+        import secrets
+        import numpy as np
+        self.span = (nbytes + 4095) // 4096 * 4096
+        size = self.span * R
+        path = None
+        if rank == 0:
+            path = "/dev/shm/rt580-%d-%s" % (os.getpid(), secrets.token_hex(6))
+            fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+            os.ftruncate(fd, size)
+        name = _broadcast_bytes(dist, path.encode() if path else None, 128, device).rstrip(b"\0").decode()
+        if rank != 0:
+            fd = os.open(name, os.O_RDWR)
+        try:
+            self.mm = mmap.mmap(fd, size)
+        finally:
+            os.close(fd)
+        dist.barrier()
+        if rank == 0:
+            os.unlink(name)
+        self.arr = np.frombuffer(self.mm, dtype=np.uint8)
+        self.bufs = [self.arr[k * self.span:(k + 1) * self.span] for k in range(R)]
+
+    def close(self):
+        self.bufs = []
+        self.arr = None
+        if self.mm is not None:
+            try:
+                self.mm.close()
+            except BufferError:  # a caller still holds a view: the mapping goes with it
+                pass
+            self.mm = None
+
+
 class NativeRankFrame:
     """The steady-state multi-rank frame driven by the library (bench.py's
     multi-rank step; rt_gpu_rank_* in include/rt580.h): the library owns the
     world's RCCL communicator (ncclCommInitRank from an id rank 0 makes and
     this class broadcasts over `dist`) and runs the rank's frame loop itself --
-    count, all-gather, shading, the PPM bytes of its rows, the gather to rank 0
-    and rank 0's write of the PPM body into registered host memory -- every
-    collective on one library stream in the same order on every rank, a frame's
-    gather queued by the next frame's call so that two frames' AO phases overlap.
-    No per-frame Python, torch or event work beyond one ctypes call. Rank 0 keeps
-    a ring of R page-locked host frames (frame k lands in buffer k mod R)."""
+    count, all-gather, shading, the PPM bytes of its rows -- every collective on
+    one library stream in the same order on every rank, two frames' AO phases
+    overlapping. No per-frame Python, torch or event work beyond one ctypes call.
+
+    shared (default): the ranks' PPM bodies are ONE host frame per ring entry,
+    shared by the processes (SharedHostFrames; rt_gpu_rank_share_body): every
+    rank writes its own rows into it over its own host link and a frame ends
+    with a 4-byte all-gather. shared=False: rank 0 gathers the u8 row tiles over
+    RCCL and writes the whole body (the form for ranks on different nodes).
+    A ring of R host frames (frame k lands in buffer k mod R)."""
 
     R = 3
     ID_BYTES = 128  # NCCL_UNIQUE_ID_BYTES
 
-    def __init__(self, rt580, params, dist, torch, height, width, rank, world, device, rehearse_gathered=None):
+    def __init__(self, rt580, params, dist, torch, height, width, rank, world, device, rehearse_gathered=None,
+                 shared=True, host_frames=None):
         """rehearse_gathered (dist None): rank `rank` of `world` on this one GPU
         without a communicator, the world's per-row counts given (int32 device
-        tensor [world * n_max]; rt580_rank_rehearse) -- one rank's share timed."""
+        tensor [world * n_max]; rt580_rank_rehearse) -- one rank's share timed.
+        host_frames: the R frame buffers (numpy uint8, page-aligned, >= H*W*3
+        bytes) to write into instead of this class's own (a rehearsal's ranks
+        run one after another into the same frames)."""
         import numpy as np
         self.rt580, self.lib, self.t = rt580, rt580.load(), torch
         self.params = rt580.RenderParams.from_buffer_copy(params)
-        self.h, self.w, self.rank, self.world = height, width, rank, world
+        self.h, self.w, self.rank, self.world, self.shared = height, width, rank, world, shared
         if rehearse_gathered is not None:
             self._gathered = rehearse_gathered
             rt580.check(self.lib.rt580_rank_rehearse(world, rank, rehearse_gathered.data_ptr()), "rt580_rank_rehearse")
         else:
-            uid = torch.zeros(self.ID_BYTES, dtype=torch.uint8)
+            uid = None
             if rank == 0:
-                rt580.check(self.lib.rt_gpu_rank_unique_id(uid.data_ptr(), self.ID_BYTES), "rt_gpu_rank_unique_id")
-            on_dev = dist.get_backend() != "gloo"
-            u = uid.to(device) if on_dev else uid
-            dist.broadcast(u, src=0)
-            uid = u.cpu() if on_dev else u
-            rt580.check(self.lib.rt_gpu_rank_init(uid.data_ptr(), self.ID_BYTES, world, rank), "rt_gpu_rank_init")
-        self._reg = []
-        if rank == 0:
-            span = (height * width * 3 + 4095) // 4096 * 4096
+                u = torch.zeros(self.ID_BYTES, dtype=torch.uint8)
+                rt580.check(self.lib.rt_gpu_rank_unique_id(u.data_ptr(), self.ID_BYTES), "rt_gpu_rank_unique_id")
+                uid = bytes(u.tolist())
+            uid = _broadcast_bytes(dist, uid, self.ID_BYTES, device)
+            ub = (ctypes.c_uint8 * self.ID_BYTES).from_buffer_copy(uid)
+            rt580.check(self.lib.rt_gpu_rank_init(ctypes.addressof(ub), self.ID_BYTES, world, rank), "rt_gpu_rank_init")
+        if shared:
+            rt580.check(self.lib.rt_gpu_rank_share_body(1), "rt_gpu_rank_share_body")
+        self._shm = None
+        self._own = []  # (raw, buf) kept alive
+        body = height * width * 3
+        if host_frames is not None:
+            bufs = list(host_frames)
+        elif shared and world > 1 and dist is not None:
+            self._shm = SharedHostFrames(dist, rank, body, self.R, device)
+            bufs = self._shm.bufs
+        elif shared or rank == 0:
+            span = (body + 4095) // 4096 * 4096
+            bufs = []
             for _ in range(self.R):
                 raw = np.zeros(span + 4096, dtype=np.uint8)
                 off = (-raw.ctypes.data) % 4096
-                buf = raw[off:off + span]
-                rt580.check(self.lib.rt_gpu_host_register(buf.ctypes.data, span), "rt_gpu_host_register")
-                self._reg.append((raw, buf))
+                self._own.append(raw)
+                bufs.append(raw[off:off + span])
+        else:
+            bufs = []
+        self._reg = []
+        for buf in bufs:
+            rt580.check(self.lib.rt_gpu_host_register(buf.ctypes.data, buf.nbytes), "rt_gpu_host_register")
+            self._reg.append(buf)
         self.i = 0
         self.last = None
 
     def render(self):
-        host = self._reg[self.i][1].ctypes.data if self.rank == 0 else None
+        host = self._reg[self.i].ctypes.data if self._reg else None
         self.rt580.check(self.lib.rt_gpu_render_rank_async(ctypes.byref(self.params), host),
                          "rt_gpu_render_rank_async")
         self.last = self.i
@@ -301,7 +396,7 @@ class NativeRankFrame:
 
     def frame(self, k):
         """Rank 0: host buffer k of the ring as an (H, W, 3) uint8 array (after finish())."""
-        return self._reg[k][1][:self.h * self.w * 3].reshape(self.h, self.w, 3)
+        return self._reg[k][:self.h * self.w * 3].reshape(self.h, self.w, 3)
 
     def finish(self):
         """Complete every frame in flight; rank 0: the last frame's PPM body
@@ -313,10 +408,14 @@ class NativeRankFrame:
         return self.t.from_numpy(self.frame(self.last))
 
     def close(self):
-        """The communicator and rank 0's host buffers (every frame complete first)."""
+        """The communicator and the host buffers (every frame complete first)."""
         self.lib.rt_gpu_rank_finish()
         self.lib.rt_gpu_synchronize()
         self.lib.rt_gpu_rank_shutdown()
-        for _, buf in self._reg:
-            self.lib.rt_gpu_host_unregister(buf.ctypes.data)
+        for addr in [b.ctypes.data for b in self._reg]:
+            self.lib.rt_gpu_host_unregister(addr)
         self._reg = []
+        self._own = []
+        if self._shm is not None:
+            self._shm.close()
+            self._shm = None

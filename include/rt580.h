@@ -261,6 +261,13 @@ int rt_gpu_shade_rows_ppm(const rt_render_params* params, const uint64_t* row_ba
 int rt_gpu_rank_unique_id(void* id_out, uint64_t id_bytes);
 int rt_gpu_rank_init(const void* id, uint64_t id_bytes, int world, int rank);
 int rt_gpu_render_rank_async(const rt_render_params* params, uint8_t* ppm_body_host);
+/* Shared body (on != 0; after rt_gpu_rank_init / rt580_rank_rehearse, before
+ * the first frame): every rank passes ppm_body_host, its own registered mapping
+ * of ONE host frame shared by the ranks' processes (e.g. a /dev/shm file), and
+ * writes its rows' PPM bytes straight to their places in it; a frame's gather
+ * is then a 4-byte all-gather after every rank's write (no tiles to rank 0).
+ * With one rank there is no exchange. */
+int rt_gpu_rank_share_body(int on);
 int rt_gpu_rank_finish(void);
 int rt_gpu_rank_shutdown(void);
 /* Bench/test hook: rank `rank` of `world` rehearsed on this one GPU without a

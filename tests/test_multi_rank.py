@@ -57,6 +57,44 @@ def _worker_steady(rank, world, port, out_path, u8):
         dist.destroy_process_group()
 
 
+def _worker_shared(rank, world, port, out_path):
+    """The shared-body exchange (NativeRankFrame's default): the ranks map ONE
+    /dev/shm frame (SharedHostFrames), each writes its own rows' PPM bytes into
+    it, three frames over the ring."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dm = helpers.rt580_dist()
+    try:
+        scene, w, h, depth, ao = CASE
+        backend = helpers.OracleRows(scene, w, h, depth, ao)
+        frames = dm.SharedHostFrames(dist, rank, h * w * 3, 3)
+        lut = helpers.rt580().gamma_lut()
+        for k in range(3):
+            body = frames.bufs[k][:h * w * 3].reshape(h, w, 3)
+            got = dm.render_frame_shared(backend, dist, torch, h, w, rank, world, body, lut)
+        if rank == 0:
+            np.save(out_path, np.stack([frames.bufs[k][:h * w * 3].copy() for k in range(3)]))
+        del body, got
+        dist.barrier()
+        frames.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shared_host_frame_rows(world, tmp_path):
+    out = str(tmp_path / "frames.npy")
+    mp.start_processes(_worker_shared, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    scene, w, h, depth, ao = CASE
+    ref, _ = helpers.oracle_render(scene, w, h, depth, ao, True)
+    want = helpers.rt580().ppm_bytes(ref).split(b"\n", 3)[3]
+    for k, f in enumerate(np.load(out)):
+        assert f.tobytes() == want, "ring frame %d" % k
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("rt580-")]  # rank 0 unlinked the file
+
+
 @pytest.mark.parametrize("world,u8", [(2, False), (3, False), (2, True), (3, True)])
 def test_steady_state_dist_frame(world, u8, tmp_path):
     out = str(tmp_path / "frame.npy")
