@@ -275,6 +275,16 @@ def _broadcast_bytes(dist, data, nbytes, device, src=0):
     return bytes((u.cpu() if on_dev else u).tolist())
 
 
+def _all_ranks(dist, ok, device):
+    """True when every rank of `dist` passes ok = 1."""
+    import torch
+    t = torch.tensor([int(ok)], dtype=torch.int32)
+    on_dev = dist.get_backend() != "gloo"
+    u = t.to(device) if on_dev else t
+    dist.all_reduce(u, op=dist.ReduceOp.MIN)
+    return int(u.item()) == 1
+
+
 class SharedHostFrames:
     """R frame bodies of `nbytes` each in ONE host mapping shared by the ranks
     of this node (NativeRankFrame's shared body): rank 0 creates a /dev/shm
@@ -288,12 +298,26 @@ class SharedHostFrames:
         import numpy as np
         self.span = (nbytes + 4095) // 4096 * 4096
         size = self.span * R
+        self.mm = None
         path = None
         if rank == 0:
+            # the pages reserved now (a small tmpfs -- a container's 64 MB
+            # /dev/shm -- fails here, not with SIGBUS at a write); "" = none
             path = "/dev/shm/rt580-%d-%s" % (os.getpid(), secrets.token_hex(6))
-            fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
-            os.ftruncate(fd, size)
-        name = _broadcast_bytes(dist, path.encode() if path else None, 128, device).rstrip(b"\0").decode()
+            try:
+                fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+                try:
+                    os.posix_fallocate(fd, 0, size)
+                except OSError:
+                    os.close(fd)
+                    os.unlink(path)
+                    raise
+            except OSError:
+                path = ""
+        name = _broadcast_bytes(dist, path.encode() if path is not None else None, 128,
+                                device).rstrip(b"\0").decode()
+        if not name:
+            raise OSError("SharedHostFrames: no room for %d bytes in /dev/shm" % size)
         if rank != 0:
             fd = os.open(name, os.O_RDWR)
         try:
@@ -363,14 +387,29 @@ class NativeRankFrame:
         if shared:
             rt580.check(self.lib.rt_gpu_rank_share_body(1), "rt_gpu_rank_share_body")
         self._shm = None
-        self._own = []  # (raw, buf) kept alive
+        self._own = []  # private page-aligned buffers kept alive
+        self._reg = []
         body = height * width * 3
         if host_frames is not None:
-            bufs = list(host_frames)
+            self._register(list(host_frames))
         elif shared and world > 1 and dist is not None:
-            self._shm = SharedHostFrames(dist, rank, body, self.R, device)
-            bufs = self._shm.bufs
-        elif shared or rank == 0:
+            # every rank maps and registers the shared ring, or (any failing)
+            # all fall back to the gather form together: the two forms differ
+            # in their collectives
+            ok = 1
+            try:
+                self._shm = SharedHostFrames(dist, rank, body, self.R, device)
+                self._register(self._shm.bufs)
+            except (OSError, RuntimeError):
+                ok = 0
+            if not _all_ranks(dist, ok, device):
+                self._unregister()
+                if self._shm is not None:
+                    self._shm.close()
+                    self._shm = None
+                rt580.check(self.lib.rt_gpu_rank_share_body(0), "rt_gpu_rank_share_body")
+                self.shared = False
+        if not self._reg and (self.shared or rank == 0):
             span = (body + 4095) // 4096 * 4096
             bufs = []
             for _ in range(self.R):
@@ -378,14 +417,19 @@ class NativeRankFrame:
                 off = (-raw.ctypes.data) % 4096
                 self._own.append(raw)
                 bufs.append(raw[off:off + span])
-        else:
-            bufs = []
-        self._reg = []
-        for buf in bufs:
-            rt580.check(self.lib.rt_gpu_host_register(buf.ctypes.data, buf.nbytes), "rt_gpu_host_register")
-            self._reg.append(buf)
+            self._register(bufs)
         self.i = 0
         self.last = None
+
+    def _register(self, bufs):
+        for buf in bufs:
+            self.rt580.check(self.lib.rt_gpu_host_register(buf.ctypes.data, buf.nbytes), "rt_gpu_host_register")
+            self._reg.append(buf)
+
+    def _unregister(self):
+        for addr in [b.ctypes.data for b in self._reg]:
+            self.lib.rt_gpu_host_unregister(addr)
+        self._reg = []
 
     def render(self):
         host = self._reg[self.i].ctypes.data if self._reg else None
@@ -412,9 +456,7 @@ class NativeRankFrame:
         self.lib.rt_gpu_rank_finish()
         self.lib.rt_gpu_synchronize()
         self.lib.rt_gpu_rank_shutdown()
-        for addr in [b.ctypes.data for b in self._reg]:
-            self.lib.rt_gpu_host_unregister(addr)
-        self._reg = []
+        self._unregister()
         self._own = []
         if self._shm is not None:
             self._shm.close()

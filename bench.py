@@ -27,7 +27,8 @@ Parallel modes (the row split of SURVEY §8e, byte-identical frames for every N)
     instead of RCCL) to rehearse it on a one-GPU box.
   * under torch.distributed.run: one process per GPU (rt580_dist.NativeRankFrame:
     the library's rank loop, rt_gpu_render_rank_async -- RCCL all-gather of the
-    counts, the u8 tiles gathered to rank 0, frames in flight; --backend gloo:
+    counts, each rank's rows written into one shared host frame, frames in
+    flight; --backend gloo:
     rt580_dist.DistFrame over torch.distributed). --gpus must equal WORLD_SIZE.
 
 Rank 0 prints ONE JSON line on stdout: metric, value = whole-job Mrays/s,
@@ -354,9 +355,13 @@ def run_workload(ctx, name, steps, warmup, cpu_baseline_on, check):
                  "three frames in flight (each frame's gather and D2H overlap the next frames' kernels)"
                  % ("rt_gpu_render_multi_async (tiles mapped to bytes on their devices, gathered and de-interleaved "
                     "on device 0)" if ctx.multi else "rt_gpu_render_async_ppm", RING) if not ctx.dist_on else
-                 "one frame on every rank; rank 0 gathers the u8 tiles and writes the PPM body into page-locked host "
-                 "memory (rt580_dist.NativeRankFrame: the library's own rank loop, rt_gpu_render_rank_async -- "
-                 "count, RCCL all-gather, shading, the previous frame's gather, on one communicator)"),
+                 "one frame on every rank; %s (rt580_dist.NativeRankFrame: the library's own rank loop, "
+                 "rt_gpu_render_rank_async -- count, RCCL all-gather, shading, the frame's end, on one "
+                 "communicator)" % ("every rank writes its rows' PPM bytes into one page-locked host frame shared "
+                                    "by the processes (/dev/shm), a 4-byte all-gather ends the frame"
+                                    if dframe is not None and dframe.shared else
+                                    "rank 0 gathers the u8 tiles and writes the PPM body into page-locked host "
+                                    "memory")),
         "step_kind": step_kind,
         "scene_upload_s": round(upload_s, 3),
         "host_enqueue_ms_per_step": round(host_s / steps * 1e3, 4),

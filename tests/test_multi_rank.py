@@ -95,6 +95,37 @@ def test_shared_host_frame_rows(world, tmp_path):
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("rt580-")]  # rank 0 unlinked the file
 
 
+def _worker_shm_full(rank, world, port, out_path):
+    """/dev/shm without room on rank 0 (posix_fallocate fails): every rank
+    gets the same OSError (NativeRankFrame then falls back to the gather)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if rank == 0:
+            def full(fd, off, n):
+                raise OSError(28, "No space left on device")
+            os.posix_fallocate = full
+        try:
+            helpers.rt580_dist().SharedHostFrames(dist, rank, 1 << 20, 3)
+            raised = False
+        except OSError:
+            raised = True
+        flags = [torch.zeros(1, dtype=torch.int32) for _ in range(world)]
+        dist.all_gather(flags, torch.tensor([int(raised)], dtype=torch.int32))
+        if rank == 0:
+            np.save(out_path, torch.cat(flags).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shared_host_frame_without_room_fails_on_every_rank(tmp_path):
+    out = str(tmp_path / "flags.npy")
+    mp.start_processes(_worker_shm_full, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    assert np.load(out).tolist() == [1, 1]
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("rt580-")]
+
+
 @pytest.mark.parametrize("world,u8", [(2, False), (3, False), (2, True), (3, True)])
 def test_steady_state_dist_frame(world, u8, tmp_path):
     out = str(tmp_path / "frame.npy")
