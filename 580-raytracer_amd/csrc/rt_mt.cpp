@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <random>
 #include <thread>
 
@@ -173,7 +174,8 @@ MtWindow horner_apply(const Poly& h, const MtWindow& w) {
 }
 
 struct Cache {
-    std::vector<MtWindow> w;  // W_{k kMtBlock}, k = 0, 1, ...
+    uint64_t k0 = 0;          // block index of w[0]
+    std::vector<MtWindow> w;  // W_{(k0 + i) kMtBlock}, i = 0, 1, ...
 };
 
 }  // namespace
@@ -202,36 +204,50 @@ void mt_draws(const MtWindow& w, uint64_t count, uint32_t* out) {
     }
 }
 
-const MtWindow* mt_checkpoints(uint32_t seed, uint64_t k0, uint64_t k1) {
+bool mt_checkpoints(uint32_t seed, uint64_t k0, uint64_t k1, std::vector<MtWindow>& out) {
+    out.clear();
+    if (k1 < k0) return false;
+    // Berlekamp-Massey found no degree-19937 polynomial (cannot happen for the
+    // engine; a wrong phi would make reduce() loop forever): report, not hang
+    if (phi().empty()) return false;
+    static std::mutex mu;
     static std::map<uint32_t, Cache> caches;
+    std::lock_guard<std::mutex> lock(mu);
     Cache& c = caches[seed];
-    if (c.w.empty()) c.w.push_back(mt_seed_window(seed));
-    const uint64_t have = c.w.size();
+    // a request that does not start inside (or right after) the cached run
+    // starts a new run with ONE jump to k0 (not every window from 0)
+    if (c.w.empty() || k0 < c.k0 || k0 > c.k0 + c.w.size()) {
+        c.k0 = k0;
+        c.w.assign(1, mt_jump(mt_seed_window(seed), k0 * kMtBlock));
+    }
+    const uint64_t have = c.k0 + c.w.size();  // absolute block index one past the run
     if (k1 > have) {
         static const Poly hb = x_pow_mod(kMtBlock - 1);  // one block: W -> A hb(A) W
-        c.w.resize((size_t)k1);
+        c.w.resize((size_t)(k1 - c.k0));
         const uint64_t todo = k1 - have;
         // threads: the host's share ($OMP_NUM_THREADS on the GPU pool), at most 16
         unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::max(1, std::atoi(e));
         const unsigned nt = (unsigned)std::min<uint64_t>(std::min(hw, 16u), todo);
+        const MtWindow last = c.w[(size_t)(have - 1 - c.k0)];
         std::vector<std::thread> th;
         for (unsigned t = 0; t < nt; t++)
             th.emplace_back([&, t] {
                 const uint64_t a = have + todo * t / nt, b = have + todo * (t + 1) / nt;
                 if (a >= b) return;
-                // a thread's first window by one long jump from the last cached one,
-                // then block by block
-                MtWindow cur = mt_jump(c.w[(size_t)have - 1], (a - (have - 1)) * kMtBlock);
-                c.w[(size_t)a] = cur;
+                // a thread's first window by one long jump from the run's last
+                // window, then block by block
+                MtWindow cur = mt_jump(last, (a - (have - 1)) * kMtBlock);
+                c.w[(size_t)(a - c.k0)] = cur;
                 for (uint64_t k = a + 1; k < b; k++) {
                     cur = horner_apply(hb, cur);
-                    c.w[(size_t)k] = cur;
+                    c.w[(size_t)(k - c.k0)] = cur;
                 }
             });
         for (auto& x : th) x.join();
     }
-    return c.w.data() + k0;
+    out.assign(c.w.begin() + (ptrdiff_t)(k0 - c.k0), c.w.begin() + (ptrdiff_t)(k1 - c.k0));
+    return true;
 }
 
 }  // namespace rt580

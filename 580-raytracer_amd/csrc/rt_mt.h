@@ -34,10 +34,12 @@ MtWindow mt_seed_window(uint32_t seed);
 // W_{n+J} from W_n (J >= 0). Cost: one polynomial x^(J-1) mod phi (~36 modular
 // squarings for J ~ 2^36) and one Horner evaluation (~19937 twist steps).
 MtWindow mt_jump(const MtWindow& w, uint64_t J);
-// The windows W_{k kMtBlock} for k in [k0, k1) of the stream of `seed`,
-// process-wide cache (computed on demand, in parallel, kept for later frames).
-// Returns a pointer to k1 - k0 consecutive windows, valid until the next call.
-const MtWindow* mt_checkpoints(uint32_t seed, uint64_t k0, uint64_t k1);
+// The windows W_{k kMtBlock} for k in [k0, k1) of the stream of `seed`, copied
+// into `out`, from a process-wide cache (one run of consecutive windows per
+// seed, under a lock: computed on demand in parallel from one jump to its
+// first window, extended or restarted by later calls). False if the engine's
+// polynomial could not be found.
+bool mt_checkpoints(uint32_t seed, uint64_t k0, uint64_t k1, std::vector<MtWindow>& out);
 // Host reference: draws [n, n + count) from W_n by the twist (tests).
 void mt_draws(const MtWindow& w, uint64_t count, uint32_t* out);
 

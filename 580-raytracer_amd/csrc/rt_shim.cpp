@@ -896,7 +896,8 @@ int trace_rows(const rt_render_params* p, int row_begin, int row_step, int n_row
 // (rt_mt.h block jump-ahead, cached per seed for later frames), one workgroup
 // per block runs the twist (launch_mt_generate). Draws are addressed by
 // absolute index minus the window's base.
-constexpr uint64_t kMtMaxWindow = 1ull << 34;  // draws held at once (64 GiB of the 288 GB)
+constexpr uint64_t kMtMaxWindow = 1ull << 34;  // draws held at once per device (64 GiB of the 288 GB),
+                                                // split over its frame slots
 
 int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global, int n_rows) {
     if (p->rng_engine != RT_RNG_MT19937 || !p->ao_enabled || g.n_ambient == 0) return RT_SUCCESS;
@@ -919,18 +920,21 @@ int prepare_mt_stream(const rt_render_params* p, const uint64_t* row_base_global
     }
     const uint64_t per_call = 2ull * (uint64_t)p->ao_samples;
     const uint64_t lo = lo_call * per_call, hi = hi_call * per_call;
-    if (hi - lo > kMtMaxWindow)
-        return fail("mt19937: these rows need draws [%llu, %llu), more than the %llu one window holds (use "
-                    "minstd_rand0, or fewer rows per call)",
-                    (unsigned long long)lo, (unsigned long long)hi, (unsigned long long)kMtMaxWindow);
+    const uint64_t max_window = kMtMaxWindow / (uint64_t)(g.nslots > 0 ? g.nslots : 1);
+    if (hi - lo > max_window)
+        return fail("mt19937: these rows need draws [%llu, %llu), more than the %llu a frame slot's window holds "
+                    "(use minstd_rand0, or fewer rows per call)",
+                    (unsigned long long)lo, (unsigned long long)hi, (unsigned long long)max_window);
     SL.mt_base = lo;
     if (hi == lo) return RT_SUCCESS;
     const uint64_t k0 = lo / kMtBlock, k1 = (hi + kMtBlock - 1) / kMtBlock;
     const uint32_t nblk = (uint32_t)(k1 - k0);
     if (ensure(SL.mt_stream, (hi - lo) * 4 + 8) || ensure(SL.mt_windows, (size_t)nblk * sizeof(MtWindow)))
         return RT_FAILURE;
-    const MtWindow* cps = mt_checkpoints(p->rng_seed, k0, k1);
-    if (copy_h2d(SL.mt_windows.p, cps, (size_t)nblk * sizeof(MtWindow), fs(), "the mt19937 checkpoint windows"))
+    std::vector<MtWindow> cps;
+    if (!mt_checkpoints(p->rng_seed, k0, k1, cps))
+        return fail("mt19937: the engine's characteristic polynomial could not be found (jump-ahead unavailable)");
+    if (copy_h2d(SL.mt_windows.p, cps.data(), (size_t)nblk * sizeof(MtWindow), fs(), "the mt19937 checkpoint windows"))
         return RT_FAILURE;
     HIP_TRY(launch_mt_generate((const uint32_t*)SL.mt_windows.p, k0, nblk, lo, hi, (uint32_t*)SL.mt_stream.p, fs()));
     return RT_SUCCESS;

@@ -44,7 +44,23 @@ int main(int argc, char** argv) {
     const double t_check = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     // checkpoints k kMtBlock against direct jumps, and split jumps far out
     t0 = std::chrono::steady_clock::now();
-    const MtWindow* cp = mt_checkpoints(5489u, 0, 40);
+    std::vector<MtWindow> cpv;
+    if (!mt_checkpoints(5489u, 0, 40, cpv)) return 1;
+    const MtWindow* cp = cpv.data();
+    // a run started far out (one jump to k0), then extended, then a request
+    // before it (a new run): the same windows as direct jumps
+    std::vector<MtWindow> far_run, ext, back;
+    if (!mt_checkpoints(5489u, 5000, 5003, far_run) || !mt_checkpoints(5489u, 5002, 5006, ext) ||
+        !mt_checkpoints(5489u, 3, 5, back))
+        return 1;
+    for (auto [k, w] : {std::pair<uint64_t, const MtWindow*>{5000, &far_run[0]}, {5002, &far_run[2]},
+                        {5005, &ext[3]}, {3, &back[0]}, {4, &back[1]}}) {
+        const MtWindow d = mt_jump(mt_seed_window(5489u), k * kMtBlock);
+        if (std::memcmp(&d, w, sizeof d) != 0) {
+            std::printf("checkpoint %llu (cached run) differs from the direct jump\n", (unsigned long long)k);
+            bad++;
+        }
+    }
     const double t_cp = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     const MtWindow w0 = mt_seed_window(5489u);
     for (uint64_t k : {0ull, 1ull, 17ull, 39ull}) {
