@@ -3513,6 +3513,7 @@ hipError_t launch_trace(const DevScene& S, const DevFrame& F, const DevWork& W, 
                         uint32_t sq = 0, sb = 0;
                         if ((e = sort_far_queue(S, W, s, sq, sb, /*one_dir=*/true)) != hipSuccess) return e;
                         uint8_t* flags = W.shadow + (size_t)dl * W.far_cap;
+                        progress("trace level %d shadow light %d: far queue %u (brute %u)", level, dl, sq, sb);
                         if (sb) {
                             RT_STEP("trace shadow brute scan");
                             if ((e = launch_brute_any(S, W, sq - sb, sb, flags, s)) != hipSuccess) return e;
