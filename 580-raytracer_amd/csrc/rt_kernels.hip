@@ -2013,7 +2013,7 @@ far_cell_any_kernel(DevScene S, DevWork W, uint32_t n, uint8_t* flag) {
                     for (uint32_t j0 = 0; j0 < nr; j0 += step) {
                         const uint32_t j = j0 + (uint32_t)g;
                         bool fc = false;
-                        if (has && j < nr && shit[wave][j] == 0u) {
+                        if (has && j < nr && !((hitm >> j) & 1u)) {  // (rays hit so far: hitm, refreshed after each batch)
                             const float4 aj = sray[wave][j][0], bj = sray[wave][j][1];
                             FarRay fj;
                             fj.R = bj.w;
