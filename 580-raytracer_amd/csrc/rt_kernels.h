@@ -118,7 +118,8 @@ struct DevWork {
     size_t sort_tmp_bytes;
     uint32_t far_cap;
     // split AO pass (ao_trace_kernel): (o.xyz, call), (d.xyz, flag) per item of a chunk
-    float4* ao_rays;       // [2 * ao_cap] or null
+    float4* ao_rays;       // [ao_cap] 16-byte AO ray records of a chunk (ao_record) or null
+    float4* ao_hp;         // [ao_cap + 2]: the hit point of each call of the chunk (after ao_rays)
     uint32_t ao_cap;
     // AO rays of a chunk whose near traversal ran out of its step budget in
     // ao_trace_kernel (item index in the chunk), finished by ao_late_kernel

@@ -960,9 +960,12 @@ __device__ __forceinline__ void ao_finish(const DevScene& S, const DevWork& W, u
 template <int VARIANT>
 __device__ __forceinline__ void ao_sample(const DevScene& S, const DevFrame& F, const DevWork& W, const double* sct,
                                           uint32_t N, bool pow2, int log2n, bool wave_per_call, uint64_t item,
-                                          bool active, uint64_t& c, rv3& o, rv3& d, bool& ao_brute, bool& fix) {
+                                          bool active, uint64_t& c, rv3& o, rv3& d, bool& ao_brute, bool& fix,
+                                          rv3& vo, rv3& hpo, uint32_t& so) {
     c = 0;
     uint32_t s = 0;
+    vo = v3(0, 0, 0);
+    hpo = v3(0, 0, 0);
     if (active) {
         if (pow2) { c = item >> log2n; s = (uint32_t)(item & (N - 1)); }
         else { c = item / N; s = (uint32_t)(item - c * N); }
@@ -1024,7 +1027,10 @@ __device__ __forceinline__ void ao_sample(const DevScene& S, const DevFrame& F, 
         // Ray constructor (Raytracer.h:431-433)
         d = (VARIANT & 2048) ? v3_normalize_unit(v) : v3_normalize(v);
         if ((VARIANT & 512) && S.bv.has_far) ao_brute = far_origin(S, o);
+        vo = v;
+        hpo = hp;
     }
+    so = s;
 }
 
 template <int VARIANT>
@@ -1053,13 +1059,14 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
     for (uint64_t b0 = item_begin + (uint64_t)blockIdx.x * TB * SPL; b0 < items; b0 += (uint64_t)gridDim.x * TB * SPL) {
         bool active[SPL], ao_brute[SPL], fix[SPL], hit[SPL];
         uint64_t c[SPL];
-        rv3 o[SPL], d[SPL];
+        rv3 o[SPL], d[SPL], vv[SPL], hh[SPL];
+        uint32_t ss[SPL];
 #pragma unroll
         for (int k = 0; k < SPL; k++) {
             const uint64_t item = b0 + (uint64_t)k * TB + threadIdx.x;
             active[k] = item < items;
             ao_sample<VARIANT>(S, F, W, sct, N, pow2, log2n, wave_per_call, item, active[k], c[k], o[k], d[k],
-                               ao_brute[k], fix[k]);
+                               ao_brute[k], fix[k], vv[k], hh[k], ss[k]);
         }
 #pragma unroll
         for (int k = 0; k < SPL; k++) {
@@ -1080,13 +1087,17 @@ __device__ __forceinline__ void ao_body(const DevScene& S, const DevFrame& F, co
                 }
             }
             if (VARIANT & 16384) {
-                // generation only: the ray record for ao_trace_kernel (flag 0: no ray,
-                // 1: near query, 2: far origin)
+                // generation only: the 16-byte ray record for ao_trace_kernel -- the
+                // sample's hemisphere vector v and (call - the chunk's first call) |
+                // flag << 30 (0: no ray, 1: near query, 2: far origin) -- and the
+                // call's hit point once per call (ao_record rebuilds o and d)
                 if (item < items) {
+                    const uint64_t c0 = item_begin / N;
                     const uint32_t flag = active[k] ? (ao_brute[k] ? 2u : 1u) : 0u;
-                    float4* r = W.ao_rays + 2 * (size_t)(item - item_begin);
-                    r[0] = make_float4(o[k].x, o[k].y, o[k].z, __uint_as_float((uint32_t)c[k]));
-                    r[1] = make_float4(d[k].x, d[k].y, d[k].z, __uint_as_float(flag));
+                    W.ao_rays[item - item_begin] =
+                        make_float4(vv[k].x, vv[k].y, vv[k].z, __uint_as_float((uint32_t)(c[k] - c0) | (flag << 30)));
+                    if (ss[k] == 0u || item == item_begin)
+                        W.ao_hp[c[k] - c0] = make_float4(hh[k].x, hh[k].y, hh[k].z, 0.0f);
                 }
             }
         }
@@ -1329,6 +1340,26 @@ __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const 
     return bvh4_any_spec_walk<HOLD2, BOUND>(V, o, d, stk, budget, live, sp, c, n, tmax);
 }
 
+// The AO ray of a 16-byte record of the generation pass (ao_body, VARIANT &
+// 16384): origin hp + 0.2 v and direction normalize(v) by the generation's own
+// float operations (CalculateAmbientOcclusion, Raytracer.cpp:323-326; the Ray
+// constructor, Raytracer.h:431-433), so (o, d) are the bits the generation
+// computed; c = the call. Returns the flag (0: no ray, 1: near query, 2: far
+// origin). c0: the chunk's first call (its first item / N).
+__device__ __forceinline__ uint32_t ao_record(const DevWork& W, float4 r, uint64_t c0, rv3& o, rv3& d, uint64_t& c) {
+    const uint32_t w = __float_as_uint(r.w), rel = w & 0x3fffffffu, flag = w >> 30;
+    c = c0 + rel;
+    o = v3(0, 0, 0);
+    d = v3(0, 0, 0);
+    if (flag) {
+        const float4 h = W.ao_hp[rel];
+        const rv3 v = v3(r.x, r.y, r.z);
+        o = v3_add(v3(h.x, h.y, h.z), v3_scale(v, 0.2f));
+        d = v3_normalize_unit(v);
+    }
+    return flag;
+}
+
 // Split AO pass of BVH scenes: ao_near_kernel_w<.., V | 16384> writes each
 // item's ray (W.ao_rays); this kernel runs the near any-hit query over the
 // 4-wide tree with nothing else live, then ao_finish. Rays [0, n) of the chunk.
@@ -1345,7 +1376,7 @@ __device__ int bvh4_any_spec_budget_state(const BvhView& V, rv3 o, rv3 d, const 
 // The walk is in speculative while-while form (bvh4_any_spec_budget_state).
 template <int WPE, int LDS_D, int SORT, int KL, int BUDGET>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
-ao_trace_kernel(DevScene S, DevWork W, uint64_t n) {
+ao_trace_kernel(DevScene S, DevWork W, uint64_t n, uint64_t c0) {
     static_assert(LDS_D > 0 && SORT > 0 && BUDGET > 0, "LDS stack, block sort, step budget");
     if (frame_poisoned(W)) return;
     __shared__ uint32_t lstk[LDS_D][TB];
@@ -1365,10 +1396,10 @@ ao_trace_kernel(DevScene S, DevWork W, uint64_t n) {
 #pragma unroll
             for (int q = 0; q < SORT; q++) {
                 const uint64_t j = blk + (uint64_t)q * TB + threadIdx.x;
-                key[q] = NB;  // past the end: last
+                key[q] = NB;  // past the end (or no ray): last
                 if (j < n) {
-                    const float4 r1 = W.ao_rays[2 * j + 1];
-                    key[q] = grid_cell(v3(r1.x, r1.y, r1.z), KL);
+                    const float4 r = W.ao_rays[j];  // grouping only: v's cell (d = normalize(v))
+                    if (__float_as_uint(r.w) >> 30) key[q] = grid_cell(v3(r.x, r.y, r.z), KL);
                 }
                 atomicAdd(&s_bin[key[q]], 1u);
             }
@@ -1409,14 +1440,10 @@ ao_trace_kernel(DevScene S, DevWork W, uint64_t n) {
             __syncthreads();
         }
         const uint64_t i = blk + s_order[round * TB + threadIdx.x];
-        float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
-        if (i < n) {
-            r0 = W.ao_rays[2 * i];
-            r1 = W.ao_rays[2 * i + 1];
-        }
-        const uint32_t flag = __float_as_uint(r1.w);
+        rv3 o, d;
+        uint64_t call = 0;
+        const uint32_t flag = ao_record(W, i < n ? W.ao_rays[i] : make_float4(0, 0, 0, 0), c0, o, d, call);
         const bool active = flag != 0u, ao_brute = flag == 2u;
-        const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
         uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
         const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
         int sp = 0;
@@ -1442,7 +1469,7 @@ ao_trace_kernel(DevScene S, DevWork W, uint64_t n) {
             }
         }
         // sorted: a wave's lanes are no longer one call's samples
-        ao_finish<true>(S, W, 1u, active && !late, ao_brute, hit, (uint64_t)__float_as_uint(r0.w), o, d);
+        ao_finish<true>(S, W, 1u, active && !late, ao_brute, hit, call, o, d);
     }
 }
 
@@ -1459,7 +1486,7 @@ ao_trace_kernel(DevScene S, DevWork W, uint64_t n) {
 // answer it computed was right ("The 8-wave late-pass defect").
 template <int WPE, int LDS_D>
 __global__ void __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(WPE)))
-ao_late_kernel(DevScene S, DevWork W) {
+ao_late_kernel(DevScene S, DevWork W, uint64_t c0) {
     if (frame_poisoned(W)) return;
     __shared__ uint32_t lstk[LDS_D][TB];
     const uint32_t cnt = W.ao_late_count[0];
@@ -1467,13 +1494,14 @@ ao_late_kernel(DevScene S, DevWork W) {
         const uint32_t k = b0 + threadIdx.x;
         const bool live = k < cnt;
         uint32_t i = 0;
-        float4 r0 = make_float4(0, 0, 0, 0), r1 = make_float4(0, 0, 0, 0);
+        float4 r = make_float4(0, 0, 0, 0);
         if (live) {
             i = W.ao_late[k];
-            r0 = W.ao_rays[2 * (size_t)i];
-            r1 = W.ao_rays[2 * (size_t)i + 1];
+            r = W.ao_rays[i];
         }
-        const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
+        rv3 o, d;
+        uint64_t call = 0;
+        (void)ao_record(W, r, c0, o, d, call);
         uint32_t stk_a[RT_BVH_STACK + 4 - LDS_D];
         const LdsStack<LDS_D, TB> stk{&lstk[0][threadIdx.x], stk_a};
         // the walk ao_trace_kernel saved for this ray
@@ -1499,12 +1527,12 @@ ao_late_kernel(DevScene S, DevWork W) {
         }
         const bool hit = pre || bvh4_any_spec_walk<0>(S.bv, o, d, stk, 1 << 30, go, sp, wc, wn) > 0;
         if (live) {
-            const volatile float4* rv = W.ao_rays + 2 * (size_t)i;
-            r0 = make_float4(rv[0].x, rv[0].y, rv[0].z, rv[0].w);
-            r1 = make_float4(rv[1].x, rv[1].y, rv[1].z, rv[1].w);
+            const volatile float4* rv = W.ao_rays + i;
+            r = make_float4(rv->x, rv->y, rv->z, rv->w);
         }
-        ao_finish<true>(S, W, 1u, live, false, hit, (uint64_t)__float_as_uint(r0.w), v3(r0.x, r0.y, r0.z),
-                        v3(r1.x, r1.y, r1.z));
+        rv3 o2, d2;
+        (void)ao_record(W, r, c0, o2, d2, call);
+        ao_finish<true>(S, W, 1u, live, false, hit, call, o2, d2);
     }
 }
 
@@ -1553,11 +1581,11 @@ __global__ void __launch_bounds__(TB) ao_audit_expect_kernel(DevScene S, DevWork
                                                              unsigned long long* out) {
     if (frame_poisoned(W)) return;
     for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TB) {
-        const float4 r0 = W.ao_rays[2 * i], r1 = W.ao_rays[2 * i + 1];
-        const uint32_t flag = __float_as_uint(r1.w);
+        rv3 o, d;
+        uint64_t c64 = 0;
+        const uint32_t flag = ao_record(W, W.ao_rays[i], c_lo, o, d, c64);
         if (flag == 0u) continue;
-        const rv3 o = v3(r0.x, r0.y, r0.z), d = v3(r1.x, r1.y, r1.z);
-        const uint32_t c = __float_as_uint(r0.w);
+        const uint32_t c = (uint32_t)c64;
         const bool hit = flag == 1u && bvh4_any_near(S.bv, o, d);
         if (flag == 1u) atomicAdd(&out[0], 1ull);
         if (hit) {
@@ -1566,7 +1594,8 @@ __global__ void __launch_bounds__(TB) ao_audit_expect_kernel(DevScene S, DevWork
         } else if (S.bv.has_far && (flag == 2u || far_live(S.bv, o, d))) {
             const uint32_t key = flag == 2u ? RT_KEY_BRUTE : far_key(S.bv, o, d);
             atomicAdd(&aud[0], 1ull);
-            atomicAdd(&aud[1], audit_mix(make_float4(o.x, o.y, o.z, r0.w), make_float4(d.x, d.y, d.z, INFINITY), key));
+            atomicAdd(&aud[1], audit_mix(make_float4(o.x, o.y, o.z, __uint_as_float(c)), make_float4(d.x, d.y, d.z, INFINITY),
+                                         key));
         }
     }
 }
@@ -1605,7 +1634,11 @@ __global__ void __launch_bounds__(TB) ao_audit_compare_kernel(DevScene S, DevWor
             const int64_t j0 = (int64_t)c * N - (int64_t)item0, j1 = j0 + N;
             why = 2u;
             for (int64_t j = j0 < 0 ? 0 : j0; j < j1 && j < (int64_t)n; j++) {
-                const float4 r0 = W.ao_rays[2 * j], r1 = W.ao_rays[2 * j + 1];
+                rv3 oj, dj;
+                uint64_t cj = 0;
+                const uint32_t flag = ao_record(W, W.ao_rays[j], c_lo, oj, dj, cj);
+                const float4 r0 = make_float4(oj.x, oj.y, oj.z, __uint_as_float((uint32_t)cj)),
+                             r1 = make_float4(dj.x, dj.y, dj.z, __uint_as_float(flag));
                 if (why == 2u && a.x != a.z && __float_as_uint(r0.z) == __float_as_uint(a.x) &&
                     __float_as_uint(r0.y) == __float_as_uint(a.y) && __float_as_uint(r0.x) == __float_as_uint(a.z))
                     why = 16u;  // a sample of the call has this origin with x and z exchanged
@@ -1621,7 +1654,6 @@ __global__ void __launch_bounds__(TB) ao_audit_compare_kernel(DevScene S, DevWor
                                    __float_as_uint(r1.y) == __float_as_uint(b.y) &&
                                    __float_as_uint(r1.z) == __float_as_uint(b.z);
                 if (!dsame) { why = 4u; continue; }
-                const uint32_t flag = __float_as_uint(r1.w);
                 const uint32_t want = flag == 2u ? RT_KEY_BRUTE : far_key(S.bv, v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z));
                 why = want == key ? 0u : 8u;
                 if (!why) break;
@@ -1633,8 +1665,11 @@ __global__ void __launch_bounds__(TB) ao_audit_compare_kernel(DevScene S, DevWor
             const unsigned long long k = atomicAdd(&out[25], 1ull);
             if (k < 2) {  // the entry and the ray it was matched with (or none)
                 unsigned long long* d = out + 26 + 18 * k;
-                const float4 r0 = found >= 0 ? W.ao_rays[2 * found] : make_float4(0, 0, 0, 0);
-                const float4 r1 = found >= 0 ? W.ao_rays[2 * found + 1] : make_float4(0, 0, 0, 0);
+                rv3 of = v3(0, 0, 0), df = v3(0, 0, 0);
+                uint64_t cf = 0;
+                const uint32_t ff = found >= 0 ? ao_record(W, W.ao_rays[found], c_lo, of, df, cf) : 0u;
+                const float4 r0 = make_float4(of.x, of.y, of.z, __uint_as_float((uint32_t)cf));
+                const float4 r1 = make_float4(df.x, df.y, df.z, __uint_as_float(ff));
                 const float v[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
                 for (int t = 0; t < 16; t++) d[t] = __float_as_uint(v[t]);
                 d[16] = key | ((unsigned long long)why << 32);
@@ -3616,9 +3651,10 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
             kt_begin(s);
+            const uint64_t c0 = b / (uint64_t)F.ao_samples;  // the chunk's first call (the records' call base)
             hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
-                               e1 - b);
-            hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W);
+                               e1 - b, c0);
+            hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W, c0);
             kt_end(s, e1 - b);
             if ((e = hipGetLastError()) != hipSuccess) return e;
 #ifdef RT580_DIAGNOSTICS

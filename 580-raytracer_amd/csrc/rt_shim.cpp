@@ -626,6 +626,7 @@ DevWork dev_work() {
     w.far_cap = std::min(SL.far_cap, g.frame_fc);
     w.ao_cap = std::min(SL.ao_cap, g.frame_ac);
     w.ao_rays = w.ao_cap ? (float4*)SL.ao_rays.p : nullptr;
+    w.ao_hp = w.ao_cap ? (float4*)SL.ao_rays.p + w.ao_cap : nullptr;  // (the buffer holds 2 ao_cap + 4 float4)
     w.ao_late = w.ao_cap ? (uint32_t*)SL.ao_late.p : nullptr;
     w.ao_late_count = w.ao_cap ? (uint32_t*)SL.ao_late_count.p : nullptr;
     w.ao_state_cap = w.ao_cap ? w.ao_cap / 16 : 0u;
@@ -721,7 +722,9 @@ int ensure_work(const rt_render_params* p, int n_rows) {
     g.frame_ac = g.bvh_ok ? ac : 0;
     g.frame_fc = 0;
     if (g.bvh_ok && SL.ao_cap < ac) {  // ray records of the split AO pass (ao_trace_kernel)
-        if (ensure(SL.ao_rays, (size_t)ac * 32) || ensure(SL.ao_late, (size_t)ac * 4) || ensure(SL.ao_late_count, 64) ||
+        // 16-byte records, then one hit point per call (<= ac + 2 calls per chunk)
+        if (ensure(SL.ao_rays, (size_t)ac * 32 + 64) || ensure(SL.ao_late, (size_t)ac * 4) ||
+            ensure(SL.ao_late_count, 64) ||
             ensure(SL.ao_state, (size_t)(ac / 16) * kLateWords * 4))
             return RT_FAILURE;
         SL.ao_cap = ac;
