@@ -211,6 +211,9 @@ hipError_t launch_gamma_u8_wide(const int16_t* fb, uint64_t n, uint8_t* out, hip
 // places in a whole frame's body (a rank's rows straight into the shared host frame)
 hipError_t launch_gamma_rows_u8(const int16_t* fb, int n_rows, int width, int row0, int step, uint8_t* out,
                                 hipStream_t s);
+// one device read of host memory (a mapped host address) after this device's
+// writes into it: those writes are in host memory when it completes
+hipError_t launch_host_flush_read(const void* host_dev, uint32_t* sink, hipStream_t s);
 // mt19937 draws [lo, hi) of the serial stream into out[0, hi - lo): one
 // workgroup per checkpoint block k in [k0, k0 + nblk) (rt_mt.h: windows[j] =
 // W_{(k0 + j) kMtBlock}), each running the twist from its window.

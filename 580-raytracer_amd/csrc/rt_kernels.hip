@@ -3149,6 +3149,22 @@ hipError_t launch_gamma_rows_u8(const int16_t* fb, int n_rows, int width, int ro
     return hipGetLastError();
 }
 
+// One read of host memory from the device after this device's writes into it
+// (a rank's rows in the shared host frame): a read does not pass the earlier
+// posted writes of its requester on the host link, so when it completes every
+// byte those writes carried is in host memory -- whatever path the frame's
+// "done" signal later takes to the rank that reads the frame (the 4-byte
+// all-gather over xGMI). The value lands in a device word.
+__global__ void host_flush_read_kernel(const volatile uint32_t* p, uint32_t* sink) {
+    if (threadIdx.x == 0) sink[0] = p[0];
+}
+
+hipError_t launch_host_flush_read(const void* host_dev, uint32_t* sink, hipStream_t s) {
+    hipLaunchKernelGGL(host_flush_read_kernel, dim3(1), dim3(64), 0, s,
+                       (const volatile uint32_t*)((uintptr_t)host_dev & ~(uintptr_t)3), sink);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- math self-test
 // The device-only fast sequences against the plain operations they replace:
 //  [0] rt_sqrt_nr vs sqrtf over EVERY float in [2^-96, +inf] and +0

@@ -2640,13 +2640,22 @@ int rank_frame(const rt_render_params* p, uint8_t* ppm_host) {
         HostRange* hr = host_range_ready(ppm_host, body);
         if (!hr) return fail("rt_gpu_render_rank_async: the shared frame's buffer is not registered");
         HIP_TRY(hipStreamWaitEvent(fs(), hr->copied, 0));
-        if (uint8_t* dst = (uint8_t*)mapped(hr, ppm_host)) {
+        uint8_t* dst = (uint8_t*)mapped(hr, ppm_host);
+        if (dst) {
             HIP_TRY(launch_gamma_rows_u8((const int16_t*)SL.fb.p, n_rows, W, rank, n, dst, fs()));
         } else {  // (not device-mapped: the rows' bytes on the device, one strided copy)
             HIP_TRY(launch_gamma_u8((const int16_t*)SL.fb.p, nv, (uint8_t*)g_rank.t8[r].p, fs()));
             if (n_rows)
                 HIP_TRY(hipMemcpy2DAsync(ppm_host + (size_t)rank * W * 3, (size_t)n * W * 3, g_rank.t8[r].p,
                                          (size_t)W * 3, (size_t)W * 3, (size_t)n_rows, hipMemcpyDeviceToHost, fs()));
+        }
+        // other ranks read these rows once the frame's 4-byte all-gather is done:
+        // the rows must be in host memory before this rank's part of it is sent
+        // (a rehearsed rank pays for the read too)
+        if (n > 1 && n_rows && hr->dev) {
+            const size_t last = ((size_t)rank + (size_t)(n_rows - 1) * n) * W * 3;
+            HIP_TRY(launch_host_flush_read((const char*)hr->dev + ((const char*)ppm_host - hr->p) + last,
+                                           (uint32_t*)g_rank.bar[r].p + rank, fs()));
         }
         HIP_TRY(hipEventRecord(hr->copied, fs()));
     } else {
