@@ -3670,7 +3670,10 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             const uint64_t c0 = b / (uint64_t)F.ao_samples;  // the chunk's first call (the records' call base)
             hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
                                e1 - b, c0);
-            hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(4096), dim3(TB), 0, s, S, W, c0);
+            // 12288 workgroups (~2 late rays per lane): late pass per 4 north-star
+            // frames 1536 / 3072 / 4096 / 12288 / 24576 / 49152 workgroups:
+            // 11.93 / 11.49 / 11.15-11.24 / 10.47-10.55 / 11.04 / 10.82 ms
+            hipLaunchKernelGGL((ao_late_kernel<6, 16>), dim3(12288), dim3(TB), 0, s, S, W, c0);
             kt_end(s, e1 - b);
             if ((e = hipGetLastError()) != hipSuccess) return e;
 #ifdef RT580_DIAGNOSTICS
