@@ -3668,7 +3668,11 @@ hipError_t launch_ao(const DevScene& S, const DevFrame& F, const DevWork& W, hip
             if ((e = hipMemsetAsync(W.ao_late_count, 0, 8, s)) != hipSuccess) return e;
             kt_begin(s);
             const uint64_t c0 = b / (uint64_t)F.ao_samples;  // the chunk's first call (the records' call base)
-            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 16384)), dim3(TB), 0, s, S, W,
+            // up to 65536 workgroups: one 2048-sample block each for a full 2^27 chunk
+            // (AO trace per 4 north-star frames, cap 4608 / 8192 / 16384 / 32768 /
+            // 65536 / 131072: 92.4 / 90.8 / 89.7-89.8 / 88.1 / 88.0-88.2 / 88.0 ms;
+            // Cornell 165.3 -> 164.6 ms at 65536)
+            hipLaunchKernelGGL((ao_trace_kernel<6, 16, 8, 4, 4>), dim3(grid_for(e1 - b, 65536)), dim3(TB), 0, s, S, W,
                                e1 - b, c0);
             // 12288 workgroups (~2 late rays per lane): late pass per 4 north-star
             // frames 1536 / 3072 / 4096 / 12288 / 24576 / 49152 workgroups:
